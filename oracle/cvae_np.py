@@ -1,0 +1,148 @@
+"""Analytic (hand-derived) forward/backward/Adam of the CVAE step in numpy — TEST INFRASTRUCTURE.
+
+The HIP kernels implement the backward pass analytically (no autograd), so this
+module restates exactly those formulas on the CPU and is checked against the
+autograd goldens of the reference (``tests/test_oracle_golden.py``).  It also
+serves as a float64 yardstick when calibrating the bf16 tolerances.
+
+Formulas (reference lines cited per function):
+  loss      Training_VAE.py:240-267
+  dL/dr     = w_r·2(r−x)/(B·S·D)
+              + [s=0, d∈{1,2}] w_s·2(r−x)/(2B)
+              + [s=0, d=0]     w_t·2r/B
+              + [d=0] w_t/(B(S−1)) · ([r_s > r_{s+1}] − [r_{s−1} > r_s])   (ReLU'(0)=0)
+  dL/dmu    = w_k·mu/(B·Z) + dz
+  dL/dlv    = w_k·½(e^lv − 1)/(B·Z) + dz·eps·½·e^{lv/2}
+  Linear    dX = G·W,  dW = Gᵀ·X,  db = Σ_b G;  h_c collects two consumers
+  Adam      torch/optim/adam.py ``_single_tensor_adam`` op order (lerp, mul+addcmul,
+            sqrt/bias-correction, addcdiv)
+"""
+from __future__ import annotations
+
+import numpy as np
+
+KEYS_ORDER = None  # filled by param_keys()
+
+
+def param_keys(n_enc=4, n_dec=4):
+    """state_dict order of Training_VAE.py:132-167 (24 keys at 4+4)."""
+    ks = ["condition_encoder.0", "condition_encoder.2"]
+    ks += [f"encoder.{2 * i + 1}" for i in range(n_enc)]
+    ks += ["fc_mu", "fc_logvar"]
+    ks += [f"decoder.{2 * i}" for i in range(n_dec)]
+    out = []
+    for k in ks:
+        out += [k + ".weight", k + ".bias"]
+    return out
+
+
+def _lin(x, p, name):
+    return x @ p[name + ".weight"].T + p[name + ".bias"]
+
+
+def forward(p, x, eps, n_enc=4, n_dec=4, dt=np.float32):
+    """x: (B,S,D) absolute trajectories.  Returns (recon, mu, logvar, h_c, cache)."""
+    p = {k: v.astype(dt) for k, v in p.items()}
+    x = x.astype(dt)
+    B, S, D = x.shape
+    start = x[:, 0, 1:3].copy()
+    rel = x.copy()
+    rel[:, :, 1:3] -= start[:, None, :]
+    c = {"start": start, "rel": rel, "eps": eps.astype(dt)}
+    a = rel.reshape(B, S * D)
+    c["enc_in"] = [a]
+    for i in range(n_enc):
+        a = np.maximum(_lin(a, p, f"encoder.{2 * i + 1}"), 0)
+        c["enc_in"].append(a)
+    h1 = np.maximum(_lin(start, p, "condition_encoder.0"), 0)
+    hc = np.maximum(_lin(h1, p, "condition_encoder.2"), 0)
+    c["hc1"], c["hc"] = h1, hc
+    h = np.concatenate([a, hc], 1)
+    c["h"] = h
+    mu, lv = _lin(h, p, "fc_mu"), _lin(h, p, "fc_logvar")
+    std = np.exp(dt(0.5) * lv)
+    z = mu + c["eps"] * std
+    c["std"] = std
+    d = np.concatenate([z, hc], 1)
+    c["dec_in"] = [d]
+    for i in range(n_dec - 1):
+        d = np.maximum(_lin(d, p, f"decoder.{2 * i}"), 0)
+        c["dec_in"].append(d)
+    r = _lin(d, p, f"decoder.{2 * (n_dec - 1)}").reshape(B, S, D)
+    return r, mu, lv, hc, c
+
+
+def losses(r, x_rel, mu, lv, w=(0.1, 0.1, 1.0, 1.0)):
+    B, S, D = r.shape
+    rec = np.mean((r - x_rel) ** 2)
+    kld = -0.5 * np.mean(1 + lv - mu ** 2 - np.exp(lv))
+    st = np.mean((r[:, 0, 1:3] - x_rel[:, 0, 1:3]) ** 2)
+    tl = np.mean(r[:, 0, 0] ** 2) + np.mean(np.maximum(r[:, :-1, 0] - r[:, 1:, 0], 0))
+    tot = w[0] * rec + w[1] * kld + w[2] * st + w[3] * tl
+    return np.array([tot, rec, kld, st, tl])
+
+
+def dloss_drecon(r, x_rel, w=(0.1, 0.1, 1.0, 1.0), B_norm=None):
+    B, S, D = r.shape
+    Bn = B if B_norm is None else B_norm
+    g = w[0] * 2 * (r - x_rel) / (Bn * S * D)
+    g[:, 0, 1:3] += w[2] * 2 * (r[:, 0, 1:3] - x_rel[:, 0, 1:3]) / (2 * Bn)
+    g[:, 0, 0] += w[3] * 2 * r[:, 0, 0] / Bn
+    m = (r[:, :-1, 0] > r[:, 1:, 0]).astype(r.dtype) * (w[3] / (Bn * (S - 1)))
+    g[:, :-1, 0] += m
+    g[:, 1:, 0] -= m
+    return g
+
+
+def backward(p, c, r, mu, lv, w=(0.1, 0.1, 1.0, 1.0), n_enc=4, n_dec=4, dt=np.float32):
+    """Gradients of the total loss w.r.t. every parameter (dict keyed like state_dict)."""
+    p = {k: v.astype(dt) for k, v in p.items()}
+    B, S, D = r.shape
+    Z = mu.shape[1]
+    g = {}
+    G = dloss_drecon(r, c["rel"], w).reshape(B, S * D)
+    for i in reversed(range(n_dec)):
+        name = f"decoder.{2 * i}"
+        X = c["dec_in"][i]
+        g[name + ".weight"] = G.T @ X
+        g[name + ".bias"] = G.sum(0)
+        dX = G @ p[name + ".weight"]
+        if i > 0:
+            G = dX * (c["dec_in"][i] > 0)
+    dz, dhc2 = dX[:, :Z], dX[:, Z:]
+    dmu = w[1] * mu / (B * Z) + dz
+    dlv = w[1] * 0.5 * (np.exp(lv) - 1) / (B * Z) + dz * c["eps"] * 0.5 * c["std"]
+    h = c["h"]
+    g["fc_mu.weight"], g["fc_mu.bias"] = dmu.T @ h, dmu.sum(0)
+    g["fc_logvar.weight"], g["fc_logvar.bias"] = dlv.T @ h, dlv.sum(0)
+    dh = dmu @ p["fc_mu.weight"] + dlv @ p["fc_logvar.weight"]
+    H = c["hc"].shape[1]
+    G = dh[:, :H] * (c["enc_in"][n_enc] > 0)
+    for i in reversed(range(n_enc)):
+        name = f"encoder.{2 * i + 1}"
+        X = c["enc_in"][i]
+        g[name + ".weight"] = G.T @ X
+        g[name + ".bias"] = G.sum(0)
+        if i > 0:
+            G = (G @ p[name + ".weight"]) * (c["enc_in"][i] > 0)
+    Gc = (dh[:, H:] + dhc2) * (c["hc"] > 0)
+    g["condition_encoder.2.weight"], g["condition_encoder.2.bias"] = Gc.T @ c["hc1"], Gc.sum(0)
+    Gc1 = (Gc @ p["condition_encoder.2.weight"]) * (c["hc1"] > 0)
+    g["condition_encoder.0.weight"], g["condition_encoder.0.bias"] = Gc1.T @ c["start"], Gc1.sum(0)
+    return g
+
+
+def adam(p, g, m, v, step, lr=1e-3, b1=0.9, b2=0.999, eps=1e-8):
+    """torch ``_single_tensor_adam`` (amsgrad=False, wd=0) on float32 arrays, in place."""
+    f = np.float32
+    bc1 = 1 - b1 ** step
+    bc2 = 1 - b2 ** step
+    step_size = f(lr / bc1)
+    bc2s = f(bc2 ** 0.5)
+    for k in p:
+        gg = g[k].astype(f)
+        m[k] = (m[k] + f(1 - b1) * (gg - m[k])).astype(f)           # lerp, weight < 0.5 branch
+        v[k] = (v[k] * f(b2) + f(1 - b2) * gg * gg).astype(f)
+        denom = (np.sqrt(v[k]) / bc2s + f(eps)).astype(f)
+        p[k] = (p[k] + (-step_size) * m[k] / denom).astype(f)
+    return p, m, v
