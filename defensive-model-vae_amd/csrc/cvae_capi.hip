@@ -1,0 +1,521 @@
+// cvae_capi.hip — host side of the C-ABI (include/cvae.h): planning, workspace,
+// launches.  All launches go to the caller's stream; nothing here synchronises.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/cvae.h"
+#include "cvae_device.h"
+#include "cvae_rowchain.h"
+#include "cvae_wgrad.h"
+#include "cvae_loss.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCK(call)                                                                          \
+  do {                                                                                       \
+    hipError_t e_ = (call);                                                                  \
+    if (e_ != hipSuccess)                                                                    \
+      return fail(CVAE_E_HIP, std::string(#call) + " failed: " + hipGetErrorString(e_));      \
+  } while (0)
+
+struct ParamInfo {
+  int64_t offset, numel;
+  int rows, cols;
+};
+
+}  // namespace
+
+struct cvae_handle {
+  cvae_config cfg{};
+  int device = 0;
+  int R = 32;               // rows per row-chain workgroup
+  int tsize = 2;
+  NetDev net{};
+  std::vector<ParamInfo> params;
+  int64_t nparams = 0;
+  std::vector<TileDesc> tiles;
+  TileDesc* d_tiles = nullptr;
+  char* arena = nullptr;    // weight copies + activations
+  int64_t arena_bytes = 0;
+  float* d_partials = nullptr;
+  int max_row_tiles = 0;
+  int lds_bytes = 0;
+  bool timing = false;
+  // timing: per call, a chain of events on the caller's stream; segment i of a
+  // call spans ev[i] → ev[i+1] and is named by the kernel launched after ev[i]
+  std::vector<hipEvent_t> pool;
+  int n_used = 0;
+  struct Seg { int e0, e1; std::string name; };
+  std::vector<Seg> segs;
+  int call_last = -1;
+};
+
+namespace {
+
+int rup_i(int v, int a) { return (v + a - 1) / a * a; }
+
+int build_plan(cvae_handle* h) {
+  const cvae_config& c = h->cfg;
+  NetDev& n = h->net;
+  n.S = c.seq_len; n.D = c.dim; n.Z = c.latent_dim; n.H = c.hidden_dim;
+  n.I = c.seq_len * c.dim;
+  n.n_enc = c.n_enc; n.n_dec = c.n_dec;
+  n.n_layers = 2 + c.n_enc + 1 + c.n_dec;
+  n.Ip = rup_i(n.I, 32); n.Hp = rup_i(n.H, 32); n.Hcp = rup_i(2 * n.H, 32);
+  n.ZHp = rup_i(n.Z + n.H, 32); n.Zp2 = rup_i(2 * n.Z, 32); n.Cp = 32;
+  n.dtype = c.dtype;
+  h->tsize = c.dtype == CVAE_BF16 ? 2 : 4;
+  h->R = c.dtype == CVAE_BF16 ? 32 : 16;
+  // arena rows: whole row tiles, and a multiple of the K chunk of the wgrad GEMM
+  n.Bp = rup_i(c.max_batch, 32);
+  h->max_row_tiles = (c.max_batch + h->R - 1) / h->R;
+
+  // layer table (in = K, out = N) in state_dict order
+  struct LD { int K, N, relu; };
+  std::vector<LD> ld;
+  ld.push_back({2, n.H, 1});
+  ld.push_back({n.H, n.H, 1});
+  for (int i = 0; i < n.n_enc; ++i) ld.push_back({i == 0 ? n.I : n.H, n.H, 1});
+  ld.push_back({2 * n.H, 2 * n.Z, 0});
+  for (int i = 0; i < n.n_dec; ++i) {
+    const bool last = i == n.n_dec - 1;
+    ld.push_back({i == 0 ? n.Z + n.H : n.H, last ? n.I : n.H, last ? 0 : 1});
+  }
+  if ((int)ld.size() > CVAE_MAX_LAYERS) return fail(CVAE_E_INVALID, "too many layers");
+
+  // flat parameter table (state_dict order; fc splits into fc_mu / fc_logvar)
+  h->params.clear();
+  int64_t off = 0;
+  auto add = [&](int rows, int cols) {
+    ParamInfo p{off, (int64_t)rows * (cols > 0 ? cols : 1), rows, cols};
+    h->params.push_back(p);
+    off += p.numel;
+    return p.offset;
+  };
+  for (int l = 0; l < (int)ld.size(); ++l) {
+    LayerDev& L = n.L[l];
+    L.K = ld[l].K; L.N = ld[l].N; L.Kp = rup_i(L.K, 32); L.Np = rup_i(L.N, 32); L.relu = ld[l].relu;
+    if (l == lFC(n)) {
+      L.nseg = 2; L.seg_rows0 = n.Z;
+      L.pw[0] = add(n.Z, L.K); L.pb[0] = add(n.Z, 0);
+      L.pw[1] = add(n.Z, L.K); L.pb[1] = add(n.Z, 0);
+    } else {
+      L.nseg = 1; L.seg_rows0 = L.N;
+      L.pw[0] = add(L.N, L.K); L.pb[0] = add(L.N, 0);
+      L.pw[1] = L.pw[0]; L.pb[1] = L.pb[0];
+    }
+  }
+  h->nparams = off;
+
+  // LDS budget of the row-chain kernel
+  const LdsPlan lp = lds_plan(n, h->R, h->tsize);
+  h->lds_bytes = lp.total;
+  if (lp.total > 160 * 1024)
+    return fail(CVAE_E_INVALID, "configuration needs " + std::to_string(lp.total) +
+                                    " B of LDS per row tile (> 160 KiB); reduce seq_len*dim or latent_dim");
+  if (c.dim < 3) return fail(CVAE_E_INVALID, "dim must be >= 3 (channel 0 = time, 1:3 = x,y)");
+
+  // weight-gradient / parameter tiles: 32×32 over each layer's padded (Np × Kp)
+  h->tiles.clear();
+  for (int l = 0; l < n.n_layers; ++l)
+    for (int o = 0; o < n.L[l].Np; o += 32)
+      for (int i = 0; i < n.L[l].Kp; i += 32) h->tiles.push_back({l, o, i, 0});
+  return CVAE_OK;
+}
+
+int alloc_arena(cvae_handle* h) {
+  NetDev& n = h->net;
+  const int ts = h->tsize;
+  std::vector<int64_t> offs;
+  int64_t total = 0;
+  auto take = [&](int64_t bytes) { int64_t o = total; total += (bytes + 255) / 256 * 256; return o; };
+  struct Off { int64_t wf, wb, bias, xT, gT; };
+  std::vector<Off> lo(n.n_layers);
+  for (int l = 0; l < n.n_layers; ++l) {
+    LayerDev& L = n.L[l];
+    lo[l].wf = take((int64_t)L.Np * L.Kp * ts);
+    lo[l].wb = take((int64_t)L.Kp * L.Np * ts);
+    lo[l].bias = take((int64_t)L.Np * 4);
+  }
+  // activations: every layer has its own xT and gT (inputs that are concatenations
+  // are written by their producers at column offsets)
+  for (int l = 0; l < n.n_layers; ++l) {
+    LayerDev& L = n.L[l];
+    lo[l].xT = take((int64_t)L.Kp * n.Bp * ts);
+    lo[l].gT = take((int64_t)L.Np * n.Bp * ts);
+  }
+  const int64_t part_off = take((int64_t)h->max_row_tiles * 8 * 4);
+  const int64_t tile_off = take((int64_t)h->tiles.size() * sizeof(TileDesc));
+  HIPCK(hipMalloc(&h->arena, total));
+  HIPCK(hipMemset(h->arena, 0, total));
+  h->arena_bytes = total;
+  for (int l = 0; l < n.n_layers; ++l) {
+    LayerDev& L = n.L[l];
+    L.Wf = h->arena + lo[l].wf;
+    L.Wb = h->arena + lo[l].wb;
+    L.bias = (float*)(h->arena + lo[l].bias);
+    L.xT = h->arena + lo[l].xT;
+    L.gT = h->arena + lo[l].gT;
+  }
+  h->d_partials = (float*)(h->arena + part_off);
+  h->d_tiles = (TileDesc*)(h->arena + tile_off);
+  HIPCK(hipMemcpy(h->d_tiles, h->tiles.data(), h->tiles.size() * sizeof(TileDesc), hipMemcpyHostToDevice));
+  return CVAE_OK;
+}
+
+template <typename T>
+int set_lds_attrs(cvae_handle* h) {
+  constexpr int R = sizeof(T) == 2 ? 32 : 16;
+  HIPCK(hipFuncSetAttribute((const void*)rowchain_kernel<T, R, RC_TRAIN>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, h->lds_bytes));
+  HIPCK(hipFuncSetAttribute((const void*)rowchain_kernel<T, R, RC_FWD>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, h->lds_bytes));
+  HIPCK(hipFuncSetAttribute((const void*)rowchain_kernel<T, R, RC_DECODE>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, h->lds_bytes));
+  return CVAE_OK;
+}
+
+// ---- timing helpers (events on the caller's stream; no syncs)
+void tbegin(cvae_handle* h) { h->call_last = -1; }
+int tmark(cvae_handle* h, hipStream_t s, const char* name) {
+  if (!h->timing) return CVAE_OK;
+  if (h->n_used >= (int)h->pool.size()) {
+    hipEvent_t e;
+    HIPCK(hipEventCreate(&e));
+    h->pool.push_back(e);
+  }
+  const int id = h->n_used++;
+  HIPCK(hipEventRecord(h->pool[id], s));
+  if (h->call_last >= 0) h->segs.back().e1 = id;
+  if (std::strcmp(name, "end") != 0) {
+    h->segs.push_back({id, -1, name});
+    h->call_last = id;
+  } else {
+    h->call_last = -1;
+  }
+  return CVAE_OK;
+}
+
+template <typename T, int MODE>
+int launch_rowchain(cvae_handle* h, const RowArgs& a, hipStream_t s) {
+  constexpr int R = sizeof(T) == 2 ? 32 : 16;
+  const int grid = (a.batch + R - 1) / R;
+  hipLaunchKernelGGL((rowchain_kernel<T, R, MODE>), dim3(grid), dim3(CVAE_THREADS), h->lds_bytes, s, h->net, a);
+  HIPCK(hipGetLastError());
+  return CVAE_OK;
+}
+
+int check_batch(cvae_handle* h, int batch) {
+  if (batch <= 0) return fail(CVAE_E_INVALID, "batch must be > 0");
+  if (batch > h->cfg.max_batch)
+    return fail(CVAE_E_CAPACITY, "batch " + std::to_string(batch) + " > max_batch " + std::to_string(h->cfg.max_batch));
+  return CVAE_OK;
+}
+
+AdamArgs make_adam(float* params, float* grads, float* m, float* v, int step, float lr, float b1, float b2,
+                   float eps, float grad_scale) {
+  AdamArgs a{};
+  a.params = params; a.grads = grads; a.m = m; a.v = v;
+  a.grad_scale = grad_scale;
+  // torch computes these python scalars in double, then the CPU kernels see them as float
+  const double bc1 = 1.0 - std::pow((double)b1, (double)step);
+  const double bc2 = 1.0 - std::pow((double)b2, (double)step);
+  a.lr_neg_step = (float)(-((double)lr / bc1));
+  a.bc2_sqrt = (float)std::sqrt(bc2);
+  a.beta1_w = (float)(1.0 - (double)b1);
+  a.beta2 = b2;
+  a.one_m_beta2 = (float)(1.0 - (double)b2);
+  a.eps = eps;
+  return a;
+}
+
+template <typename T>
+int train_fwd_bwd_impl(cvae_handle* h, const void* x, const int64_t* idx, int batch, const float* eps,
+                       uint64_t seed, uint64_t offset, const cvae_loss_weights* w, hipStream_t s,
+                       RowArgs& ra) {
+  ra = RowArgs{};
+  ra.x = x; ra.idx = idx; ra.batch = batch; ra.eps = eps; ra.seed = seed; ra.offset = offset;
+  ra.w_recon = w ? w->recon : 0.1f; ra.w_kld = w ? w->kld : 0.1f;
+  ra.w_start = w ? w->start : 1.0f; ra.w_time = w ? w->time : 1.0f;
+  ra.partials = h->d_partials;
+  int rc = tmark(h, s, "rowchain");
+  if (rc) return rc;
+  return launch_rowchain<T, RC_TRAIN>(h, ra, s);
+}
+
+LossArgs make_loss(cvae_handle* h, const RowArgs& ra, float* loss_out, float* loss_accum) {
+  LossArgs la{};
+  la.partials = h->d_partials;
+  la.ntiles = (ra.batch + h->R - 1) / h->R;
+  la.batch = ra.batch;
+  la.w_recon = ra.w_recon; la.w_kld = ra.w_kld; la.w_start = ra.w_start; la.w_time = ra.w_time;
+  la.loss_out = loss_out; la.loss_accum = loss_accum;
+  return la;
+}
+
+int bk_of(cvae_handle* h, int batch) { return (batch + h->R - 1) / h->R * h->R; }
+
+}  // namespace
+
+extern "C" {
+
+const char* cvae_last_error(void) { return g_err.c_str(); }
+int cvae_abi_version(void) { return CVAE_ABI_VERSION; }
+
+int cvae_create(const cvae_config* cfg, int device, cvae_handle** out) {
+  if (!cfg || !out) return fail(CVAE_E_INVALID, "null argument");
+  if (cfg->seq_len < 1 || cfg->dim < 1 || cfg->latent_dim < 1 || cfg->hidden_dim < 1 || cfg->n_enc < 1 ||
+      cfg->n_dec < 1 || cfg->max_batch < 1 || (cfg->dtype != CVAE_F32 && cfg->dtype != CVAE_BF16))
+    return fail(CVAE_E_INVALID, "invalid cvae_config");
+  cvae_handle* h = new cvae_handle();
+  h->cfg = *cfg;
+  h->device = device;
+  int rc = build_plan(h);
+  if (rc) { delete h; return rc; }
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) { delete h; return fail(CVAE_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e)); }
+  rc = alloc_arena(h);
+  if (!rc) rc = h->cfg.dtype == CVAE_BF16 ? set_lds_attrs<__bf16>(h) : set_lds_attrs<float>(h);
+  if (rc) { cvae_destroy(h); return rc; }
+  *out = h;
+  return CVAE_OK;
+}
+
+int cvae_destroy(cvae_handle* h) {
+  if (!h) return CVAE_OK;
+  for (auto e : h->pool) (void)hipEventDestroy(e);
+  if (h->arena) (void)hipFree(h->arena);
+  delete h;
+  return CVAE_OK;
+}
+
+int cvae_num_params(const cvae_handle* h, int64_t* total, int* n_tensors) {
+  if (!h) return fail(CVAE_E_INVALID, "null handle");
+  if (total) *total = h->nparams;
+  if (n_tensors) *n_tensors = (int)h->params.size();
+  return CVAE_OK;
+}
+
+int cvae_param_info(const cvae_handle* h, int i, int64_t* offset, int64_t* numel, int* rows, int* cols) {
+  if (!h || i < 0 || i >= (int)h->params.size()) return fail(CVAE_E_INVALID, "bad param index");
+  const ParamInfo& p = h->params[i];
+  if (offset) *offset = p.offset;
+  if (numel) *numel = p.numel;
+  if (rows) *rows = p.rows;
+  if (cols) *cols = p.cols;
+  return CVAE_OK;
+}
+
+int cvae_config_info(const cvae_config* cfg, int64_t* total_params, int* n_tensors, int* lds_bytes) {
+  if (!cfg) return fail(CVAE_E_INVALID, "null argument");
+  cvae_handle tmp;
+  tmp.cfg = *cfg;
+  const int rc = build_plan(&tmp);
+  if (total_params) *total_params = tmp.nparams;
+  if (n_tensors) *n_tensors = (int)tmp.params.size();
+  if (lds_bytes) *lds_bytes = tmp.lds_bytes;
+  return rc;
+}
+
+int cvae_workspace_bytes(const cvae_handle* h, int64_t* bytes) {
+  if (!h || !bytes) return fail(CVAE_E_INVALID, "null argument");
+  *bytes = h->arena_bytes;
+  return CVAE_OK;
+}
+
+int cvae_pack_weights(cvae_handle* h, const float* params, void* stream) {
+  if (!h || !params) return fail(CVAE_E_INVALID, "null argument");
+  hipStream_t s = (hipStream_t)stream;
+  AdamArgs aa{};
+  aa.params = (float*)params;
+  const int nt = (int)h->tiles.size();
+  if (h->cfg.dtype == CVAE_BF16)
+    hipLaunchKernelGGL((param_kernel<__bf16, PM_PACK>), dim3(nt), dim3(CVAE_THREADS), 0, s, h->net, h->d_tiles, aa);
+  else
+    hipLaunchKernelGGL((param_kernel<float, PM_PACK>), dim3(nt), dim3(CVAE_THREADS), 0, s, h->net, h->d_tiles, aa);
+  HIPCK(hipGetLastError());
+  return CVAE_OK;
+}
+
+int cvae_forward(cvae_handle* h, const void* x, const int64_t* idx, int batch, const float* start, const float* eps,
+                 uint64_t seed, uint64_t offset, float* recon, float* mu, float* logvar, float* hc, void* stream) {
+  if (!h || !x) return fail(CVAE_E_INVALID, "null argument");
+  int rc = check_batch(h, batch);
+  if (rc) return rc;
+  RowArgs a{};
+  a.x = x; a.idx = idx; a.batch = batch; a.eps = eps; a.seed = seed; a.offset = offset;
+  a.start_in = start; a.x_relative = start ? 1 : 0;
+  a.recon_out = recon; a.mu_out = mu; a.lv_out = logvar; a.hc_out = hc;
+  a.partials = h->d_partials;
+  hipStream_t s = (hipStream_t)stream;
+  return h->cfg.dtype == CVAE_BF16 ? launch_rowchain<__bf16, RC_FWD>(h, a, s) : launch_rowchain<float, RC_FWD>(h, a, s);
+}
+
+int cvae_condition(cvae_handle* h, const float* start, int batch, float* hc, void* stream) {
+  if (!h || !start || !hc) return fail(CVAE_E_INVALID, "null argument");
+  int rc = check_batch(h, batch);
+  if (rc) return rc;
+  RowArgs a{};
+  a.batch = batch; a.start_in = start; a.hc_out = hc;
+  a.partials = h->d_partials;
+  hipStream_t s = (hipStream_t)stream;
+  return h->cfg.dtype == CVAE_BF16 ? launch_rowchain<__bf16, RC_DECODE>(h, a, s)
+                                   : launch_rowchain<float, RC_DECODE>(h, a, s);
+}
+
+int cvae_decode(cvae_handle* h, const float* z, const float* start, const float* hc, int batch, float* out,
+                void* stream) {
+  if (!h || !z || !out || (!start && !hc)) return fail(CVAE_E_INVALID, "null argument");
+  int rc = check_batch(h, batch);
+  if (rc) return rc;
+  RowArgs a{};
+  a.batch = batch; a.z_in = z; a.start_in = start; a.hc_in = hc; a.recon_out = out;
+  a.partials = h->d_partials;
+  hipStream_t s = (hipStream_t)stream;
+  return h->cfg.dtype == CVAE_BF16 ? launch_rowchain<__bf16, RC_DECODE>(h, a, s)
+                                   : launch_rowchain<float, RC_DECODE>(h, a, s);
+}
+
+int cvae_train_fwd_bwd(cvae_handle* h, const void* x, const int64_t* idx, int batch, const float* eps,
+                       uint64_t seed, uint64_t offset, const cvae_loss_weights* w, float* grads,
+                       float* loss_out, float* loss_accum, void* stream) {
+  if (!h || !x || !grads) return fail(CVAE_E_INVALID, "null argument");
+  int rc = check_batch(h, batch);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  tbegin(h);
+  RowArgs ra;
+  rc = h->cfg.dtype == CVAE_BF16 ? train_fwd_bwd_impl<__bf16>(h, x, idx, batch, eps, seed, offset, w, s, ra)
+                                 : train_fwd_bwd_impl<float>(h, x, idx, batch, eps, seed, offset, w, s, ra);
+  if (rc) return rc;
+  AdamArgs aa{};
+  aa.grads = grads;
+  const LossArgs la = make_loss(h, ra, loss_out, loss_accum);
+  const int nt = (int)h->tiles.size();
+  if ((rc = tmark(h, s, "wgrad"))) return rc;
+  if (h->cfg.dtype == CVAE_BF16)
+    hipLaunchKernelGGL((wgrad_kernel<__bf16, PM_GRAD>), dim3(nt), dim3(CVAE_THREADS), 0, s, h->net, h->d_tiles,
+                       bk_of(h, batch), aa, la);
+  else
+    hipLaunchKernelGGL((wgrad_kernel<float, PM_GRAD>), dim3(nt), dim3(CVAE_THREADS), 0, s, h->net, h->d_tiles,
+                       bk_of(h, batch), aa, la);
+  HIPCK(hipGetLastError());
+  return tmark(h, s, "end");
+}
+
+int cvae_adam(cvae_handle* h, float* params, const float* grads, float* m, float* v, int step, float lr,
+              float beta1, float beta2, float eps, float grad_scale, void* stream) {
+  if (!h || !params || !grads || !m || !v) return fail(CVAE_E_INVALID, "null argument");
+  if (step < 1) return fail(CVAE_E_INVALID, "step must be >= 1");
+  hipStream_t s = (hipStream_t)stream;
+  AdamArgs aa = make_adam(params, (float*)grads, m, v, step, lr, beta1, beta2, eps, grad_scale);
+  const int nt = (int)h->tiles.size();
+  int rc = tmark(h, s, "adam");
+  if (rc) return rc;
+  if (h->cfg.dtype == CVAE_BF16)
+    hipLaunchKernelGGL((param_kernel<__bf16, PM_ADAM>), dim3(nt), dim3(CVAE_THREADS), 0, s, h->net, h->d_tiles, aa);
+  else
+    hipLaunchKernelGGL((param_kernel<float, PM_ADAM>), dim3(nt), dim3(CVAE_THREADS), 0, s, h->net, h->d_tiles, aa);
+  HIPCK(hipGetLastError());
+  return tmark(h, s, "end");
+}
+
+int cvae_train_step(cvae_handle* h, const void* x, const int64_t* idx, int batch, const float* eps, uint64_t seed,
+                    uint64_t offset, const cvae_loss_weights* w, float* params, float* m, float* v, int step,
+                    float lr, float beta1, float beta2, float adam_eps, float* loss_out, float* loss_accum,
+                    void* stream) {
+  if (!h || !x || !params || !m || !v) return fail(CVAE_E_INVALID, "null argument");
+  if (step < 1) return fail(CVAE_E_INVALID, "step must be >= 1");
+  int rc = check_batch(h, batch);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  tbegin(h);
+  RowArgs ra;
+  rc = h->cfg.dtype == CVAE_BF16 ? train_fwd_bwd_impl<__bf16>(h, x, idx, batch, eps, seed, offset, w, s, ra)
+                                 : train_fwd_bwd_impl<float>(h, x, idx, batch, eps, seed, offset, w, s, ra);
+  if (rc) return rc;
+  AdamArgs aa = make_adam(params, nullptr, m, v, step, lr, beta1, beta2, adam_eps, 1.f);
+  const LossArgs la = make_loss(h, ra, loss_out, loss_accum);
+  const int nt = (int)h->tiles.size();
+  if ((rc = tmark(h, s, "wgrad_adam"))) return rc;
+  if (h->cfg.dtype == CVAE_BF16)
+    hipLaunchKernelGGL((wgrad_kernel<__bf16, PM_ADAM>), dim3(nt), dim3(CVAE_THREADS), 0, s, h->net, h->d_tiles,
+                       bk_of(h, batch), aa, la);
+  else
+    hipLaunchKernelGGL((wgrad_kernel<float, PM_ADAM>), dim3(nt), dim3(CVAE_THREADS), 0, s, h->net, h->d_tiles,
+                       bk_of(h, batch), aa, la);
+  HIPCK(hipGetLastError());
+  return tmark(h, s, "end");
+}
+
+int cvae_loss(const float* recon, const float* x, const float* mu, const float* logvar, int batch, int seq_len,
+              int dim, int latent_dim, const cvae_loss_weights* w, float* loss_out, float* workspace,
+              void* stream) {
+  if (!recon || !x || !mu || !logvar || !loss_out || !workspace || !w)
+    return fail(CVAE_E_INVALID, "null argument");
+  if (batch < 1 || seq_len < 1 || dim < 3 || latent_dim < 1) return fail(CVAE_E_INVALID, "bad shape");
+  hipStream_t s = (hipStream_t)stream;
+  const int nb = (batch + 31) / 32;
+  hipLaunchKernelGGL(loss_partial_kernel, dim3(nb), dim3(CVAE_THREADS), 0, s, recon, x, mu, logvar, batch, seq_len,
+                     dim, latent_dim, workspace);
+  HIPCK(hipGetLastError());
+  LossArgs la{};
+  la.partials = workspace; la.ntiles = nb; la.batch = batch;
+  la.w_recon = w->recon; la.w_kld = w->kld; la.w_start = w->start; la.w_time = w->time;
+  la.loss_out = loss_out;
+  hipLaunchKernelGGL(loss_finish_kernel, dim3(1), dim3(64), 0, s, la, seq_len, dim, latent_dim);
+  HIPCK(hipGetLastError());
+  return CVAE_OK;
+}
+
+int cvae_set_timing(cvae_handle* h, int enabled) {
+  if (!h) return fail(CVAE_E_INVALID, "null handle");
+  h->timing = enabled != 0;
+  h->segs.clear();
+  h->n_used = 0;
+  h->call_last = -1;
+  return CVAE_OK;
+}
+
+int cvae_kernel_times(cvae_handle* h, char* names, int names_len, float* ms, int max_n) {
+  if (!h) return fail(CVAE_E_INVALID, "null handle");
+  std::vector<std::string> keys;
+  std::vector<double> tot;
+  std::vector<int> cnt;
+  for (const auto& sg : h->segs) {
+    if (sg.e1 < 0) continue;
+    float t = 0.f;
+    HIPCK(hipEventElapsedTime(&t, h->pool[sg.e0], h->pool[sg.e1]));
+    size_t k = 0;
+    while (k < keys.size() && keys[k] != sg.name) ++k;
+    if (k == keys.size()) { keys.push_back(sg.name); tot.push_back(0.0); cnt.push_back(0); }
+    tot[k] += t;
+    cnt[k] += 1;
+  }
+  std::string all;
+  int n = 0;
+  for (size_t k = 0; k < keys.size() && n < max_n; ++k, ++n) {
+    if (ms) ms[n] = (float)(tot[k] / cnt[k]);
+    if (!all.empty()) all += ",";
+    all += keys[k] + ":" + std::to_string(cnt[k]);
+  }
+  if (names && names_len > 0) {
+    std::strncpy(names, all.c_str(), names_len - 1);
+    names[names_len - 1] = 0;
+  }
+  return n;
+}
+
+}  // extern "C"

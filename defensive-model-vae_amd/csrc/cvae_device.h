@@ -1,0 +1,130 @@
+// cvae_device.h — device-side data structures and CDNA4 building blocks for the
+// conditional trajectory VAE hot path (gfx950 only).
+//
+// Layout conventions:
+//  * Every Linear layer l has padded dims Kp = roundup(in, 32), Np = roundup(out, 32).
+//  * Device weight copies in the operand dtype T (fp32 or bf16):
+//      Wf[Np][Kp]  (= nn.Linear (out,in) zero-padded) — B operand of the forward GEMM
+//      Wb[Kp][Np]  (= Wᵀ zero-padded)                  — B operand of the dX GEMM
+//    plus a padded fp32 bias[Np].  The fp32 master parameters stay in the
+//    caller's flat state_dict-ordered buffer.
+//  * Activation arena, feature-major ("transposed") [features][Bp] in T:
+//      xT(l) = input of layer l, gT(l) = dL/d(pre-activation) of layer l.
+//    The weight-gradient kernel reduces over the batch with both operands
+//    batch-contiguous: dW_l = gT(l) · xT(l)ᵀ.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define CVAE_MAX_LAYERS 40
+#define CVAE_NW 4            // waves per workgroup
+#define CVAE_THREADS 256
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct LayerDev {
+  int K, N, Kp, Np;      // real / padded in-out dims
+  int relu;              // 1: ReLU after this layer
+  int nseg, seg_rows0;   // parameter segments along N (fc fuses mu‖logvar: 2 segments)
+  int pad_;
+  int64_t pw[2], pb[2];  // flat fp32 offsets of weight / bias of each segment
+  void* Wf;              // [Np][Kp] T
+  void* Wb;              // [Kp][Np] T
+  float* bias;           // [Np] fp32
+  void* xT;              // [Kp][Bp] T   input of the layer (feature-major)
+  void* gT;              // [Np][Bp] T   gradient w.r.t. pre-activation
+};
+
+struct NetDev {
+  int S, D, Z, H, I;
+  int n_enc, n_dec, n_layers;
+  int Ip, Hp, Hcp, ZHp, Zp2, Cp;
+  int Bp;                // arena row capacity
+  int dtype;             // 0 fp32, 1 bf16
+  LayerDev L[CVAE_MAX_LAYERS];
+};
+
+// layer indices: C0=0, C1=1, E0=2 .. E0+n_enc-1, FC, D0 .. D0+n_dec-1
+__host__ __device__ inline int lC0(const NetDev&) { return 0; }
+__host__ __device__ inline int lC1(const NetDev&) { return 1; }
+__host__ __device__ inline int lE(const NetDev&, int i) { return 2 + i; }
+__host__ __device__ inline int lFC(const NetDev& n) { return 2 + n.n_enc; }
+__host__ __device__ inline int lD(const NetDev& n, int i) { return 3 + n.n_enc + i; }
+
+struct TileDesc { int layer, o0, i0, pad_; };
+
+// ------------------------------------------------------------------ operand types
+template <typename T> struct Op;
+template <> struct Op<float> {
+  using V = f32x4;            // 16 B per lane = 4 fp32 along K
+  static constexpr int EPL = 4;
+  static constexpr int KC = 16;   // K covered by one 16-B fragment (4 MFMA 16x16x4)
+};
+template <> struct Op<__bf16> {
+  using V = bf16x8;           // 16 B per lane = 8 bf16 along K
+  static constexpr int EPL = 8;
+  static constexpr int KC = 32;   // one MFMA 16x16x32
+};
+
+// acc += A·B over one 16-B-per-lane K chunk.  Lane l holds A[l&15][kq..kq+EPL) and
+// B[kq..kq+EPL)[l&15], kq = EPL*(l>>4).  For fp32 the four 16x16x4 MFMAs take element j
+// of every lane, i.e. a permuted but identical K order on both operands.
+__device__ __forceinline__ f32x4 mfma_chunk(f32x4 a, f32x4 b, f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b[2], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b[3], c, 0, 0, 0);
+  return c;
+}
+__device__ __forceinline__ f32x4 mfma_chunk(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+template <typename T> __device__ __forceinline__ T to_t(float v);
+template <> __device__ __forceinline__ float to_t<float>(float v) { return v; }
+template <> __device__ __forceinline__ __bf16 to_t<__bf16>(float v) { return (__bf16)v; }
+__device__ __forceinline__ float to_f(float v) { return v; }
+__device__ __forceinline__ float to_f(__bf16 v) { return (float)v; }
+
+// store 4 consecutive T values (8 B for bf16, 16 B for fp32)
+__device__ __forceinline__ void store4(float* p, f32x4 v) { *(f32x4*)p = v; }
+__device__ __forceinline__ void store4(__bf16* p, f32x4 v) {
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  bf16x4 h;
+  h[0] = (__bf16)v[0]; h[1] = (__bf16)v[1]; h[2] = (__bf16)v[2]; h[3] = (__bf16)v[3];
+  *(bf16x4*)p = h;
+}
+
+// ------------------------------------------------------------------ Philox4x32-10
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+    k.x += 0x9E3779B9u;
+    k.y += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// standard normal eps for (row b, latent j): Box-Muller on Philox(seed; b, j/4, offset)
+__device__ __forceinline__ float philox_normal(uint64_t seed, uint64_t offset, uint32_t b, uint32_t j) {
+  const uint4 r = philox4x32_10(make_uint4(b, j >> 2, (uint32_t)offset, (uint32_t)(offset >> 32)),
+                                make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+  const uint32_t u0 = (j & 2) ? r.z : r.x, u1 = (j & 2) ? r.w : r.y;
+  const float f0 = ((float)u0 + 1.0f) * 2.3283064365386963e-10f;  // (0,1]
+  const float f1 = (float)u1 * 2.3283064365386963e-10f;
+  const float rad = sqrtf(-2.0f * logf(f0));
+  float s, c;
+  sincosf(6.283185307179586f * f1, &s, &c);
+  return (j & 1) ? rad * s : rad * c;
+}
+
+// ------------------------------------------------------------------ wave reduction
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}

@@ -1,0 +1,173 @@
+/*
+ * cvae.h — C-ABI of the MI355X-native conditional trajectory VAE training path.
+ *
+ * This is the drop-in boundary for the reference's hot path
+ * (yslf2035/Defensive-Model-VAE, Training_VAE.py).  The reference has no FFI of
+ * its own (it is torch-CPU Python); each entry point below names the reference
+ * code it replaces.  Plain pointers and sizes only — no torch types: every
+ * device pointer is a HIP device allocation owned by the CALLER (torch tensors
+ * pass data_ptr()), every `stream` is a hipStream_t (torch's current stream).
+ * The library owns only its workspace (padded weight copies + activation
+ * arena), allocated in cvae_create and sized by cfg->max_batch.
+ *
+ * Errors: every function returns 0 on success or a negative CVAE_E* code; it
+ * never aborts.  cvae_last_error() returns a thread-local message.
+ * Threading: one handle per device per process; a handle is not thread-safe.
+ * No call synchronises the device: all work is queued on `stream`, so every
+ * call is capturable into a hipGraph.
+ */
+#ifndef CVAE_H
+#define CVAE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CVAE_ABI_VERSION 1
+
+enum cvae_dtype { CVAE_F32 = 0, CVAE_BF16 = 1 };
+
+enum cvae_status {
+  CVAE_OK = 0,
+  CVAE_E_INVALID = -1,   /* bad argument / unsupported configuration        */
+  CVAE_E_HIP = -2,       /* a HIP runtime call failed (message has details) */
+  CVAE_E_CAPACITY = -3,  /* batch larger than cfg.max_batch                  */
+  CVAE_E_NOMEM = -4
+};
+
+/* Model shape.  Training_VAE.py:124 ConditionalTrajectoryVAE(seq_len, dim,
+ * latent_dim, hidden_dim=128); n_enc/n_dec are 4/4 in the reference
+ * (:141-167) and may be raised for the wide config. */
+typedef struct cvae_config {
+  int seq_len;     /* S */
+  int dim;         /* D (channel 0 = time, 1:3 = x,y; Training_VAE.py:250-262) */
+  int latent_dim;  /* Z */
+  int hidden_dim;  /* H */
+  int n_enc;       /* Linear layers in `encoder`  (reference: 4) */
+  int n_dec;       /* Linear layers in `decoder`  (reference: 4) */
+  int dtype;       /* cvae_dtype: GEMM operand / activation type; master weights, Adam and loss are fp32 */
+  int max_batch;   /* rows per call the workspace is sized for */
+} cvae_config;
+
+typedef struct cvae_handle cvae_handle;
+
+/* Loss weights in the reference's order (Training_VAE.py:229, call site :356-359). */
+typedef struct cvae_loss_weights {
+  float recon, kld, start, time;
+} cvae_loss_weights;
+
+/* Create/destroy.  Replaces ConditionalTrajectoryVAE.__init__ (Training_VAE.py:124-167)
+ * for the device side; parameters themselves live in the caller's flat fp32 buffer. */
+int cvae_create(const cvae_config* cfg, int device, cvae_handle** out);
+int cvae_destroy(cvae_handle* h);
+
+/* Flat fp32 parameter layout = the reference's state_dict order and shapes
+ * (Training_VAE.py:132-167; 24 tensors at 4+4 layers).  Tensor i occupies
+ * [offset, offset+numel) of the flat buffer, row-major nn.Linear (out,in). */
+int cvae_num_params(const cvae_handle* h, int64_t* total, int* n_tensors);
+int cvae_param_info(const cvae_handle* h, int i, int64_t* offset, int64_t* numel, int* rows, int* cols);
+
+/* Host-only query (no device needed): parameter count / tensor count of the
+ * flat layout, and the LDS bytes one row-chain workgroup needs (0 < lds <=
+ * 163840 when the configuration is supported). */
+int cvae_config_info(const cvae_config* cfg, int64_t* total_params, int* n_tensors, int* lds_bytes);
+
+/* Workspace bytes the handle allocated (informational). */
+int cvae_workspace_bytes(const cvae_handle* h, int64_t* bytes);
+
+/* Rebuild the device copies of the weights (padded operand-dtype W and Wᵀ,
+ * padded fp32 biases) from the flat fp32 master `params`.  Call after the
+ * caller writes parameters (init, load_state_dict).  cvae_adam/cvae_train_step
+ * keep the copies current themselves. */
+int cvae_pack_weights(cvae_handle* h, const float* params, void* stream);
+
+/* Inference: encode → reparameterise → decode.  Replaces
+ * ConditionalTrajectoryVAE.forward (Training_VAE.py:217-226).
+ *   x      (N_total,S,D) trajectories, operand dtype, row-major.  With
+ *          start == NULL x holds ABSOLUTE coordinates and the relative
+ *          transform of :345-348 is applied in-kernel (condition = x[:,0,1:3]);
+ *          with start != NULL x is used as given (already relative, as
+ *          model(batch_rel, start_points) at :352) and start fp32 (batch,2) is
+ *          the condition.
+ *   idx    optional int64[batch] row gather into x (NULL = rows 0..batch-1)
+ *   eps    optional fp32 (batch,Z); NULL = in-kernel Philox(seed, offset)
+ *   recon  fp32 (batch,S,D) relative trajectories; mu, logvar fp32 (batch,Z);
+ *   hc     fp32 (batch,H) condition features (any output may be NULL).      */
+int cvae_forward(cvae_handle* h, const void* x, const int64_t* idx, int batch,
+                 const float* start, const float* eps, uint64_t seed, uint64_t offset,
+                 float* recon, float* mu, float* logvar, float* hc, void* stream);
+
+/* Condition encoder only: h_c = condition_encoder(start)
+ * (Training_VAE.py:132-137, called at :190 and Tools.py:55).
+ *   start fp32 (batch,2) absolute start points → hc fp32 (batch,H). */
+int cvae_condition(cvae_handle* h, const float* start, int batch, float* hc, void* stream);
+
+/* Decode (generation).  Replaces ConditionalTrajectoryVAE.decode
+ * (Training_VAE.py:208-215) and the sampling of Tools.py:46-63.
+ *   z fp32 (batch,Z); exactly the condition given:
+ *     hc    fp32 (batch,H) condition features (decode(z, h_c) semantics), or
+ *     start fp32 (batch,2) absolute start points (condition encoder fused in);
+ *   out fp32 (batch,S,D) relative trajectories (caller adds start for global). */
+int cvae_decode(cvae_handle* h, const float* z, const float* start, const float* hc, int batch,
+                float* out, void* stream);
+
+/* Forward + conditional_vae_loss + full backward for one batch, gradients into
+ * the flat fp32 `grads` (overwritten, same layout as params).  Replaces
+ * Training_VAE.py:351-362 (zero_grad, model(), conditional_vae_loss(),
+ * loss.backward()).  `loss_out` fp32[5] = (total, recon, kld, start, time) as
+ * returned by conditional_vae_loss (:268); `loss_accum` (nullable) fp32[5]
+ * += loss * batch (the per-epoch accumulators of :366-370, kept on device).
+ * Means are over this call's batch, so a data-parallel caller all-reduces
+ * `grads` and passes grad_scale = 1/world to cvae_adam. */
+int cvae_train_fwd_bwd(cvae_handle* h, const void* x, const int64_t* idx, int batch,
+                       const float* eps, uint64_t seed, uint64_t offset,
+                       const cvae_loss_weights* w, float* grads,
+                       float* loss_out, float* loss_accum, void* stream);
+
+/* torch.optim.Adam step (amsgrad=False, weight_decay=0) over the flat buffers
+ * — replaces optimizer.step() (Training_VAE.py:363; torch/optim/adam.py
+ * _single_tensor_adam).  step is the 1-based step count after increment.
+ * g_eff = grads * grad_scale.  Also refreshes the device weight copies. */
+int cvae_adam(cvae_handle* h, float* params, const float* grads, float* m, float* v,
+              int step, float lr, float beta1, float beta2, float eps, float grad_scale,
+              void* stream);
+
+/* Fused single-device step: cvae_train_fwd_bwd + cvae_adam with the weight
+ * gradient GEMMs and Adam in one kernel (the gradient never round-trips HBM).
+ * Replaces the whole body of Training_VAE.py:345-370 for one batch. */
+int cvae_train_step(cvae_handle* h, const void* x, const int64_t* idx, int batch,
+                    const float* eps, uint64_t seed, uint64_t offset,
+                    const cvae_loss_weights* w,
+                    float* params, float* m, float* v, int step,
+                    float lr, float beta1, float beta2, float adam_eps,
+                    float* loss_out, float* loss_accum, void* stream);
+
+/* Standalone conditional_vae_loss (Training_VAE.py:229-268), forward only, for
+ * callers holding (recon, x, mu, logvar) fp32 device tensors; x is the RELATIVE
+ * batch as at the reference call site (:356-359).  loss_out fp32[5] =
+ * (total, recon, kld, start, time); workspace: >= 8*ceil(batch/32) fp32 on device.
+ * Handle-free.  The training entry points fuse the loss and do not need this. */
+int cvae_loss(const float* recon, const float* x, const float* mu, const float* logvar,
+              int batch, int seq_len, int dim, int latent_dim, const cvae_loss_weights* w,
+              float* loss_out, float* workspace, void* stream);
+
+/* Per-kernel device time, measured with HIP events recorded on `stream`
+ * around every kernel of every call made while timing is enabled (no
+ * synchronisation is added; read after the stream is synchronised).
+ * cvae_set_timing(h, 1) enables and resets the record.  cvae_kernel_times
+ * writes, per kernel name ("rowchain", "wgrad", "wgrad_adam", "adam"), the
+ * AVERAGE duration in ms to ms[i] and "name:count" comma-separated to names;
+ * returns the number of kernel names. */
+int cvae_set_timing(cvae_handle* h, int enabled);
+int cvae_kernel_times(cvae_handle* h, char* names, int names_len, float* ms, int max_n);
+
+const char* cvae_last_error(void);
+int cvae_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CVAE_H */

@@ -1,0 +1,76 @@
+"""CPU-side checks of the C-ABI library (no GPU calls): it loads, exports every
+symbol include/cvae.h declares, and its host-only planner agrees with the
+reference's parameter layout (Training_VAE.py:132-167)."""
+import os
+
+import pytest
+import torch
+
+from conftest import ROOT
+from oracle.cvae_oracle import OracleCVAE
+
+
+@pytest.fixture(scope="module")
+def cl():
+    from cvae_amd import _build, _lib
+    _build.build()
+    return _lib
+
+
+def test_library_exports_every_header_symbol(cl):
+    names = cl.header_symbols(os.path.join(ROOT, "include", "cvae.h"))
+    assert len(names) >= 15
+    L = cl.lib()
+    for n in names:
+        assert hasattr(L, n), n
+    assert L.cvae_abi_version() == 1
+
+
+@pytest.mark.parametrize("S,D,Z,H,dtype", [(10, 3, 8, 128, "fp32"), (100, 6, 8, 128, "bf16"),
+                                           (100, 6, 8, 128, "fp32"), (10, 3, 8, 16, "fp32"),
+                                           (10, 3, 8, 16, "bf16"), (50, 4, 16, 64, "bf16")])
+def test_param_layout_matches_state_dict(cl, S, D, Z, H, dtype):
+    from cvae_amd import config_info
+    n, nt, lds = config_info(S, D, Z, H, dtype=dtype)
+    ref = OracleCVAE(S, D, Z, H)
+    assert nt == len(ref.state_dict()) == 24
+    assert n == sum(p.numel() for p in ref.parameters())
+    assert 0 < lds <= 160 * 1024
+
+
+def test_known_param_counts(cl):
+    from cvae_amd import config_info
+    assert config_info(10, 3, 8)[0] == 128942      # SURVEY §2 (measured on the reference)
+    assert config_info(100, 6, 8)[0] == 275432
+
+
+def test_unsupported_config_reports_error(cl):
+    from cvae_amd import config_info
+    from cvae_amd._lib import CvaeError
+    with pytest.raises(CvaeError, match="LDS"):
+        config_info(200, 6, 512, 128, 8, 8, dtype="bf16")
+    with pytest.raises(CvaeError, match="dim"):
+        config_info(10, 2, 8)
+
+
+def test_engine_refuses_without_gpu(cl):
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from cvae_amd import ConditionalTrajectoryVAE, CVAEEngine
+    with pytest.raises(RuntimeError, match="HIP device"):
+        CVAEEngine(10, 3, 8)
+    m = ConditionalTrajectoryVAE(10, 3, 8)
+    with pytest.raises(RuntimeError, match="attach"):
+        m(torch.zeros(2, 10, 3), torch.zeros(2, 2))
+
+
+def test_model_init_and_state_dict_match_reference_layout(cl):
+    from cvae_amd import ConditionalTrajectoryVAE
+    torch.manual_seed(0)
+    a = ConditionalTrajectoryVAE(10, 3, 8)
+    torch.manual_seed(0)
+    b = OracleCVAE(10, 3, 8)
+    sa, sb = a.state_dict(), b.state_dict()
+    assert list(sa.keys()) == list(sb.keys())
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k
