@@ -4,6 +4,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -51,6 +52,11 @@ struct cvae_handle {
   int64_t arena_bytes = 0;
   float* d_partials = nullptr;
   int max_row_tiles = 0;
+  // step tables of the row-chain interpreter, one per mode (device copies in the arena)
+  enum { ST_TRAIN = 0, ST_FWD, ST_DEC, ST_DEC_HC, ST_COND, ST_N };
+  StepDesc* d_steps[ST_N] = {};
+  int n_steps[ST_N] = {};
+  unsigned long long* d_stamps = nullptr;  // diagnostic builds only
   int lds_bytes = 0;
   bool timing = false;
   // timing: per call, a chain of events on the caller's stream; segment i of a
@@ -77,10 +83,10 @@ int build_plan(cvae_handle* h) {
   n.ZHp = rup_i(n.Z + n.H, 32); n.Zp2 = rup_i(2 * n.Z, 32); n.Cp = 32;
   n.dtype = c.dtype;
   h->tsize = c.dtype == CVAE_BF16 ? 2 : 4;
-  h->R = c.dtype == CVAE_BF16 ? 32 : 16;
+  h->R = c.dtype == CVAE_BF16 ? RowsPerTile<__bf16>::R : RowsPerTile<float>::R;
   // arena rows: whole row tiles, and a multiple of the K chunk of the wgrad GEMM
   n.Bp = rup_i(c.max_batch, 32);
-  h->max_row_tiles = (c.max_batch + h->R - 1) / h->R;
+  h->max_row_tiles = rup_i(c.max_batch, 32) / h->R;
 
   // layer table (in = K, out = N) in state_dict order
   struct LD { int K, N, relu; };
@@ -126,6 +132,8 @@ int build_plan(cvae_handle* h) {
     return fail(CVAE_E_INVALID, "configuration needs " + std::to_string(lp.total) +
                                     " B of LDS per row tile (> 160 KiB); reduce seq_len*dim or latent_dim");
   if (c.dim < 3) return fail(CVAE_E_INVALID, "dim must be >= 3 (channel 0 = time, 1:3 = x,y)");
+  if (c.hidden_dim % 4 || c.latent_dim % 4)
+    return fail(CVAE_E_INVALID, "hidden_dim and latent_dim must be multiples of 4 (4-feature epilogue vectors)");
 
   // weight-gradient / parameter tiles: 32×32 over each layer's padded (Np × Kp)
   h->tiles.clear();
@@ -133,6 +141,98 @@ int build_plan(cvae_handle* h) {
     for (int o = 0; o < n.L[l].Np; o += 32)
       for (int i = 0; i < n.L[l].Kp; i += 32) h->tiles.push_back({l, o, i, 0});
   return CVAE_OK;
+}
+
+// Step tables (see cvae_rowchain.h).  Masks: C0=0, C1=1, E_i=2+i, D_i=2+n_enc+i.
+std::vector<StepDesc> build_steps(const NetDev& n, int mode) {
+  const bool train = mode == cvae_handle::ST_TRAIN;
+  const int ne = n.n_enc, nd = n.n_dec, Z = n.Z, H = n.H;
+  auto arena = [&](void* p) -> void* { return train ? p : nullptr; };
+  auto blank = [&]() {
+    StepDesc s{};
+    s.mask_out = -1; s.mask_in = -1; s.dst1 = B_NONE; s.dst2 = B_NONE;
+    return s;
+  };
+  auto fwd = [&](int l, int xbuf, int epi) {
+    StepDesc s = blank();
+    const LayerDev& L = n.L[l];
+    s.W = L.Wf; s.bias = L.bias; s.Kp = L.Kp; s.Np = L.Np; s.N = L.N; s.xbuf = xbuf; s.epi = epi;
+    return s;
+  };
+  auto bwd = [&](int l, int xbuf, int epi) {
+    StepDesc s = blank();
+    const LayerDev& L = n.L[l];
+    s.W = L.Wb; s.bias = n.zbias; s.Kp = L.Np; s.Np = L.Kp; s.N = L.K; s.xbuf = xbuf; s.epi = epi;
+    return s;
+  };
+  auto pb = [](int i) { return (i & 1) ? B_P1 : B_P0; };
+  std::vector<StepDesc> v;
+  if (mode != cvae_handle::ST_DEC_HC) {
+    StepDesc s = fwd(lC0(n), B_CIN, E_RELU);
+    s.mask_out = 0; s.dst1 = B_P0; s.g1 = arena(n.L[lC1(n)].xT);
+    v.push_back(s);
+    s = fwd(lC1(n), B_P0, E_RELU);
+    s.mask_out = 1; s.concat = 1;
+    s.dst1 = B_HC; s.off1 = H; s.dst2 = B_DEC; s.off2 = Z;
+    s.g1 = arena(n.L[lFC(n)].xT); s.goff1 = H; s.g2 = arena(n.L[lD(n, 0)].xT); s.goff2 = Z;
+    s.hc_out = train ? 0 : 1;
+    v.push_back(s);
+  }
+  if (mode == cvae_handle::ST_COND) return v;
+  if (mode == cvae_handle::ST_TRAIN || mode == cvae_handle::ST_FWD) {
+    for (int i = 0; i < ne; ++i) {
+      StepDesc s = fwd(lE(n, i), i == 0 ? B_XIN : pb(i - 1), E_RELU);
+      s.mask_out = 2 + i;
+      if (i == ne - 1) {
+        s.dst1 = B_HC; s.off1 = 0; s.concat = 1; s.g1 = arena(n.L[lFC(n)].xT);
+      } else {
+        s.dst1 = pb(i); s.g1 = arena(n.L[lE(n, i + 1)].xT);
+      }
+      v.push_back(s);
+    }
+    v.push_back(fwd(lFC(n), B_HC, E_FC));
+  }
+  for (int i = 0; i < nd - 1; ++i) {
+    StepDesc s = fwd(lD(n, i), i == 0 ? B_DEC : pb(i - 1), E_RELU);
+    s.mask_out = 2 + ne + i; s.dst1 = pb(i); s.g1 = arena(n.L[lD(n, i + 1)].xT);
+    v.push_back(s);
+  }
+  {
+    StepDesc s = fwd(lD(n, nd - 1), nd == 1 ? B_DEC : pb(nd - 2), train ? E_LOSS : E_RECON);
+    if (train) s.g1 = n.L[lD(n, nd - 1)].gT;
+    v.push_back(s);
+  }
+  if (!train) return v;
+  // backward: decoder → reparameterisation → fc → encoder / condition encoder
+  int cur = B_XIN, pp = 0;
+  for (int i = nd - 1; i >= 1; --i) {
+    StepDesc s = bwd(lD(n, i), cur, E_BWD);
+    s.mask_in = 2 + ne + i - 1; s.dst1 = pp ? B_P1 : B_P0; s.g1 = n.L[lD(n, i - 1)].gT;
+    v.push_back(s);
+    cur = s.dst1;
+    pp ^= 1;
+  }
+  v.push_back(bwd(lD(n, 0), cur, E_D0B));
+  {
+    StepDesc s = bwd(lFC(n), B_P0, E_FCB);
+    s.g1 = n.L[lE(n, ne - 1)].gT; s.g2 = n.L[lC1(n)].gT;
+    v.push_back(s);
+  }
+  cur = B_P1;
+  int p = 0;
+  for (int i = ne - 1; i >= 1; --i) {
+    StepDesc s = bwd(lE(n, i), cur, E_BWD);
+    s.mask_in = 2 + i - 1; s.dst1 = i > 1 ? (p ? B_P1 : B_P0) : B_NONE; s.g1 = n.L[lE(n, i - 1)].gT;
+    v.push_back(s);
+    cur = s.dst1;
+    p ^= 1;
+  }
+  {
+    StepDesc s = bwd(lC1(n), B_HC, E_BWD);
+    s.mask_in = 0; s.g1 = n.L[lC0(n)].gT;
+    v.push_back(s);
+  }
+  return v;
 }
 
 int alloc_arena(cvae_handle* h) {
@@ -156,8 +256,13 @@ int alloc_arena(cvae_handle* h) {
     lo[l].xT = take((int64_t)L.Kp * n.Bp * ts);
     lo[l].gT = take((int64_t)L.Np * n.Bp * ts);
   }
+  int maxnp = 32;
+  for (int l = 0; l < n.n_layers; ++l) maxnp = std::max(maxnp, std::max(n.L[l].Np, n.L[l].Kp));
+  const int64_t zb_off = take((int64_t)maxnp * 4);
   const int64_t part_off = take((int64_t)h->max_row_tiles * 8 * 4);
   const int64_t tile_off = take((int64_t)h->tiles.size() * sizeof(TileDesc));
+  int64_t step_off[cvae_handle::ST_N];
+  for (int m = 0; m < cvae_handle::ST_N; ++m) step_off[m] = take(64 * (int64_t)sizeof(StepDesc));
   HIPCK(hipMalloc(&h->arena, total));
   HIPCK(hipMemset(h->arena, 0, total));
   h->arena_bytes = total;
@@ -169,15 +274,23 @@ int alloc_arena(cvae_handle* h) {
     L.xT = h->arena + lo[l].xT;
     L.gT = h->arena + lo[l].gT;
   }
+  n.zbias = (const float*)(h->arena + zb_off);
   h->d_partials = (float*)(h->arena + part_off);
   h->d_tiles = (TileDesc*)(h->arena + tile_off);
   HIPCK(hipMemcpy(h->d_tiles, h->tiles.data(), h->tiles.size() * sizeof(TileDesc), hipMemcpyHostToDevice));
+  for (int m = 0; m < cvae_handle::ST_N; ++m) {
+    const std::vector<StepDesc> st = build_steps(n, m);
+    if (st.empty() || st.size() > 64) return fail(CVAE_E_INVALID, "bad step table");
+    h->d_steps[m] = (StepDesc*)(h->arena + step_off[m]);
+    h->n_steps[m] = (int)st.size();
+    HIPCK(hipMemcpy(h->d_steps[m], st.data(), st.size() * sizeof(StepDesc), hipMemcpyHostToDevice));
+  }
   return CVAE_OK;
 }
 
 template <typename T>
 int set_lds_attrs(cvae_handle* h) {
-  constexpr int R = sizeof(T) == 2 ? 32 : 16;
+  constexpr int R = RowsPerTile<T>::R;
   HIPCK(hipFuncSetAttribute((const void*)rowchain_kernel<T, R, RC_TRAIN>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, h->lds_bytes));
   HIPCK(hipFuncSetAttribute((const void*)rowchain_kernel<T, R, RC_FWD>,
@@ -209,9 +322,17 @@ int tmark(cvae_handle* h, hipStream_t s, const char* name) {
 }
 
 template <typename T, int MODE>
-int launch_rowchain(cvae_handle* h, const RowArgs& a, hipStream_t s) {
-  constexpr int R = sizeof(T) == 2 ? 32 : 16;
-  const int grid = (a.batch + R - 1) / R;
+int launch_rowchain(cvae_handle* h, RowArgs a, hipStream_t s) {
+  constexpr int R = RowsPerTile<T>::R;
+  // the grid covers roundup(batch, 32) rows: the wgrad K range (a multiple of the 32-deep bf16
+  // chunk) then only reads rows this launch wrote (zeros past the batch)
+  const int grid = rup_i(a.batch, 32) / R;
+  int st = cvae_handle::ST_TRAIN;
+  if (MODE == RC_FWD) st = cvae_handle::ST_FWD;
+  if (MODE == RC_DECODE) st = a.hc_in ? cvae_handle::ST_DEC_HC : (a.z_in ? cvae_handle::ST_DEC : cvae_handle::ST_COND);
+  a.steps = h->d_steps[st];
+  a.nsteps = h->n_steps[st];
+  a.stamps = h->d_stamps;
   hipLaunchKernelGGL((rowchain_kernel<T, R, MODE>), dim3(grid), dim3(CVAE_THREADS), h->lds_bytes, s, h->net, a);
   HIPCK(hipGetLastError());
   return CVAE_OK;
@@ -258,14 +379,14 @@ int train_fwd_bwd_impl(cvae_handle* h, const void* x, const int64_t* idx, int ba
 LossArgs make_loss(cvae_handle* h, const RowArgs& ra, float* loss_out, float* loss_accum) {
   LossArgs la{};
   la.partials = h->d_partials;
-  la.ntiles = (ra.batch + h->R - 1) / h->R;
+  la.ntiles = rup_i(ra.batch, 32) / h->R;
   la.batch = ra.batch;
   la.w_recon = ra.w_recon; la.w_kld = ra.w_kld; la.w_start = ra.w_start; la.w_time = ra.w_time;
   la.loss_out = loss_out; la.loss_accum = loss_accum;
   return la;
 }
 
-int bk_of(cvae_handle* h, int batch) { return (batch + h->R - 1) / h->R * h->R; }
+int bk_of(cvae_handle*, int batch) { return rup_i(batch, 32); }
 
 }  // namespace
 
@@ -479,6 +600,21 @@ int cvae_loss(const float* recon, const float* x, const float* mu, const float* 
   HIPCK(hipGetLastError());
   return CVAE_OK;
 }
+
+#if CVAE_DIAG_SUB
+int cvae_diag_set_sub(unsigned long long* dev_buf) {
+  HIPCK(hipMemcpyToSymbol(HIP_SYMBOL(g_sub), &dev_buf, sizeof(dev_buf)));
+  return CVAE_OK;
+}
+#endif
+
+#if CVAE_DIAG_STAMPS
+// diagnostic builds only: per-block step stamps (s_memrealtime, 100 MHz) of the next launches
+int cvae_diag_set_stamps(cvae_handle* h, unsigned long long* dev_buf) {
+  h->d_stamps = dev_buf;
+  return CVAE_OK;
+}
+#endif
 
 int cvae_set_timing(cvae_handle* h, int enabled) {
   if (!h) return fail(CVAE_E_INVALID, "null handle");

@@ -42,6 +42,7 @@ struct NetDev {
   int Ip, Hp, Hcp, ZHp, Zp2, Cp;
   int Bp;                // arena row capacity
   int dtype;             // 0 fp32, 1 bf16
+  const float* zbias;    // zeros (>= max Np floats): the "bias" of the dX GEMMs
   LayerDev L[CVAE_MAX_LAYERS];
 };
 
@@ -95,6 +96,16 @@ __device__ __forceinline__ void store4(__bf16* p, f32x4 v) {
   h[0] = (__bf16)v[0]; h[1] = (__bf16)v[1]; h[2] = (__bf16)v[2]; h[3] = (__bf16)v[3];
   *(bf16x4*)p = h;
 }
+
+// ------------------------------------------------------------------ global-address-space access
+// Pointers that come out of descriptors in memory are generic: hipcc then emits FLAT
+// loads/stores, which count on lgkmcnt as well as vmcnt — every LDS wait would also wait for
+// the in-flight weight stream and arena stores.  These casts force global_* instructions.
+#define CVAE_GLOBAL __attribute__((address_space(1)))
+template <typename V>
+__device__ __forceinline__ V gld(const void* p) { return *(const CVAE_GLOBAL V*)p; }
+template <typename V>
+__device__ __forceinline__ void gst(void* p, V v) { *(CVAE_GLOBAL V*)p = v; }
 
 // ------------------------------------------------------------------ Philox4x32-10
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {

@@ -13,30 +13,81 @@
 // stores every layer input xT(l) and pre-activation gradient gT(l)
 // feature-major into the activation arena.
 //
-// GEMM core: `dense` computes Y[R×Np] = X[R×Kp]·Wᵀ with X from LDS (A operand,
-// ds_read_b128) and W streamed from L2 straight into registers (B operand, one
-// 16-B global load per lane per K chunk, PF chunks in flight).  Each wave owns
-// pairs of 16-column tiles; MFMA 16x16x32 bf16 or 4×16x16x4 f32 per chunk.
-// ReLU masks are kept as bits in LDS for the backward pass.
+// Structure: a compact LAYER INTERPRETER.  The host builds a step table (one
+// entry per GEMM: operand buffers, weights, epilogue kind and targets); the
+// kernel runs ONE instance of the GEMM loop over it, epilogues chosen by a
+// wave-uniform switch.  A fully inlined version of the same chain compiled to
+// 90 KB of straight-line code that ran once per launch — larger than the
+// instruction cache — and spent ~3 µs per layer fetching instructions; this
+// version keeps the hot code small and re-executed.
+//
+// GEMM core: Y[R×Np] = X[R×Kp]·Wᵀ, X from LDS (A operand, ds_read_b128), W streamed
+// from L2 straight into registers (B operand), double-buffered across K blocks,
+// column groups and layers (see `dense`).  MFMA 16x16x32 bf16 or 4×16x16x4 f32.
+// ReLU masks are kept as bits in LDS for the backward pass.  Barriers between
+// steps are LDS-only (`lds_barrier`): global stores never drain at a barrier.
 #pragma once
 #include "cvae_device.h"
 
 enum { RC_TRAIN = 0, RC_FWD = 1, RC_DECODE = 2 };
 
-// Diagnostic builds only (scripts/diag_rowchain.sh): drop the arena stores / bias loads to
-// price them.  Results are wrong in those builds; the shipped library defines neither.
+// batch rows per workgroup (the MFMA N dimension of the swapped GEMM: a multiple of 16)
+template <typename T> struct RowsPerTile { static constexpr int R = 16; };
+
+// Diagnostic builds only (scripts/diag_*.sh): drop the arena stores to price them /
+// record per-step time stamps.  Results are wrong under NOSTORE; the shipped library
+// defines neither.
 #ifndef CVAE_DIAG_NOSTORE
 #define CVAE_DIAG_NOSTORE 0
 #endif
-#ifndef CVAE_DIAG_NOBIAS
-#define CVAE_DIAG_NOBIAS 0
+#ifndef CVAE_DIAG_STAMPS
+#define CVAE_DIAG_STAMPS 0
 #endif
+#ifndef CVAE_DIAG_SUB
+#define CVAE_DIAG_SUB 0
+#endif
+#if CVAE_DIAG_SUB
+// [block][wave][step][5]: entry, weights arrived, MFMAs done, epilogue done, barrier passed
+__device__ unsigned long long* g_sub;
+__device__ int g_sub_step;
+#define SUBSTAMP(k)                                                                                     \
+  do {                                                                                                  \
+    if ((threadIdx.x & 63) == 0 && g_sub && g_sub_step < 32)                                            \
+      g_sub[((blockIdx.x * 4 + (threadIdx.x >> 6)) * 32 + g_sub_step) * 5 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define SUBSTAMP(k) do { } while (0)
+#endif
+
+// LDS buffers a step can read or write
+enum { B_NONE = -1, B_XIN = 0, B_P0 = 1, B_P1 = 2, B_HC = 3, B_DEC = 4, B_CIN = 5 };
+// epilogue kinds; post-step element-wise phases
+enum { E_RELU = 0, E_FC = 1, E_LOSS = 2, E_RECON = 3, E_BWD = 4, E_D0B = 5, E_FCB = 6 };
+
+struct StepDesc {
+  const void* W;     // B operand [Np][Kp] (forward Wf or backward Wb)
+  const float* bias; // [Np] (zeros for backward)
+  void* g1;          // arena destination (feature-major), nullable
+  void* g2;
+  int Kp, Np;        // reduction / output dims (padded)
+  int N;             // real output columns
+  int xbuf;          // LDS source
+  int epi;           // E_*
+  int mask_out;      // forward: ReLU mask index to set (-1 none)
+  int mask_in;       // backward: ReLU mask index to apply
+  int dst1, off1;    // LDS destinations (B_NONE = none) and column offsets
+  int dst2, off2;
+  int goff1, goff2;  // arena row offsets of g1 / g2
+  int concat;        // skip columns >= N (destination is part of a concatenation)
+  int hc_out;        // inference: also write h_c (fp32) to RowArgs::hc_out
+};
 
 struct RowArgs {
   const void* x;          // (N_total, S, D) operand dtype
   const int64_t* idx;     // optional row gather
   int batch;
-  int pad_;
+  int nsteps;
+  const StepDesc* steps;  // step table of this mode (device)
   const float* eps;       // optional (batch, Z)
   uint64_t seed, offset;
   float w_recon, w_kld, w_start, w_time;
@@ -48,8 +99,9 @@ struct RowArgs {
   const float* z_in;      // DECODE inputs
   const float* start_in;  // DECODE, or FWD with x already relative
   const float* hc_in;     // DECODE: given condition features (skips the condition encoder)
+  unsigned long long* stamps;  // diagnostic builds only
   int x_relative;         // 1: x is relative, condition = start_in (no transform)
-  int pad2_;
+  int pad_;
 };
 
 struct LdsPlan {
@@ -61,16 +113,17 @@ struct LdsPlan {
 
 __host__ __device__ inline int rup(int v, int a) { return (v + a - 1) / a * a; }
 
+__host__ __device__ inline int n_masks(const NetDev& n) { return 2 + n.n_enc + (n.n_dec - 1); }
+
 __host__ __device__ inline LdsPlan lds_plan(const NetDev& n, int R, int tsize) {
   LdsPlan p;
-  const int pad = 16 / tsize;
+  const int pad = 16 / tsize;  // +16 B per row: 16-B LDS reads of 16 consecutive rows hit distinct banks
   p.sx = n.Ip + pad;
   p.sp = (n.Hp > n.Zp2 ? n.Hp : n.Zp2) + pad;
   p.shc = n.Hcp + pad;
   p.sdec = n.ZHp + pad;
   p.scin = n.Cp + pad;
   p.mw = n.Hp / 32;
-  const int nmask = 2 + n.n_enc + (n.n_dec - 1);
   int o = 0;
   auto take = [&](int bytes) { int r = o; o += rup(bytes, 16); return r; };
   p.oXin = take(R * p.sx * tsize);
@@ -89,61 +142,130 @@ __host__ __device__ inline LdsPlan lds_plan(const NetDev& n, int R, int tsize) {
   p.oGd0 = p.oU + R * n.S * 4;
   p.oStart = take(R * 2 * 4);
   p.oRow = take(R * 8);
-  p.oMask = take(nmask * R * p.mw * 4);
+  p.oMask = take(n_masks(n) * R * p.mw * 4);
   p.oPart = take(CVAE_NW * 8 * 4);
   p.total = o;
   return p;
 }
 
-// Y = X·Wᵀ over the workgroup's R rows; epi(row0, col, v) receives rows row0..row0+3 of column col.
-template <typename T, int R, class Epi>
-__device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T* __restrict__ W,
-                                      int Kp, int Np, Epi&& epi) {
+// ---------------------------------------------------------------- weight-stream GEMM
+// A wave owns 32-column groups g = wave, wave+4, ...; each group's K range is cut into
+// blocks of NKB chunks held in a register block.  The weight stream is double-buffered
+// across blocks, groups AND steps: while block i is multiplied, block i+1 — possibly of the
+// next group, or the first block of the NEXT step — is already in flight in `pre`.
+// Every load is unconditional (the source is selected, chunk indices clamped): a load under
+// a branch makes hipcc wait vmcnt(0) (cdna_hip_programming.md §5 trap (c)).  Loads are
+// issued before the epilogue's global stores, so waiting for them never waits for those
+// stores (vmcnt retires in order).
+constexpr int NKB = 4;
+
+template <typename T>
+struct WBlock {
+  typename Op<T>::V b[NKB][2];
+};
+
+template <typename T>
+__device__ __forceinline__ void load_block(WBlock<T>& wb, const T* __restrict__ W, int Kp, int Np, int g, int blk) {
   using V = typename Op<T>::V;
-  constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC, MT = R / 16, NB = 2, PF = 4;
+  constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC;
+  const int lane = threadIdx.x & 63, r16 = lane & 15, kq = (lane >> 4) * EPL;
+  const int nk = Kp / KC, ng = Np >> 5;
+  g = min(g, ng - 1);
+  const T* w0 = W + (size_t)(g * 32 + r16) * Kp + kq;
+  const T* w1 = w0 + (size_t)16 * Kp;
+#pragma unroll
+  for (int u = 0; u < NKB; ++u) {
+    const int kc = min(blk * NKB + u, nk - 1);
+    wb.b[u][0] = gld<V>(w0 + kc * KC);
+    wb.b[u][1] = gld<V>(w1 + kc * KC);
+  }
+}
+
+// epi(row, f0, v) receives v[i] = Y[row][f0 + i], i = 0..3: the MFMA computes Yᵀ = W·Xᵀ
+// (A = weights, B = activations), so a lane's accumulator holds FOUR CONSECUTIVE FEATURES of
+// one row — one 8/16-B LDS store, one float4 bias and one 4-bit mask nibble per call.
+template <typename T, int R, class Epi>
+__device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T* __restrict__ W, int Kp, int Np,
+                                      WBlock<T>& pre, const T* nW, int nKp, int nNp, Epi&& epi) {
+  using V = typename Op<T>::V;
+  constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC, MT = R / 16;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, kq = (lane >> 4) * EPL;
-  const int NT = Np >> 4, nk = Kp / KC;
-  for (int nt0 = wave * NB; nt0 < NT; nt0 += CVAE_NW * NB) {
-    f32x4 acc[NB][MT];
+  const int NG = Np >> 5, nk = Kp / KC, nblk = (nk + NKB - 1) / NKB;
+  const int ng_mine = NG > wave ? (NG - wave + CVAE_NW - 1) / CVAE_NW : 0;
+  const int nitems = ng_mine * nblk;
+  if (nitems == 0) {  // idle in this step: still stream the next step's first block
+    if (nW) load_block(pre, nW, nKp, nNp, wave, 0);
+    return;
+  }
+  f32x4 acc[2][MT];
 #pragma unroll
-    for (int j = 0; j < NB; ++j)
+  for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int m = 0; m < MT; ++m) acc[j][m] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const T* wp[NB];
+    for (int m = 0; m < MT; ++m) acc[j][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int it = 0; it < nitems; ++it) {
+    const int gi = it / nblk, blk = it - gi * nblk;
+    const int g = wave + gi * CVAE_NW;
+    const WBlock<T> cur = pre;
+#if CVAE_DIAG_SUB
+    if (it == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      SUBSTAMP(1);
+    }
+#endif
+    {  // next item: this step's next block/group, else the next step's first block
+      const int it2 = it + 1;
+      const bool same = it2 < nitems;
+      const int gi2 = it2 / nblk;
+      const T* W2 = same ? W : (nW ? nW : W);
+      const int Kp2 = same ? Kp : (nW ? nKp : Kp);
+      const int Np2 = same ? Np : (nW ? nNp : Np);
+      const int g2 = same ? wave + gi2 * CVAE_NW : wave;
+      const int blk2 = same ? it2 - gi2 * nblk : 0;
+      load_block(pre, W2, Kp2, Np2, g2, blk2);
+    }
+    // all LDS reads of the block first (one lgkmcnt wait per block, not per chunk), then the
+    // MFMAs unconditionally: chunks past K read a clamped (valid) address and are zeroed, so a
+    // short block costs a few idle MFMAs instead of branches and per-chunk waits
+    V xa[NKB][MT];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) wp[j] = W + (size_t)((nt0 + j) * 16 + r16) * Kp + kq;
-    V bq[PF][NB];
+    for (int u = 0; u < NKB; ++u) {
+      const int kc = min(blk * NKB + u, nk - 1);
 #pragma unroll
-    for (int u = 0; u < PF; ++u)
-      if (u < nk) {
-#pragma unroll
-        for (int j = 0; j < NB; ++j) bq[u][j] = *(const V*)(wp[j] + u * KC);
-      }
-    for (int kc0 = 0; kc0 < nk; kc0 += PF) {
-#pragma unroll
-      for (int u = 0; u < PF; ++u) {
-        const int kc = kc0 + u;
-        if (kc < nk) {
-          V a[MT];
-#pragma unroll
-          for (int m = 0; m < MT; ++m) a[m] = *(const V*)(Xs + (m * 16 + r16) * ldx + kc * KC + kq);
-#pragma unroll
-          for (int j = 0; j < NB; ++j)
-#pragma unroll
-            for (int m = 0; m < MT; ++m) acc[j][m] = mfma_chunk(a[m], bq[u][j], acc[j][m]);
-          if (kc + PF < nk) {
-#pragma unroll
-            for (int j = 0; j < NB; ++j) bq[u][j] = *(const V*)(wp[j] + (kc + PF) * KC);
-          }
-        }
-      }
+      for (int m = 0; m < MT; ++m) xa[u][m] = *(const V*)(Xs + (m * 16 + r16) * ldx + kc * KC + kq);
     }
 #pragma unroll
-    for (int j = 0; j < NB; ++j)
+    for (int u = 0; u < NKB; ++u) {
+      const bool on = blk * NKB + u < nk;
 #pragma unroll
-      for (int m = 0; m < MT; ++m) epi(m * 16 + (lane >> 4) * 4, (nt0 + j) * 16 + r16, acc[j][m]);
+      for (int m = 0; m < MT; ++m) {
+        const V xb = on ? xa[u][m] : V{};
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[j][m] = mfma_chunk(cur.b[u][j], xb, acc[j][m]);
+      }
+    }
+#if CVAE_DIAG_SUB
+    if (it == 0) SUBSTAMP(2);
+#endif
+    if (blk == nblk - 1) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          epi(m * 16 + r16, g * 32 + j * 16 + (lane >> 4) * 4, acc[j][m]);
+          acc[j][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#if CVAE_DIAG_SUB
+      if (it == nblk - 1) SUBSTAMP(3);
+#endif
+    }
   }
+}
+
+// Workgroup barrier for LDS hand-offs only: no vmcnt drain, so global stores and the weight
+// prefetch stay in flight across it (nothing in this kernel reads back its global stores).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 template <typename T>
@@ -151,51 +273,97 @@ __device__ __forceinline__ void st4(T* p, f32x4 v) {
   if (!CVAE_DIAG_NOSTORE) store4(p, v);
 }
 
-__device__ __forceinline__ bool mask_bit(const uint32_t* mk, int mw, int row, int col) {
-  return (mk[row * mw + (col >> 5)] >> (col & 31)) & 1u;
+// 4 consecutive T values from floats: one 8-B (bf16) / 16-B (fp32) LDS or global store
+__device__ __forceinline__ void put4(float* p, f32x4 v) { *(f32x4*)p = v; }
+__device__ __forceinline__ void put4(__bf16* p, f32x4 v) {
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  bf16x4 h;
+  h[0] = (__bf16)v[0]; h[1] = (__bf16)v[1]; h[2] = (__bf16)v[2]; h[3] = (__bf16)v[3];
+  *(bf16x4*)p = h;
+}
+__device__ __forceinline__ f32x4 get4(const float* p) { return *(const f32x4*)p; }
+__device__ __forceinline__ f32x4 get4(const __bf16* p) {
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  const bf16x4 h = *(const bf16x4*)p;
+  return f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+}
+__device__ __forceinline__ void gstore4(float* p, f32x4 v) { gst<f32x4>(p, v); }
+__device__ __forceinline__ void gstore4(__bf16* p, f32x4 v) {
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  bf16x4 h;
+  h[0] = (__bf16)v[0]; h[1] = (__bf16)v[1]; h[2] = (__bf16)v[2]; h[3] = (__bf16)v[3];
+  gst<bf16x4>(p, h);
+}
+// feature-major arena store of 4 consecutive features of one row (4 element stores)
+template <typename T>
+__device__ __forceinline__ void put4T(T* base, int Bp, f32x4 v) {
+  if (CVAE_DIAG_NOSTORE) return;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) gst<T>(base + (size_t)i * Bp, to_t<T>(v[i]));
+}
+// the 4 ReLU bits of features f0..f0+3 (f0 % 4 == 0) of one row
+__device__ __forceinline__ uint32_t mask4(const uint32_t* mk, int mw, int row, int f0) {
+  return (mk[row * mw + (f0 >> 5)] >> (f0 & 31)) & 15u;
 }
 
 template <typename T, int R, int MODE>
 __global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  using V = typename Op<T>::V;
   const LdsPlan P = lds_plan(net, R, (int)sizeof(T));
-  T* Xin = (T*)(smem + P.oXin);
-  T* GL = Xin;  // dL/drecon overwrites the input tile in place in the loss epilogue
+  T* const Xin = (T*)(smem + P.oXin);
+  T* const GL = Xin;  // dL/drecon overwrites the input tile in place in the loss epilogue
   T* const P0b = (T*)(smem + P.oP0);
   T* const P1b = (T*)(smem + P.oP1);
-  // ping-pong select without a runtime-indexed pointer array (that would live in scratch)
-  auto Pb = [&](int i) { return (i & 1) ? P1b : P0b; };
-  T* Hc = (T*)(smem + P.oHc);
-  T* Q = Hc;    // condition-branch gradient overlays [h_traj ‖ h_c] (dead after fc fwd)
-  T* Dec = (T*)(smem + P.oDec);
-  T* Cin = (T*)(smem + P.oCin);
-  float* MuLv = (float*)(smem + P.oMuLv);
-  float* Eps = (float*)(smem + P.oEps);
-  float* Std = (float*)(smem + P.oStd);
-  float* Dz = (float*)(smem + P.oDz);
-  float* Rch0 = (float*)(smem + P.oRch0);
-  float* Gd0 = (float*)(smem + P.oGd0);
-  float* Dhc2 = (float*)(smem + P.oU);
-  float* Start = (float*)(smem + P.oStart);
-  int64_t* RowG = (int64_t*)(smem + P.oRow);
-  uint32_t* Mask = (uint32_t*)(smem + P.oMask);
-  float* Part = (float*)(smem + P.oPart);
+  T* const Hc = (T*)(smem + P.oHc);
+  T* const Q = Hc;  // condition-branch gradient overlays [h_traj ‖ h_c] (dead after fc fwd)
+  T* const Dec = (T*)(smem + P.oDec);
+  T* const Cin = (T*)(smem + P.oCin);
+  float* const MuLv = (float*)(smem + P.oMuLv);
+  float* const Eps = (float*)(smem + P.oEps);
+  float* const Std = (float*)(smem + P.oStd);
+  float* const Dz = (float*)(smem + P.oDz);
+  float* const Rch0 = (float*)(smem + P.oRch0);
+  float* const Gd0 = (float*)(smem + P.oGd0);
+  float* const Dhc2 = (float*)(smem + P.oU);
+  float* const Start = (float*)(smem + P.oStart);
+  int64_t* const RowG = (int64_t*)(smem + P.oRow);
+  uint32_t* const Mask = (uint32_t*)(smem + P.oMask);
+  float* const Part = (float*)(smem + P.oPart);
+  // LDS buffer by id (a select chain on a uniform value: no runtime-indexed pointer array)
+  auto buf = [&](int id) -> T* {
+    return id == B_XIN ? Xin : id == B_P0 ? P0b : id == B_P1 ? P1b : id == B_HC ? Hc : id == B_DEC ? Dec : Cin;
+  };
+  auto ld_of = [&](int id) -> int {
+    return id == B_XIN ? P.sx : (id == B_P0 || id == B_P1) ? P.sp : id == B_HC ? P.shc : id == B_DEC ? P.sdec : P.scin;
+  };
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b0 = blockIdx.x * R;
-  const int nrows = min(R, a.batch - b0);
+  const int nrows = max(0, min(R, a.batch - b0));  // tiles past the batch write zeros
   const int Bp = net.Bp, Z = net.Z, H = net.H, S = net.S, D = net.D, I = net.I;
   const int mw = P.mw;
   const T* xg = (const T*)a.x;
   constexpr bool TRAIN = MODE == RC_TRAIN;
-  const int nmask = 2 + net.n_enc + (net.n_dec - 1);
-  const int mC0 = 0, mC1 = 1;
-  auto mE = [&](int i) { return 2 + i; };
-  auto mD = [&](int i) { return 2 + net.n_enc + i; };
+  const bool skip_cond = MODE == RC_DECODE && a.hc_in != nullptr;
+  int stamp_i = 0;
+  auto stamp = [&]() {
+    if (CVAE_DIAG_STAMPS && a.stamps && tid == 0)
+      gst<unsigned long long>(a.stamps + blockIdx.x * 64 + (stamp_i < 63 ? stamp_i : 63), __builtin_amdgcn_s_memrealtime());
+    ++stamp_i;
+  };
 
   float s_recon = 0.f, s_kl = 0.f, s_start = 0.f, s_t0 = 0.f, s_relu = 0.f;
 
-  // ---------------------------------------------------------------- phase 0: zero + load
+  // the weight stream starts before anything else: first block of the first step
+  WBlock<T> pre;
+  {
+    const StepDesc s0 = a.steps[0];
+    load_block(pre, (const T*)s0.W, s0.Kp, s0.Np, wave, 0);
+  }
+  stamp();
+
+  // ---------------------------------------------------------------- prologue: zero + start points
   {
     auto zero = [&](void* p, int bytes) {
       f32x4* q = (f32x4*)p;
@@ -204,20 +372,20 @@ __global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowA
     zero(Hc, R * P.shc * (int)sizeof(T));
     zero(Dec, R * P.sdec * (int)sizeof(T));
     zero(Cin, R * P.scin * (int)sizeof(T));
-    zero(Mask, rup(nmask * R * mw * 4, 16));
+    zero(Mask, rup(n_masks(net) * R * mw * 4, 16));
     for (int r = tid; r < R; r += CVAE_THREADS) {
       float s0 = 0.f, s1 = 0.f;
       int64_t g = 0;
       if (r < nrows) {
-        g = a.idx ? a.idx[b0 + r] : (int64_t)(b0 + r);
+        g = a.idx ? gld<int64_t>(a.idx + b0 + r) : (int64_t)(b0 + r);
         if (MODE == RC_DECODE || a.x_relative) {
           if (a.start_in) {  // decode(z, h_c) carries no start point
-            s0 = a.start_in[(size_t)(b0 + r) * 2 + 0];
-            s1 = a.start_in[(size_t)(b0 + r) * 2 + 1];
+            s0 = gld<float>(a.start_in + (size_t)(b0 + r) * 2 + 0);
+            s1 = gld<float>(a.start_in + (size_t)(b0 + r) * 2 + 1);
           }
         } else {
-          s0 = to_f(xg[g * I + 1]);   // x[:,0,1:3]  (Training_VAE.py:345)
-          s1 = to_f(xg[g * I + 2]);
+          s0 = to_f(gld<T>(xg + g * I + 1));  // x[:,0,1:3]  (Training_VAE.py:345)
+          s1 = to_f(gld<T>(xg + g * I + 2));
         }
       }
       Start[r * 2 + 0] = s0;
@@ -225,47 +393,42 @@ __global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowA
       RowG[r] = g;
     }
   }
-  __syncthreads();
+  lds_barrier();
   for (int r = tid; r < nrows; r += CVAE_THREADS) {
     Cin[r * P.scin + 0] = to_t<T>(Start[r * 2 + 0]);
     Cin[r * P.scin + 1] = to_t<T>(Start[r * 2 + 1]);
   }
   if (MODE != RC_DECODE) {
     // relative transform fused into the tile load (Training_VAE.py:347-348)
-    using V = typename Op<T>::V;
     constexpr int EPL = Op<T>::EPL, U = 12;
     const bool vec = (I % EPL) == 0 && (((uintptr_t)xg) & 15) == 0;
     if (vec) {
-      // 16-B loads, U per thread issued before any is consumed (one memory latency per U·256 vectors)
+      // 16-B loads, U per thread issued before any is consumed; clamped indices so no load is
+      // conditional; the channel pattern (d = col mod D) is advanced without divisions
       const int VPR = I / EPL, NV = R * VPR;
       for (int base = 0; base < NV; base += U * CVAE_THREADS) {
-        V buf[U];
+        V bufv[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          const int v = base + u * CVAE_THREADS + tid;
-          if (v < NV) {
-            const int r = v / VPR, c = v - r * VPR;
-            if (r < nrows) buf[u] = *(const V*)(xg + RowG[r] * I + c * EPL);
-          }
+          const int v = min(base + u * CVAE_THREADS + tid, NV - 1);
+          const int r = v / VPR, c = v - r * VPR;
+          bufv[u] = gld<V>(xg + RowG[r] * I + c * EPL);  // RowG = row 0 past nrows
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int v = base + u * CVAE_THREADS + tid;
           if (v < NV) {
             const int r = v / VPR, c = v - r * VPR;
+            const bool live = r < nrows;
+            const float s0 = a.x_relative ? 0.f : Start[r * 2 + 0];
+            const float s1 = a.x_relative ? 0.f : Start[r * 2 + 1];
+            int d = (c * EPL) % D;
             V o;
 #pragma unroll
             for (int e = 0; e < EPL; ++e) {
-              float val = 0.f;
-              if (r < nrows) {
-                val = (float)buf[u][e];
-                if (!a.x_relative) {
-                  const int d = (c * EPL + e) % D;
-                  if (d == 1) val -= Start[r * 2 + 0];
-                  else if (d == 2) val -= Start[r * 2 + 1];
-                }
-              }
-              o[e] = to_t<T>(val);
+              const float val = (float)bufv[u][e] - (d == 1 ? s0 : 0.f) - (d == 2 ? s1 : 0.f);
+              o[e] = to_t<T>(live ? val : 0.f);
+              d = d + 1 == D ? 0 : d + 1;
             }
             *(V*)(Xin + r * P.sx + c * EPL) = o;
           }
@@ -283,118 +446,193 @@ __global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowA
         float v = 0.f;
         if (r < nrows && c < I) {
           const int d = c % D;
-          v = to_f(xg[RowG[r] * I + c]);
-          if (!a.x_relative) {
-            if (d == 1) v -= Start[r * 2 + 0];
-            else if (d == 2) v -= Start[r * 2 + 1];
-          }
+          v = to_f(gld<T>(xg + RowG[r] * I + c));
+          if (!a.x_relative) v -= (d == 1 ? Start[r * 2 + 0] : 0.f) + (d == 2 ? Start[r * 2 + 1] : 0.f);
         }
         Xin[r * P.sx + c] = to_t<T>(v);
       }
     }
-  }
-  __syncthreads();
-  if (TRAIN && !CVAE_DIAG_NOSTORE) {
-    T* xc0 = (T*)net.L[lC0(net)].xT;
-    for (int e = tid; e < net.Cp * R; e += CVAE_THREADS) {
-      const int c = e / R, r = e - c * R;
-      xc0[(size_t)c * Bp + b0 + r] = Cin[r * P.scin + c];
+  } else {
+    if (skip_cond) {
+      for (int e = tid; e < R * H; e += CVAE_THREADS) {
+        const int r = e / H, c = e - r * H;
+        Dec[r * P.sdec + Z + c] = to_t<T>(r < nrows ? gld<float>(a.hc_in + (size_t)(b0 + r) * H + c) : 0.f);
+      }
     }
-    T* xe0 = (T*)net.L[lE(net, 0)].xT;
-    for (int e = tid; e < net.Ip * R; e += CVAE_THREADS) {
-      const int c = e / R, r = e - c * R;
-      xe0[(size_t)c * Bp + b0 + r] = Xin[r * P.sx + c];
+    if (a.z_in) {
+      for (int e = tid; e < R * Z; e += CVAE_THREADS) {
+        const int r = e / Z, j = e - r * Z;
+        Dec[r * P.sdec + j] = to_t<T>(r < nrows ? gld<float>(a.z_in + (size_t)(b0 + r) * Z + j) : 0.f);
+      }
     }
   }
+  lds_barrier();
+  stamp();
 
-  // Forward ReLU epilogue: LDS dst (+ optional second), arena xT of the consumer, mask bits.
-  auto relu_epi = [&](const LayerDev& L, int mi, T* d1, int ld1, int off1, T* d2, int ld2, int off2,
-                      T* g1, int goff1, T* g2, int goff2, bool concat) {
-    return [&, d1, ld1, off1, d2, ld2, off2, g1, goff1, g2, goff2, concat, mi](int row0, int col, f32x4 v) {
-      const float bias = CVAE_DIAG_NOBIAS ? 0.f : L.bias[col];
-      f32x4 y;
+  // feature-major copy of the input tiles for the weight-gradient kernel: one 4-row × 1-column
+  // quad per task → one 8-B (bf16) / 16-B (fp32) store
+  if (TRAIN && !CVAE_DIAG_NOSTORE) {
+    auto copy_T = [&](const T* src, int ld, int ncols, T* dst) {
+      constexpr int RQ = R / 4;
+      for (int t = tid; t < ncols * RQ; t += CVAE_THREADS) {
+        const int c = t / RQ, q = t - c * RQ;
+        f32x4 v;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float t = fmaxf(v[i] + bias, 0.f);
-        if (row0 + i >= nrows || col >= L.N) t = 0.f;
-        y[i] = t;
-        if (t > 0.f) atomicOr(&Mask[(mi * R + row0 + i) * mw + (col >> 5)], 1u << (col & 31));
-      }
-      if (concat && col >= L.N) return;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        d1[(row0 + i) * ld1 + off1 + col] = to_t<T>(y[i]);
-        if (d2) d2[(row0 + i) * ld2 + off2 + col] = to_t<T>(y[i]);
-      }
-      if (TRAIN) {
-        if (g1) st4(g1 + (size_t)(goff1 + col) * Bp + b0 + row0, y);
-        if (g2) st4(g2 + (size_t)(goff2 + col) * Bp + b0 + row0, y);
-      }
-      if (MODE != RC_TRAIN && a.hc_out && mi == mC1 && col < L.N) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (row0 + i < nrows) a.hc_out[(size_t)(b0 + row0 + i) * H + col] = y[i];
+        for (int i = 0; i < 4; ++i) v[i] = to_f(src[(4 * q + i) * ld + c]);
+        gstore4(dst + (size_t)c * Bp + b0 + 4 * q, v);
       }
     };
-  };
-
-  // ---------------------------------------------------------------- condition encoder
-  if (MODE == RC_DECODE && a.hc_in) {
-    for (int e = tid; e < R * H; e += CVAE_THREADS) {
-      const int r = e / H, c = e - r * H;
-      Dec[r * P.sdec + Z + c] = to_t<T>(r < nrows ? a.hc_in[(size_t)(b0 + r) * H + c] : 0.f);
-    }
-    __syncthreads();
-  } else {
-    const LayerDev& L0 = net.L[lC0(net)];
-    dense<T, R>(Cin, P.scin, (const T*)L0.Wf, L0.Kp, L0.Np,
-                relu_epi(L0, mC0, Pb(0), P.sp, 0, nullptr, 0, 0, (T*)net.L[lC1(net)].xT, 0, nullptr, 0, false));
-    __syncthreads();
-    const LayerDev& L1 = net.L[lC1(net)];
-    dense<T, R>(Pb(0), P.sp, (const T*)L1.Wf, L1.Kp, L1.Np,
-                relu_epi(L1, mC1, Hc, P.shc, H, Dec, P.sdec, Z, (T*)net.L[lFC(net)].xT, H,
-                         (T*)net.L[lD(net, 0)].xT, Z, true));
-    __syncthreads();
+    copy_T(Cin, P.scin, net.Cp, (T*)net.L[lC0(net)].xT);
+    copy_T(Xin, P.sx, net.Ip, (T*)net.L[lE(net, 0)].xT);
   }
 
-  if (MODE != RC_DECODE) {
-    // ---------------------------------------------------------------- encoder
-    const T* in = Xin;
-    int ldin = P.sx;
-    for (int i = 0; i < net.n_enc; ++i) {
-      const LayerDev& L = net.L[lE(net, i)];
-      const bool last = i == net.n_enc - 1;
-      if (last)
-        dense<T, R>(in, ldin, (const T*)L.Wf, L.Kp, L.Np,
-                    relu_epi(L, mE(i), Hc, P.shc, 0, nullptr, 0, 0, (T*)net.L[lFC(net)].xT, 0, nullptr, 0, true));
-      else
-        dense<T, R>(in, ldin, (const T*)L.Wf, L.Kp, L.Np,
-                    relu_epi(L, mE(i), Pb(i & 1), P.sp, 0, nullptr, 0, 0, (T*)net.L[lE(net, i + 1)].xT, 0,
-                             nullptr, 0, false));
-      __syncthreads();
-      in = Pb(i & 1);
-      ldin = P.sp;
-    }
-    // ---------------------------------------------------------------- fc_mu ‖ fc_logvar
-    {
-      const LayerDev& L = net.L[lFC(net)];
-      dense<T, R>(Hc, P.shc, (const T*)L.Wf, L.Kp, L.Np, [&](int row0, int col, f32x4 v) {
-        const float bias = CVAE_DIAG_NOBIAS ? 0.f : L.bias[col];
+  const float Bf = (float)a.batch;
+  const float inv_BSD = 1.f / (Bf * (float)(S * D));
+  const float inv_2B = 1.f / (2.f * Bf);
+  const float inv_B = 1.f / Bf;
+  const float inv_BS1 = S > 1 ? 1.f / (Bf * (float)(S - 1)) : 0.f;
+  const float inv_BZ = 1.f / (Bf * (float)Z);
+  const bool use_start = a.w_start > 0.f, use_time = a.w_time > 0.f;  // Training_VAE.py:247, :256
+  const uint32_t* mkEl = Mask + (2 + net.n_enc - 1) * R * mw;  // last encoder layer
+  const uint32_t* mkC1 = Mask + 1 * R * mw;
+
+  // ---------------------------------------------------------------- the step interpreter
+  for (int si = 0; si < a.nsteps; ++si) {
+    // descriptors copied BY VALUE: read through a reference into global memory, every field
+    // would be re-loaded after each global store of the epilogue (the compiler cannot rule out
+    // aliasing), serialising scalar-load latencies inside the hot loop
+    const StepDesc st = a.steps[si];
+    const bool has_next = si + 1 < a.nsteps;
+    const void* const nW = a.steps[has_next ? si + 1 : si].W;
+    const int nKp = a.steps[has_next ? si + 1 : si].Kp;
+    const int nNp = a.steps[has_next ? si + 1 : si].Np;
+    T* const d1 = st.dst1 >= 0 ? buf(st.dst1) : nullptr;
+    T* const d2 = st.dst2 >= 0 ? buf(st.dst2) : nullptr;
+    const int ld1 = st.dst1 >= 0 ? ld_of(st.dst1) : 0;
+    const int ld2 = st.dst2 >= 0 ? ld_of(st.dst2) : 0;
+    T* const g1 = (T*)st.g1;
+    T* const g2 = (T*)st.g2;
+    const int kind = st.epi, N = st.N;
+    uint32_t* const mko = Mask + (st.mask_out >= 0 ? st.mask_out : 0) * R * mw;
+    const uint32_t* const mki = Mask + (st.mask_in >= 0 ? st.mask_in : 0) * R * mw;
+
+    const float* const bias = st.bias;
+#if CVAE_DIAG_SUB
+    g_sub_step = si;
+    SUBSTAMP(0);
+#endif
+    dense<T, R>(buf(st.xbuf), ld_of(st.xbuf), (const T*)st.W, st.Kp, st.Np, pre,
+                has_next ? (const T*)nW : (const T*)nullptr, nKp, nNp,
+                [&](int row, int f0, f32x4 v) {
+      const bool live = row < nrows;
+      f32x4 y;
+      if (kind == E_RELU) {  // forward hidden layer: ReLU, mask nibble, LDS dst(s), arena xT of consumers
+        const f32x4 b4 = gld<f32x4>(bias + f0);  // zero-padded: pad features come out 0
+        uint32_t nib = 0;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int row = row0 + i;
-          const float t = (row < nrows && col < L.N) ? v[i] + bias : 0.f;
-          MuLv[row * net.Zp2 + col] = t;
-          if (MODE == RC_FWD && row < nrows && col < L.N) {
-            if (col < Z) { if (a.mu_out) a.mu_out[(size_t)(b0 + row) * Z + col] = t; }
-            else if (a.lv_out) a.lv_out[(size_t)(b0 + row) * Z + col - Z] = t;
+          y[i] = live ? fmaxf(v[i] + b4[i], 0.f) : 0.f;
+          nib |= (y[i] > 0.f ? 1u : 0u) << i;
+        }
+        if (nib) atomicOr(mko + row * mw + (f0 >> 5), nib << (f0 & 31));
+        if (st.concat && f0 >= N) return;  // part of a concatenation: never write its pads
+        put4(d1 + row * ld1 + st.off1 + f0, y);
+        if (d2) put4(d2 + row * ld2 + st.off2 + f0, y);
+        if (g1) put4T(g1 + (size_t)(st.goff1 + f0) * Bp + b0 + row, Bp, y);
+        if (g2) put4T(g2 + (size_t)(st.goff2 + f0) * Bp + b0 + row, Bp, y);
+        if (st.hc_out && a.hc_out && live && f0 < N) gst<f32x4>(a.hc_out + (size_t)(b0 + row) * H + f0, y);
+      } else if (kind == E_BWD) {  // backward: mask with the producer's ReLU bits
+        const uint32_t nib = mask4(mki, mw, row, f0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) y[i] = (nib >> i) & 1u ? v[i] : 0.f;
+        if (d1) put4(d1 + row * ld1 + f0, y);
+        put4T(g1 + (size_t)f0 * Bp + b0 + row, Bp, y);
+      } else if (kind == E_FC) {  // mu ‖ logvar, fp32 in LDS
+        const f32x4 b4 = gld<f32x4>(bias + f0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) y[i] = live ? v[i] + b4[i] : 0.f;
+        *(f32x4*)(MuLv + row * net.Zp2 + f0) = y;
+        if (MODE == RC_FWD && live) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int c = f0 + i;
+            if (c < Z) { if (a.mu_out) gst<float>(a.mu_out + (size_t)(b0 + row) * Z + c, y[i]); }
+            else if (c < 2 * Z && a.lv_out) gst<float>(a.lv_out + (size_t)(b0 + row) * Z + c - Z, y[i]);
           }
         }
-      });
-      __syncthreads();
-    }
-    // ---------------------------------------------------------------- reparameterize (:199-206) + KL terms (:243)
-    {
+      } else if (kind == E_LOSS) {  // recon r = acc + bias (fp32); dL/dr → GL (LDS) + gT
+        const f32x4 b4 = gld<f32x4>(bias + f0);
+        // target x_rel from the resident input tile; GL overwrites it in place below
+        // (same lane, same elements), so no other reader is affected
+        const f32x4 xr = get4(Xin + row * P.sx + f0);
+        int s = f0 / D, d = f0 - s * D;
+        T* gcol = g1 + (size_t)f0 * Bp + b0 + row;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float gi = 0.f;
+          if (live && f0 + i < I) {
+            const float r = v[i] + b4[i];
+            const float diff = r - xr[i];
+            s_recon += diff * diff;
+            gi = a.w_recon * 2.f * diff * inv_BSD;
+            if (s == 0 && (d == 1 || d == 2) && use_start) {
+              s_start += diff * diff;
+              gi += a.w_start * 2.f * diff * inv_2B;
+            }
+            if (d == 0) {
+              Rch0[row * S + s] = r;
+              if (s == 0 && use_time) {
+                s_t0 += r * r;
+                gi += a.w_time * 2.f * r * inv_B;
+              }
+              Gd0[row * S + s] = gi;
+            }
+          }
+          y[i] = gi;
+          // the time channel (d == 0) is finished by the fix-up pass once its neighbours exist
+          if (!CVAE_DIAG_NOSTORE && (d != 0 || f0 + i >= I)) gst<T>(gcol + (size_t)i * Bp, to_t<T>(gi));
+          if (++d == D) { d = 0; ++s; }
+        }
+        put4(GL + row * P.sx + f0, y);  // d == 0 entries are overwritten by the fix-up pass
+      } else if (kind == E_RECON) {
+        if (!a.recon_out || !live) return;
+        const f32x4 b4 = gld<f32x4>(bias + f0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (f0 + i < I) gst<float>(a.recon_out + (size_t)(b0 + row) * I + f0 + i, v[i] + b4[i]);
+      } else if (kind == E_D0B) {  // decoder L0 backward: dz and the decoder's share of dh_c
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int c = f0 + i;
+          if (c < Z) Dz[row * Z + c] = v[i];
+          else if (c < Z + H) Dhc2[row * H + c - Z] = v[i];
+        }
+      } else {  // E_FCB: dh = G_fc·W_fc → [dh_traj ‖ dh_c(fc share)]   (H % 4 == 0: no straddle)
+        if (f0 < H) {
+          const uint32_t nib = mask4(mkEl, mw, row, f0);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) y[i] = (nib >> i) & 1u ? v[i] : 0.f;
+          put4(P1b + row * P.sp + f0, y);
+          put4T(g1 + (size_t)f0 * Bp + b0 + row, Bp, y);
+        } else if (f0 < 2 * H) {
+          const int c = f0 - H;
+          const uint32_t nib = mask4(mkC1, mw, row, c);
+          const f32x4 dh2 = *(const f32x4*)(Dhc2 + row * H + c);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) y[i] = (nib >> i) & 1u ? v[i] + dh2[i] : 0.f;
+          put4(Q + row * P.shc + c, y);
+          put4T(g2 + (size_t)c * Bp + b0 + row, Bp, y);
+        }
+      }
+    });
+    lds_barrier();
+#if CVAE_DIAG_SUB
+    SUBSTAMP(4);
+#endif
+
+    // ------------------------------------------------------------ element-wise phases after a step
+    if (kind == E_FC && MODE != RC_DECODE) {
+      // reparameterize (:199-206) + KL terms (:243)
       T* xd0 = (T*)net.L[lD(net, 0)].xT;
       for (int e = tid; e < R * Z; e += CVAE_THREADS) {
         const int r = e / Z, j = e - r * Z;
@@ -402,227 +640,75 @@ __global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowA
         if (r < nrows) {
           const float mu = MuLv[r * net.Zp2 + j], lv = MuLv[r * net.Zp2 + Z + j];
           sd = expf(0.5f * lv);
-          ep = a.eps ? a.eps[(size_t)(b0 + r) * Z + j] : philox_normal(a.seed, a.offset, (uint32_t)(b0 + r), (uint32_t)j);
+          ep = a.eps ? gld<float>(a.eps + (size_t)(b0 + r) * Z + j)
+                     : philox_normal(a.seed, a.offset, (uint32_t)(b0 + r), (uint32_t)j);
           z = mu + ep * sd;
           s_kl += 1.f + lv - mu * mu - expf(lv);
         }
         Eps[r * Z + j] = ep;
         Std[r * Z + j] = sd;
         Dec[r * P.sdec + j] = to_t<T>(z);
-        if (TRAIN && !CVAE_DIAG_NOSTORE) xd0[(size_t)j * Bp + b0 + r] = to_t<T>(z);
+        if (TRAIN && !CVAE_DIAG_NOSTORE) gst<T>(xd0 + (size_t)j * Bp + b0 + r, to_t<T>(z));
       }
-      __syncthreads();
-    }
-  } else {
-    if (!a.z_in) return;  // condition encoder only (cvae_condition)
-    for (int e = tid; e < R * Z; e += CVAE_THREADS) {
-      const int r = e / Z, j = e - r * Z;
-      Dec[r * P.sdec + j] = to_t<T>(r < nrows ? a.z_in[(size_t)(b0 + r) * Z + j] : 0.f);
-    }
-    __syncthreads();
-  }
-
-  // ---------------------------------------------------------------- decoder
-  const int nd = net.n_dec;
-  const T* din = Dec;
-  int lddin = P.sdec;
-  for (int i = 0; i < nd - 1; ++i) {
-    const LayerDev& L = net.L[lD(net, i)];
-    dense<T, R>(din, lddin, (const T*)L.Wf, L.Kp, L.Np,
-                relu_epi(L, mD(i), Pb(i & 1), P.sp, 0, nullptr, 0, 0, (T*)net.L[lD(net, i + 1)].xT, 0,
-                         nullptr, 0, false));
-    __syncthreads();
-    din = Pb(i & 1);
-    lddin = P.sp;
-  }
-  const LayerDev& LL = net.L[lD(net, nd - 1)];
-  const float Bf = (float)a.batch;
-  const float inv_BSD = 1.f / (Bf * (float)(S * D));
-  const float inv_2B = 1.f / (2.f * Bf);
-  const float inv_B = 1.f / Bf;
-  const float inv_BS1 = S > 1 ? 1.f / (Bf * (float)(S - 1)) : 0.f;
-  const float inv_BZ = 1.f / (Bf * (float)Z);
-  if (!TRAIN) {
-    dense<T, R>(din, lddin, (const T*)LL.Wf, LL.Kp, LL.Np, [&](int row0, int col, f32x4 v) {
-      if (col >= I || !a.recon_out) return;
-      const float bias = CVAE_DIAG_NOBIAS ? 0.f : LL.bias[col];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (row0 + i < nrows) a.recon_out[(size_t)(b0 + row0 + i) * I + col] = v[i] + bias;
-    });
-    return;
-  }
-  // loss epilogue: recon r = acc + bias stays fp32; dL/dr into GL (LDS) and gT(D_last)
-  {
-    T* gl = (T*)LL.gT;
-    const bool use_start = a.w_start > 0.f, use_time = a.w_time > 0.f;  // :247, :256
-    dense<T, R>(din, lddin, (const T*)LL.Wf, LL.Kp, LL.Np, [&](int row0, int col, f32x4 v) {
-      const float bias = CVAE_DIAG_NOBIAS ? 0.f : LL.bias[col];
-      const int s = col / D, d = col - s * D;
-      f32x4 g;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = row0 + i;
-        float gi = 0.f;
-        if (row < nrows && col < I) {
-          const float r = v[i] + bias;
-          // target x_rel from the resident input tile; GL overwrites it in place below
-          // (same lane, same element), so no other reader is affected
-          const float xr = to_f(Xin[row * P.sx + col]);
-          const float diff = r - xr;
-          s_recon += diff * diff;
-          gi = a.w_recon * 2.f * diff * inv_BSD;
-          if (s == 0 && (d == 1 || d == 2) && use_start) {
-            s_start += diff * diff;
-            gi += a.w_start * 2.f * diff * inv_2B;
-          }
-          if (d == 0) {
-            Rch0[row * S + s] = r;
-            if (s == 0 && use_time) {
-              s_t0 += r * r;
-              gi += a.w_time * 2.f * r * inv_B;
+      lds_barrier();
+    } else if (kind == E_LOSS) {
+      // time-monotonicity term: relu(r_s - r_{s+1}) (:261-262), ReLU'(0) = 0
+      T* gl = g1;
+      for (int e = tid; e < R * S; e += CVAE_THREADS) {
+        const int r = e / S, s = e - r * S;
+        float g = 0.f;
+        if (r < nrows) {
+          g = Gd0[r * S + s];
+          if (use_time) {
+            if (s < S - 1) {
+              const float u = Rch0[r * S + s] - Rch0[r * S + s + 1];
+              if (u > 0.f) {
+                g += a.w_time * inv_BS1;
+                s_relu += u;
+              }
             }
-            Gd0[row * S + s] = gi;
+            if (s > 0) {
+              const float u = Rch0[r * S + s - 1] - Rch0[r * S + s];
+              if (u > 0.f) g -= a.w_time * inv_BS1;
+            }
           }
         }
-        g[i] = gi;
+        GL[r * P.sx + s * D] = to_t<T>(g);
+        if (!CVAE_DIAG_NOSTORE) gst<T>(gl + (size_t)(s * D) * Bp + b0 + r, to_t<T>(g));
       }
-      if (d == 0 && col < I) return;  // time-channel gradient finished after the neighbours exist
-#pragma unroll
-      for (int i = 0; i < 4; ++i) GL[(row0 + i) * P.sx + col] = to_t<T>(g[i]);
-      st4(gl + (size_t)col * Bp + b0 + row0, g);
-    });
-    __syncthreads();
-    // time-monotonicity term: relu(r_s - r_{s+1}) (:261-262), ReLU'(0) = 0
-    for (int e = tid; e < R * S; e += CVAE_THREADS) {
-      const int r = e / S, s = e - r * S;
-      float g = 0.f;
-      if (r < nrows) {
-        g = Gd0[r * S + s];
-        if (use_time) {
-          if (s < S - 1) {
-            const float u = Rch0[r * S + s] - Rch0[r * S + s + 1];
-            if (u > 0.f) { g += a.w_time * inv_BS1; s_relu += u; }
-          }
-          if (s > 0) {
-            const float u = Rch0[r * S + s - 1] - Rch0[r * S + s];
-            if (u > 0.f) g -= a.w_time * inv_BS1;
+      lds_barrier();
+    } else if (kind == E_D0B) {
+      // reparameterisation + KL backward → G_fc = [dmu ‖ dlogvar] into P0 (the fc-backward input)
+      T* gfc = (T*)net.L[lFC(net)].gT;
+      for (int e = tid; e < R * net.Zp2; e += CVAE_THREADS) {
+        const int r = e / net.Zp2, c = e - r * net.Zp2;
+        float g = 0.f;
+        if (r < nrows && c < 2 * Z) {
+          const int j = c < Z ? c : c - Z;
+          const float dz = Dz[r * Z + j];
+          if (c < Z) {
+            g = a.w_kld * MuLv[r * net.Zp2 + j] * inv_BZ + dz;
+          } else {
+            const float lv = MuLv[r * net.Zp2 + Z + j];
+            g = a.w_kld * 0.5f * (expf(lv) - 1.f) * inv_BZ + dz * Eps[r * Z + j] * 0.5f * Std[r * Z + j];
           }
         }
+        P0b[r * P.sp + c] = to_t<T>(g);
+        if (!CVAE_DIAG_NOSTORE) gst<T>(gfc + (size_t)c * Bp + b0 + r, to_t<T>(g));
       }
-      GL[r * P.sx + s * D] = to_t<T>(g);
-      if (!CVAE_DIAG_NOSTORE) gl[(size_t)(s * D) * Bp + b0 + r] = to_t<T>(g);
-    }
-    __syncthreads();
-  }
-
-  // ---------------------------------------------------------------- backward
-  // dX = G·W with W from the transposed copy Wb[Kp][Np]; mask with the producer's ReLU bits.
-  auto bwd_epi = [&](int mi, T* dst, int ld, T* gdst) {
-    return [&, mi, dst, ld, gdst](int row0, int col, f32x4 v) {
-      f32x4 g;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        g[i] = mask_bit(Mask + mi * R * mw, mw, row0 + i, col) ? v[i] : 0.f;
-      if (dst) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) dst[(row0 + i) * ld + col] = to_t<T>(g[i]);
-      }
-      st4(gdst + (size_t)col * Bp + b0 + row0, g);
-    };
-  };
-  const T* gin = GL;
-  int ldg = P.sx;
-  int pp = 0;
-  for (int i = nd - 1; i >= 1; --i) {
-    const LayerDev& L = net.L[lD(net, i)];
-    dense<T, R>(gin, ldg, (const T*)L.Wb, L.Np, L.Kp,
-                bwd_epi(mD(i - 1), Pb(pp), P.sp, (T*)net.L[lD(net, i - 1)].gT));
-    __syncthreads();
-    gin = Pb(pp);
-    ldg = P.sp;
-    pp ^= 1;
-  }
-  {  // decoder L0 backward splits into dz and the decoder's share of dh_c
-    const LayerDev& L = net.L[lD(net, 0)];
-    dense<T, R>(gin, ldg, (const T*)L.Wb, L.Np, L.Kp, [&](int row0, int col, f32x4 v) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if (col < Z) Dz[(row0 + i) * Z + col] = v[i];
-        else if (col < Z + H) Dhc2[(row0 + i) * H + col - Z] = v[i];
-      }
-    });
-    __syncthreads();
-  }
-  {  // reparameterisation + KL backward → G_fc = [dmu ‖ dlogvar]
-    const LayerDev& L = net.L[lFC(net)];
-    T* gfc = (T*)L.gT;
-    T* P0 = Pb(0);
-    for (int e = tid; e < R * net.Zp2; e += CVAE_THREADS) {
-      const int r = e / net.Zp2, c = e - r * net.Zp2;
-      float g = 0.f;
-      if (r < nrows && c < 2 * Z) {
-        const int j = c < Z ? c : c - Z;
-        const float dz = Dz[r * Z + j];
-        if (c < Z) {
-          g = a.w_kld * MuLv[r * net.Zp2 + j] * inv_BZ + dz;
-        } else {
-          const float lv = MuLv[r * net.Zp2 + Z + j];
-          g = a.w_kld * 0.5f * (expf(lv) - 1.f) * inv_BZ + dz * Eps[r * Z + j] * 0.5f * Std[r * Z + j];
+      // pads of the two gradient targets of the fc backward must read as zero
+      if (net.Hp > H) {
+        for (int e = tid; e < R * (net.Hp - H); e += CVAE_THREADS) {
+          const int r = e / (net.Hp - H), c = H + e % (net.Hp - H);
+          P1b[r * P.sp + c] = to_t<T>(0.f);
+          Q[r * P.shc + c] = to_t<T>(0.f);
         }
       }
-      P0[r * P.sp + c] = to_t<T>(g);
-      if (!CVAE_DIAG_NOSTORE) gfc[(size_t)c * Bp + b0 + r] = to_t<T>(g);
+      lds_barrier();
     }
-    // pads of the two gradient targets of the fc backward must read as zero
-    if (net.Hp > H) {
-      for (int e = tid; e < R * (net.Hp - H); e += CVAE_THREADS) {
-        const int r = e / (net.Hp - H), c = H + e % (net.Hp - H);
-        Pb(1)[r * P.sp + c] = to_t<T>(0.f);
-        Q[r * P.shc + c] = to_t<T>(0.f);
-      }
-    }
-    __syncthreads();
-    // fc backward: dh = G_fc·W_fc → [dh_traj ‖ dh_c(fc share)]
-    T* ge = (T*)net.L[lE(net, net.n_enc - 1)].gT;
-    T* gc1 = (T*)net.L[lC1(net)].gT;
-    const uint32_t* mkE = Mask + mE(net.n_enc - 1) * R * mw;
-    const uint32_t* mkC = Mask + mC1 * R * mw;
-    dense<T, R>(P0, P.sp, (const T*)L.Wb, L.Np, L.Kp, [&](int row0, int col, f32x4 v) {
-      f32x4 g;
-      if (col < H) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) g[i] = mask_bit(mkE, mw, row0 + i, col) ? v[i] : 0.f;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) Pb(1)[(row0 + i) * P.sp + col] = to_t<T>(g[i]);
-        st4(ge + (size_t)col * Bp + b0 + row0, g);
-      } else if (col < 2 * H) {
-        const int c = col - H;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          g[i] = mask_bit(mkC, mw, row0 + i, c) ? v[i] + Dhc2[(row0 + i) * H + c] : 0.f;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) Q[(row0 + i) * P.shc + c] = to_t<T>(g[i]);
-        st4(gc1 + (size_t)c * Bp + b0 + row0, g);
-      }
-    });
-    __syncthreads();
+    stamp();
   }
-  {  // encoder backward (G of E0 is the last one needed: the input has no grad)
-    const T* g = Pb(1);
-    int p = 0;
-    for (int i = net.n_enc - 1; i >= 1; --i) {
-      const LayerDev& L = net.L[lE(net, i)];
-      dense<T, R>(g, P.sp, (const T*)L.Wb, L.Np, L.Kp,
-                  bwd_epi(mE(i - 1), i > 1 ? Pb(p) : nullptr, P.sp, (T*)net.L[lE(net, i - 1)].gT));
-      __syncthreads();
-      g = Pb(p);
-      p ^= 1;
-    }
-    // condition encoder L2 backward → G of condition L1
-    const LayerDev& L = net.L[lC1(net)];
-    dense<T, R>(Q, P.shc, (const T*)L.Wb, L.Np, L.Kp, bwd_epi(mC0, nullptr, 0, (T*)net.L[lC0(net)].gT));
-  }
+  if (!TRAIN) return;
 
   // ---------------------------------------------------------------- loss partial sums (deterministic order)
   s_recon = wave_sum(s_recon);
@@ -637,10 +723,10 @@ __global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowA
     Part[wave * 8 + 3] = s_t0;
     Part[wave * 8 + 4] = s_relu;
   }
-  __syncthreads();
+  lds_barrier();
   if (tid < 5) {
     float s = 0.f;
     for (int w = 0; w < CVAE_NW; ++w) s += Part[w * 8 + tid];
-    a.partials[blockIdx.x * 8 + tid] = s;
+    gst<float>(a.partials + blockIdx.x * 8 + tid, s);
   }
 }

@@ -19,6 +19,12 @@
 
 enum { PM_GRAD = 0, PM_ADAM = 1, PM_PACK = 2 };
 
+// Diagnostic builds only: skip refreshing the operand copies after Adam (wrong results) to
+// price the row-chain's cold weight reads.
+#ifndef CVAE_DIAG_NOWPACK
+#define CVAE_DIAG_NOWPACK 0
+#endif
+
 struct AdamArgs {
   float* params;      // flat fp32 master (state_dict order)
   float* m;
@@ -76,6 +82,7 @@ __device__ __forceinline__ void apply_weight(const LayerDev& L, int o, int i, fl
   } else if (MODE == PM_GRAD) {
     return;
   }
+  if (CVAE_DIAG_NOWPACK && MODE == PM_ADAM) return;
   ((T*)L.Wf)[(size_t)o * L.Kp + i] = to_t<T>(w);
   ((T*)L.Wb)[(size_t)i * L.Np + o] = to_t<T>(w);
 }
@@ -96,6 +103,7 @@ __device__ __forceinline__ void apply_bias(const LayerDev& L, int o, float g, co
   } else if (MODE == PM_GRAD) {
     return;
   }
+  if (CVAE_DIAG_NOWPACK && MODE == PM_ADAM) return;
   L.bias[o] = w;
 }
 
@@ -148,16 +156,15 @@ __global__ __launch_bounds__(CVAE_THREADS) void wgrad_kernel(NetDev net, const T
   const int nmine = nk > wave ? (nk - wave + CVAE_NW - 1) / CVAE_NW : 0;
   constexpr int PF = 4;
   V ga[PF][2], xb[PF][2];
-  auto load = [&](int u, int j) {
-    const int c = (wave + CVAE_NW * j) * KC;
+  auto load = [&](int u, int j) {  // unconditional, clamped to this wave's last chunk
+    const int c = (wave + CVAE_NW * min(j, nmine > 0 ? nmine - 1 : 0)) * KC;
 #pragma unroll
     for (int m = 0; m < 2; ++m) ga[u][m] = *(const V*)(gp[m] + c);
 #pragma unroll
     for (int n = 0; n < 2; ++n) xb[u][n] = *(const V*)(xp[n] + c);
   };
 #pragma unroll
-  for (int u = 0; u < PF; ++u)
-    if (u < nmine) load(u, u);
+  for (int u = 0; u < PF; ++u) load(u, u);
   for (int j0 = 0; j0 < nmine; j0 += PF) {
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
@@ -167,8 +174,8 @@ __global__ __launch_bounds__(CVAE_THREADS) void wgrad_kernel(NetDev net, const T
         for (int m = 0; m < 2; ++m)
 #pragma unroll
           for (int n = 0; n < 2; ++n) acc[m][n] = mfma_chunk(ga[u][m], xb[u][n], acc[m][n]);
-        if (j + PF < nmine) load(u, j + PF);
       }
+      load(u, j + PF);
     }
   }
   float* rw = red + wave * 32 * 33;

@@ -36,39 +36,57 @@ def param_keys(n_enc=4, n_dec=4):
     return out
 
 
-def _lin(x, p, name):
-    return x @ p[name + ".weight"].T + p[name + ".bias"]
+def bf16(a):
+    """Round-to-nearest-even to bfloat16, returned as float32 (the kernels' operand rounding)."""
+    a = np.ascontiguousarray(a, np.float32)
+    u = a.view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+    return r.astype(np.uint32).view(np.float32)
 
 
-def forward(p, x, eps, n_enc=4, n_dec=4, dt=np.float32):
-    """x: (B,S,D) absolute trajectories.  Returns (recon, mu, logvar, h_c, cache)."""
+def _ident(a):
+    return a
+
+
+def _lin(x, p, name, q=_ident):
+    return q(x) @ q(p[name + ".weight"]).T + p[name + ".bias"]
+
+
+def forward(p, x, eps, n_enc=4, n_dec=4, dt=np.float32, q=None):
+    """x: (B,S,D) absolute trajectories.  Returns (recon, mu, logvar, h_c, cache).
+
+    q: operand quantiser (``bf16`` emulates the bf16 kernel path exactly: GEMM operands and
+    stored activations rounded, accumulation and recon/loss in fp32, loss target = q(x_rel)).
+    """
+    q = q or _ident
     p = {k: v.astype(dt) for k, v in p.items()}
     x = x.astype(dt)
     B, S, D = x.shape
     start = x[:, 0, 1:3].copy()
     rel = x.copy()
     rel[:, :, 1:3] -= start[:, None, :]
-    c = {"start": start, "rel": rel, "eps": eps.astype(dt)}
+    rel = q(rel)
+    c = {"start": q(start), "rel": rel, "eps": eps.astype(dt), "q": q}
     a = rel.reshape(B, S * D)
     c["enc_in"] = [a]
     for i in range(n_enc):
-        a = np.maximum(_lin(a, p, f"encoder.{2 * i + 1}"), 0)
+        a = np.maximum(_lin(a, p, f"encoder.{2 * i + 1}", q), 0)
         c["enc_in"].append(a)
-    h1 = np.maximum(_lin(start, p, "condition_encoder.0"), 0)
-    hc = np.maximum(_lin(h1, p, "condition_encoder.2"), 0)
+    h1 = np.maximum(_lin(start, p, "condition_encoder.0", q), 0)
+    hc = np.maximum(_lin(h1, p, "condition_encoder.2", q), 0)
     c["hc1"], c["hc"] = h1, hc
     h = np.concatenate([a, hc], 1)
     c["h"] = h
-    mu, lv = _lin(h, p, "fc_mu"), _lin(h, p, "fc_logvar")
+    mu, lv = _lin(h, p, "fc_mu", q), _lin(h, p, "fc_logvar", q)
     std = np.exp(dt(0.5) * lv)
     z = mu + c["eps"] * std
     c["std"] = std
     d = np.concatenate([z, hc], 1)
     c["dec_in"] = [d]
     for i in range(n_dec - 1):
-        d = np.maximum(_lin(d, p, f"decoder.{2 * i}"), 0)
+        d = np.maximum(_lin(d, p, f"decoder.{2 * i}", q), 0)
         c["dec_in"].append(d)
-    r = _lin(d, p, f"decoder.{2 * (n_dec - 1)}").reshape(B, S, D)
+    r = _lin(d, p, f"decoder.{2 * (n_dec - 1)}", q).reshape(B, S, D)
     return r, mu, lv, hc, c
 
 
@@ -95,40 +113,43 @@ def dloss_drecon(r, x_rel, w=(0.1, 0.1, 1.0, 1.0), B_norm=None):
 
 
 def backward(p, c, r, mu, lv, w=(0.1, 0.1, 1.0, 1.0), n_enc=4, n_dec=4, dt=np.float32):
-    """Gradients of the total loss w.r.t. every parameter (dict keyed like state_dict)."""
+    """Gradients of the total loss w.r.t. every parameter (dict keyed like state_dict).
+
+    With the cache of ``forward(..., q=bf16)`` every stored gradient G and every GEMM operand
+    is rounded as the bf16 kernels round them (dz, the decoder's dh_c share, accumulations and
+    the loss stay fp32).
+    """
+    q = c.get("q", _ident)
     p = {k: v.astype(dt) for k, v in p.items()}
     B, S, D = r.shape
     Z = mu.shape[1]
     g = {}
-    G = dloss_drecon(r, c["rel"], w).reshape(B, S * D)
-    for i in reversed(range(n_dec)):
-        name = f"decoder.{2 * i}"
-        X = c["dec_in"][i]
+
+    def lin_grads(name, G, X):
+        G, X = q(G), q(X)
         g[name + ".weight"] = G.T @ X
         g[name + ".bias"] = G.sum(0)
-        dX = G @ p[name + ".weight"]
+        return G @ q(p[name + ".weight"])
+
+    G = dloss_drecon(r, c["rel"], w).reshape(B, S * D)
+    for i in reversed(range(n_dec)):
+        dX = lin_grads(f"decoder.{2 * i}", G, c["dec_in"][i])
         if i > 0:
             G = dX * (c["dec_in"][i] > 0)
     dz, dhc2 = dX[:, :Z], dX[:, Z:]
     dmu = w[1] * mu / (B * Z) + dz
     dlv = w[1] * 0.5 * (np.exp(lv) - 1) / (B * Z) + dz * c["eps"] * 0.5 * c["std"]
     h = c["h"]
-    g["fc_mu.weight"], g["fc_mu.bias"] = dmu.T @ h, dmu.sum(0)
-    g["fc_logvar.weight"], g["fc_logvar.bias"] = dlv.T @ h, dlv.sum(0)
-    dh = dmu @ p["fc_mu.weight"] + dlv @ p["fc_logvar.weight"]
+    dh = lin_grads("fc_mu", dmu, h) + lin_grads("fc_logvar", dlv, h)
     H = c["hc"].shape[1]
     G = dh[:, :H] * (c["enc_in"][n_enc] > 0)
     for i in reversed(range(n_enc)):
-        name = f"encoder.{2 * i + 1}"
-        X = c["enc_in"][i]
-        g[name + ".weight"] = G.T @ X
-        g[name + ".bias"] = G.sum(0)
+        dX = lin_grads(f"encoder.{2 * i + 1}", G, c["enc_in"][i])
         if i > 0:
-            G = (G @ p[name + ".weight"]) * (c["enc_in"][i] > 0)
+            G = dX * (c["enc_in"][i] > 0)
     Gc = (dh[:, H:] + dhc2) * (c["hc"] > 0)
-    g["condition_encoder.2.weight"], g["condition_encoder.2.bias"] = Gc.T @ c["hc1"], Gc.sum(0)
-    Gc1 = (Gc @ p["condition_encoder.2.weight"]) * (c["hc1"] > 0)
-    g["condition_encoder.0.weight"], g["condition_encoder.0.bias"] = Gc1.T @ c["start"], Gc1.sum(0)
+    Gc1 = lin_grads("condition_encoder.2", Gc, c["hc1"]) * (c["hc1"] > 0)
+    lin_grads("condition_encoder.0", Gc1, c["start"])
     return g
 
 

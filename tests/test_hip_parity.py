@@ -198,8 +198,11 @@ def _cfg2(cvae, dtype, B, seed=0):
     return ref, m, eng, x, eps
 
 
-@pytest.mark.parametrize("dtype,B,ltol,gtol", [("fp32", 64, 2e-5, 1e-4), ("bf16", 64, 2e-2, 5e-2),
-                                               ("bf16", 1024, 2e-2, 5e-2)])
+# bf16 vs the fp32 reference: the CPU bf16 emulation (tests/golden-free, oracle/cvae_np.py q=bf16)
+# shows rel-L2 up to 0.081 (encoder L1 weight, B=64) / 0.031 (B=1024) from operand rounding
+# alone; the tolerances below bound that, and the emulation test above pins the kernel tightly.
+@pytest.mark.parametrize("dtype,B,ltol,gtol", [("fp32", 64, 2e-5, 1e-4), ("bf16", 64, 2e-2, 1.2e-1),
+                                               ("bf16", 1024, 2e-2, 6e-2)])
 def test_cfg2_shape_vs_oracle(cvae, golden, dtype, B, ltol, gtol):
     ref, m, eng, x, eps = _cfg2(cvae, dtype, B)
     if dtype == "bf16":
@@ -270,3 +273,21 @@ def test_generate_absolute(cvae):
     rel, ab = m.generate(st, z=z.cuda())
     np.testing.assert_allclose((ab - rel)[:, :, 1:3].cpu().numpy(), st[:, None, :].expand(2, 10, 2).numpy(),
                                rtol=1e-6, atol=1e-4)
+
+
+@pytest.mark.parametrize("B", [64, 1024])
+def test_bf16_path_matches_bf16_emulation(cvae, B):
+    """The bf16 kernels against an exact CPU emulation of their rounding points
+    (oracle/cvae_np.py forward/backward with q=bf16): this pins the bf16 path tightly, while
+    test_cfg2_shape_vs_oracle bounds its distance from the fp32 reference."""
+    ref, m, eng, x, eps = _cfg2(cvae, "bf16", B)
+    x = x.to(torch.bfloat16).float()
+    loss = eng.forward_backward(x, eps=eps).cpu().numpy()
+    p = {k: v.numpy() for k, v in ref.state_dict().items()}
+    r, mu, lv, hc, c = cvae_np.forward(p, x.numpy(), eps.numpy(), q=cvae_np.bf16)
+    want = cvae_np.losses(r, c["rel"], mu, lv)
+    np.testing.assert_allclose(loss, want, rtol=2e-3, atol=1e-6)
+    gw = cvae_np.backward(p, c, r, mu, lv)
+    g = _grads(m, eng)
+    for k in cvae_np.param_keys():
+        assert rel_l2(g[k], gw[k]) < 2e-2, (k, rel_l2(g[k], gw[k]))
