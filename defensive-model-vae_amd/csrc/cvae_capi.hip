@@ -125,6 +125,12 @@ int build_plan(cvae_handle* h) {
   }
   h->nparams = off;
 
+  // all padded biases back to back (copied into LDS by the row-chain prologue)
+  n.nbias = 0;
+  for (int l = 0; l < n.n_layers; ++l) {
+    n.bias_off[l] = n.nbias;
+    n.nbias += n.L[l].Np;
+  }
   // LDS budget of the row-chain kernel
   const LdsPlan lp = lds_plan(n, h->R, h->tsize);
   h->lds_bytes = lp.total;
@@ -156,13 +162,15 @@ std::vector<StepDesc> build_steps(const NetDev& n, int mode) {
   auto fwd = [&](int l, int xbuf, int epi) {
     StepDesc s = blank();
     const LayerDev& L = n.L[l];
-    s.W = L.Wf; s.bias = L.bias; s.Kp = L.Kp; s.Np = L.Np; s.N = L.N; s.xbuf = xbuf; s.epi = epi;
+    s.W = L.Wf; s.bias = L.bias; s.bias_off = n.bias_off[l]; s.Kp = L.Kp; s.Np = L.Np; s.N = L.N;
+    s.xbuf = xbuf; s.epi = epi;
     return s;
   };
   auto bwd = [&](int l, int xbuf, int epi) {
     StepDesc s = blank();
     const LayerDev& L = n.L[l];
-    s.W = L.Wb; s.bias = n.zbias; s.Kp = L.Np; s.Np = L.Kp; s.N = L.K; s.xbuf = xbuf; s.epi = epi;
+    s.W = L.Wb; s.bias = n.zbias; s.bias_off = -1; s.Kp = L.Np; s.Np = L.Kp; s.N = L.K; s.xbuf = xbuf;
+    s.epi = epi;
     return s;
   };
   auto pb = [](int i) { return (i & 1) ? B_P1 : B_P0; };
@@ -247,8 +255,9 @@ int alloc_arena(cvae_handle* h) {
     LayerDev& L = n.L[l];
     lo[l].wf = take((int64_t)L.Np * L.Kp * ts);
     lo[l].wb = take((int64_t)L.Kp * L.Np * ts);
-    lo[l].bias = take((int64_t)L.Np * 4);
+    lo[l].bias = n.bias_off[l];  // planned in build_plan
   }
+  const int64_t bias_base = take((int64_t)n.nbias * 4);
   // activations: every layer has its own xT and gT (inputs that are concatenations
   // are written by their producers at column offsets)
   for (int l = 0; l < n.n_layers; ++l) {
@@ -270,11 +279,12 @@ int alloc_arena(cvae_handle* h) {
     LayerDev& L = n.L[l];
     L.Wf = h->arena + lo[l].wf;
     L.Wb = h->arena + lo[l].wb;
-    L.bias = (float*)(h->arena + lo[l].bias);
+    L.bias = (float*)(h->arena + bias_base) + lo[l].bias;
     L.xT = h->arena + lo[l].xT;
     L.gT = h->arena + lo[l].gT;
   }
   n.zbias = (const float*)(h->arena + zb_off);
+  n.bias_all = (const float*)(h->arena + bias_base);
   h->d_partials = (float*)(h->arena + part_off);
   h->d_tiles = (TileDesc*)(h->arena + tile_off);
   HIPCK(hipMemcpy(h->d_tiles, h->tiles.data(), h->tiles.size() * sizeof(TileDesc), hipMemcpyHostToDevice));

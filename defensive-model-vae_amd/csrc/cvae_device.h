@@ -43,6 +43,9 @@ struct NetDev {
   int Bp;                // arena row capacity
   int dtype;             // 0 fp32, 1 bf16
   const float* zbias;    // zeros (>= max Np floats): the "bias" of the dX GEMMs
+  const float* bias_all; // every layer's padded bias back to back (LayerDev::bias points into it)
+  int nbias;             // floats in bias_all (a multiple of 32)
+  int bias_off[CVAE_MAX_LAYERS];
   LayerDev L[CVAE_MAX_LAYERS];
 };
 

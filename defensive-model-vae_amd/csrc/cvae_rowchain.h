@@ -67,6 +67,8 @@ enum { E_RELU = 0, E_FC = 1, E_LOSS = 2, E_RECON = 3, E_BWD = 4, E_D0B = 5, E_FC
 struct StepDesc {
   const void* W;     // B operand [Np][Kp] (forward Wf or backward Wb)
   const float* bias; // [Np] (zeros for backward)
+  int bias_off;      // offset of this step's bias in the LDS bias copy (-1: zeros, backward)
+  int pad0_;
   void* g1;          // arena destination (feature-major), nullable
   void* g2;
   int Kp, Np;        // reduction / output dims (padded)
@@ -107,7 +109,7 @@ struct RowArgs {
 struct LdsPlan {
   int sx, sp, shc, sdec, scin;   // row strides (elements of T)
   int mw;                        // mask words per row
-  int oXin, oP0, oP1, oHc, oDec, oCin, oMuLv, oEps, oStd, oDz, oU, oRch0, oGd0, oStart, oRow, oMask, oPart;
+  int oXin, oP0, oP1, oHc, oDec, oCin, oMuLv, oEps, oStd, oDz, oU, oRch0, oGd0, oStart, oRow, oMask, oPart, oBias;
   int total;
 };
 
@@ -123,7 +125,7 @@ __host__ __device__ inline LdsPlan lds_plan(const NetDev& n, int R, int tsize) {
   p.shc = n.Hcp + pad;
   p.sdec = n.ZHp + pad;
   p.scin = n.Cp + pad;
-  p.mw = n.Hp / 32;
+  p.mw = n.Hp / 4;  // mask bytes per row (4 features per byte)
   int o = 0;
   auto take = [&](int bytes) { int r = o; o += rup(bytes, 16); return r; };
   p.oXin = take(R * p.sx * tsize);
@@ -142,8 +144,9 @@ __host__ __device__ inline LdsPlan lds_plan(const NetDev& n, int R, int tsize) {
   p.oGd0 = p.oU + R * n.S * 4;
   p.oStart = take(R * 2 * 4);
   p.oRow = take(R * 8);
-  p.oMask = take(n_masks(n) * R * p.mw * 4);
+  p.oMask = take(n_masks(n) * R * p.mw);
   p.oPart = take(CVAE_NW * 8 * 4);
+  p.oBias = take((n.nbias + 4) * 4);  // + 4 zero floats: the bias of backward steps
   p.total = o;
   return p;
 }
@@ -301,9 +304,9 @@ __device__ __forceinline__ void put4T(T* base, int Bp, f32x4 v) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) gst<T>(base + (size_t)i * Bp, to_t<T>(v[i]));
 }
-// the 4 ReLU bits of features f0..f0+3 (f0 % 4 == 0) of one row
-__device__ __forceinline__ uint32_t mask4(const uint32_t* mk, int mw, int row, int f0) {
-  return (mk[row * mw + (f0 >> 5)] >> (f0 & 31)) & 15u;
+// the 4 ReLU bits of features f0..f0+3 (f0 % 4 == 0) of one row: one byte per 4-feature group
+__device__ __forceinline__ uint32_t mask4(const uint8_t* mk, int mw, int row, int f0) {
+  return mk[row * mw + (f0 >> 2)];
 }
 
 template <typename T, int R, int MODE>
@@ -328,8 +331,9 @@ __global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowA
   float* const Dhc2 = (float*)(smem + P.oU);
   float* const Start = (float*)(smem + P.oStart);
   int64_t* const RowG = (int64_t*)(smem + P.oRow);
-  uint32_t* const Mask = (uint32_t*)(smem + P.oMask);
+  uint8_t* const Mask = (uint8_t*)(smem + P.oMask);
   float* const Part = (float*)(smem + P.oPart);
+  float* const BiasL = (float*)(smem + P.oBias);
   // LDS buffer by id (a select chain on a uniform value: no runtime-indexed pointer array)
   auto buf = [&](int id) -> T* {
     return id == B_XIN ? Xin : id == B_P0 ? P0b : id == B_P1 ? P1b : id == B_HC ? Hc : id == B_DEC ? Dec : Cin;
@@ -372,7 +376,9 @@ __global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowA
     zero(Hc, R * P.shc * (int)sizeof(T));
     zero(Dec, R * P.sdec * (int)sizeof(T));
     zero(Cin, R * P.scin * (int)sizeof(T));
-    zero(Mask, rup(n_masks(net) * R * mw * 4, 16));
+    zero(Mask, rup(n_masks(net) * R * mw, 16));
+    for (int e = tid; e < net.nbias / 4 + 1; e += CVAE_THREADS)
+      ((f32x4*)BiasL)[e] = e < net.nbias / 4 ? gld<f32x4>(net.bias_all + 4 * e) : f32x4{0.f, 0.f, 0.f, 0.f};
     for (int r = tid; r < R; r += CVAE_THREADS) {
       float s0 = 0.f, s1 = 0.f;
       int64_t g = 0;
@@ -493,8 +499,8 @@ __global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowA
   const float inv_BS1 = S > 1 ? 1.f / (Bf * (float)(S - 1)) : 0.f;
   const float inv_BZ = 1.f / (Bf * (float)Z);
   const bool use_start = a.w_start > 0.f, use_time = a.w_time > 0.f;  // Training_VAE.py:247, :256
-  const uint32_t* mkEl = Mask + (2 + net.n_enc - 1) * R * mw;  // last encoder layer
-  const uint32_t* mkC1 = Mask + 1 * R * mw;
+  const uint8_t* mkEl = Mask + (2 + net.n_enc - 1) * R * mw;  // last encoder layer
+  const uint8_t* mkC1 = Mask + 1 * R * mw;
 
   // ---------------------------------------------------------------- the step interpreter
   for (int si = 0; si < a.nsteps; ++si) {
@@ -513,28 +519,30 @@ __global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowA
     T* const g1 = (T*)st.g1;
     T* const g2 = (T*)st.g2;
     const int kind = st.epi, N = st.N;
-    uint32_t* const mko = Mask + (st.mask_out >= 0 ? st.mask_out : 0) * R * mw;
-    const uint32_t* const mki = Mask + (st.mask_in >= 0 ? st.mask_in : 0) * R * mw;
+    uint8_t* const mko = Mask + (st.mask_out >= 0 ? st.mask_out : 0) * R * mw;
+    const uint8_t* const mki = Mask + (st.mask_in >= 0 ? st.mask_in : 0) * R * mw;
 
-    const float* const bias = st.bias;
 #if CVAE_DIAG_SUB
     g_sub_step = si;
     SUBSTAMP(0);
 #endif
+    // the step's bias lives in LDS (copied once in the prologue): the epilogue issues no
+    // global loads, so it never waits behind the weight prefetch (vmcnt retires in order)
+    const float* const biasL = BiasL + (st.bias_off >= 0 ? st.bias_off : net.nbias);
     dense<T, R>(buf(st.xbuf), ld_of(st.xbuf), (const T*)st.W, st.Kp, st.Np, pre,
                 has_next ? (const T*)nW : (const T*)nullptr, nKp, nNp,
                 [&](int row, int f0, f32x4 v) {
+      const f32x4 b4 = *(const f32x4*)(biasL + f0);
       const bool live = row < nrows;
       f32x4 y;
       if (kind == E_RELU) {  // forward hidden layer: ReLU, mask nibble, LDS dst(s), arena xT of consumers
-        const f32x4 b4 = gld<f32x4>(bias + f0);  // zero-padded: pad features come out 0
         uint32_t nib = 0;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          y[i] = live ? fmaxf(v[i] + b4[i], 0.f) : 0.f;
+          y[i] = live ? fmaxf(v[i] + b4[i], 0.f) : 0.f;  // zero-padded bias: pad features come out 0
           nib |= (y[i] > 0.f ? 1u : 0u) << i;
         }
-        if (nib) atomicOr(mko + row * mw + (f0 >> 5), nib << (f0 & 31));
+        mko[row * mw + (f0 >> 2)] = (uint8_t)nib;  // this lane owns (row, f0..f0+3): no atomics
         if (st.concat && f0 >= N) return;  // part of a concatenation: never write its pads
         put4(d1 + row * ld1 + st.off1 + f0, y);
         if (d2) put4(d2 + row * ld2 + st.off2 + f0, y);
@@ -548,7 +556,6 @@ __global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowA
         if (d1) put4(d1 + row * ld1 + f0, y);
         put4T(g1 + (size_t)f0 * Bp + b0 + row, Bp, y);
       } else if (kind == E_FC) {  // mu ‖ logvar, fp32 in LDS
-        const f32x4 b4 = gld<f32x4>(bias + f0);
 #pragma unroll
         for (int i = 0; i < 4; ++i) y[i] = live ? v[i] + b4[i] : 0.f;
         *(f32x4*)(MuLv + row * net.Zp2 + f0) = y;
@@ -561,7 +568,6 @@ __global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowA
           }
         }
       } else if (kind == E_LOSS) {  // recon r = acc + bias (fp32); dL/dr → GL (LDS) + gT
-        const f32x4 b4 = gld<f32x4>(bias + f0);
         // target x_rel from the resident input tile; GL overwrites it in place below
         // (same lane, same elements), so no other reader is affected
         const f32x4 xr = get4(Xin + row * P.sx + f0);
@@ -596,7 +602,6 @@ __global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowA
         put4(GL + row * P.sx + f0, y);  // d == 0 entries are overwritten by the fix-up pass
       } else if (kind == E_RECON) {
         if (!a.recon_out || !live) return;
-        const f32x4 b4 = gld<f32x4>(bias + f0);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           if (f0 + i < I) gst<float>(a.recon_out + (size_t)(b0 + row) * I + f0 + i, v[i] + b4[i]);
