@@ -95,6 +95,7 @@ def main():
     torch.cuda.set_device(dev)
 
     from cvae_amd import ConditionalTrajectoryVAE
+    from cvae_amd.dist import DataParallelStep
 
     B, S, D, Z, H = args.batch, args.seq_len, args.dim, args.latent, args.hidden
     torch.manual_seed(0)
@@ -102,15 +103,11 @@ def main():
     eng = model.attach(dtype=args.dtype, max_batch=B, device=dev, seed=4321 + rank)
     x = torch.randn(B, S, D, generator=torch.Generator().manual_seed(1234 + rank))
     x = eng.as_input(x)  # resident in HBM, operand dtype
-    inv_world = 1.0 / world
+    dp = DataParallelStep(eng)  # N=1: fused train_step; N>1: fwd/bwd → RCCL all-reduce → Adam
+    dp.broadcast_params()
 
     def step():
-        if world == 1:
-            eng.train_step(x)
-        else:
-            eng.forward_backward(x)
-            dist.all_reduce(eng.grads)
-            eng.adam_step(inv_world)
+        dp.step(x, batch=B, global_batch=B * world)
 
     for _ in range(args.warmup):
         step()

@@ -1,0 +1,156 @@
+"""The reference training loop (Training_VAE.py:316-394) on the HIP engine.
+
+Same inputs, prints, loss history, CSV and checkpoint as the reference ``__main__`` in
+``mode='training'``; what changes is underneath:
+
+* the dataset is uploaded once and stays resident in HBM; each step hands the kernel the
+  batch's row indices and the gather + relative transform (:345-348) happen in its loader;
+* the step (zero_grad → forward → conditional_vae_loss → backward → Adam, :351-363) is ONE
+  ``cvae_train_step`` call (two kernels) — or fwd/bwd → RCCL all-reduce → Adam under DP;
+* the five ``loss.item()`` per step (:366-370) become a device accumulator read once per
+  epoch, so the step loop never synchronises with the host.
+
+RNG: ``torch.utils.data.DataLoader(shuffle=True)`` over row indices consumes the global CPU
+generator exactly as the reference's loader does.  ``eps="host"`` draws each step's
+``randn(B, Z)`` from that same generator (the reference's ``randn_like`` at :205 on CPU), so a
+seeded run replays the reference's stream; ``eps="philox"`` generates eps in-kernel instead
+(Philox4x32-10, keyed by the engine seed and step) and is the throughput mode.
+
+Outputs (Training_VAE.py:373-394, Tools.py:747-771): one line per epoch in the reference
+format; ``loss_history`` (per-epoch means) and its weighted copy; the loss CSV (header = the
+five keys, one row per epoch) next to ``loss_save_path``; ``torch.save`` of the 24-key
+state_dict (CPU tensors).  The matplotlib figure of ``plot_losses`` is not drawn.
+"""
+from __future__ import annotations
+
+import csv
+import os
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from . import dist as dp
+from .model import ConditionalTrajectoryVAE, TrajectoryDataset
+
+LOSS_KEYS = ("total_loss", "recon_loss", "kld_loss", "start_loss", "time_loss")  # :337
+
+
+class _Rows(torch.utils.data.Dataset):
+    """Row indices 0..n-1: the DataLoader then draws the reference's permutation, not the data."""
+
+    def __init__(self, n):
+        self.n = n
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        return i
+
+
+def epoch_line(epoch, means):
+    """Training_VAE.py:373 print format."""
+    t, r, k, s, ti = means
+    return (f"Epoch {epoch + 1}: Loss={t:.4f}, Recon={r:.4f}, KLD={k:.4f}, Start={s:.4f}, Time={ti:.4f}")
+
+
+def weighted_history(loss_history, weights):
+    """Training_VAE.py:385-388: component curves scaled by their loss weights."""
+    out = {k: list(v) for k, v in loss_history.items()}
+    for key, w in zip(LOSS_KEYS[1:], weights):
+        out[key] = [x * w for x in out[key]]
+    return out
+
+
+def save_loss_csv(loss_history, save_path):
+    """Tools.py:747-771: ``<save_path stem>.csv``, header = keys, one row per epoch."""
+    csv_path = os.path.splitext(save_path)[0] + ".csv"
+    d = os.path.dirname(csv_path)
+    if d:
+        os.makedirs(d, exist_ok=True)
+    keys = list(loss_history.keys())
+    with open(csv_path, "w", newline="", encoding="utf-8") as f:
+        w = csv.writer(f)
+        w.writerow(keys)
+        for i in range(len(loss_history[keys[0]])):
+            w.writerow([loss_history[k][i] for k in keys])
+    return csv_path
+
+
+def cpu_state_dict(model):
+    """The 24-key state_dict as CPU fp32 tensors (loadable by Tools.py:39-41 on any device)."""
+    return OrderedDict((k, v.detach().to("cpu", torch.float32).clone()) for k, v in model.state_dict().items())
+
+
+def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidden_dim=128,
+          weights=(0.1, 0.1, 1.0, 1.0), model_save_path=None, loss_save_path=None, dtype="fp32",
+          eps="host", device=None, seed=None, engine_seed=0, log=print, model=None):
+    """Train like ``python Training_VAE.py`` (mode='training').
+
+    data: path to the (N, seq_len, dim) ``.npy`` (TrajectoryDataset, :105-115) or an array.
+    weights: (recon, kld, start, time) — the values of :300-306.
+    seed: if given, ``torch.manual_seed(seed)`` first (the reference leaves it unseeded).
+    Under ``torch.distributed`` every rank runs this with the same arguments; batch_size is
+    then per rank (global batch = batch_size · world) and rank 0 logs and saves.
+
+    Returns (model, loss_history, weighted_loss_history).
+    """
+    if seed is not None:
+        torch.manual_seed(seed)
+    rank, world_size = dp.world()
+    if isinstance(data, (str, os.PathLike)):
+        arr = TrajectoryDataset(data).data
+    else:
+        arr = np.ascontiguousarray(np.asarray(data, dtype=np.float32))
+    n = len(arr)
+    if rank == 0 and log:
+        log(f"Training parameters: seq_len={seq_len}, latent_dim={latent_dim}, batch_size={batch_size}, lr={lr}")
+        log(f"Dataset size: {n} trajectories")
+    if model is None:
+        model = ConditionalTrajectoryVAE(seq_len, dim, latent_dim, hidden_dim)  # init from the global RNG
+    eng = model.__dict__.get("_engine") or model.attach(dtype=dtype, max_batch=batch_size, device=device,
+                                                        seed=engine_seed)
+    if eng.max_batch < batch_size:
+        raise ValueError(f"engine max_batch {eng.max_batch} < batch_size {batch_size}")
+    eng.set_optimizer(lr=lr)
+    eng.weights = tuple(float(w) for w in weights)
+    step = dp.DataParallelStep(eng)
+    step.broadcast_params()
+    x_dev = eng.as_input(torch.from_numpy(arr))          # resident for the whole run
+    Z = latent_dim
+    gb = batch_size * world_size
+    loader = torch.utils.data.DataLoader(_Rows(n), batch_size=gb, shuffle=True)
+    eng.loss_accum.zero_()
+    loss_history = {k: [] for k in LOSS_KEYS}
+    for epoch in range(epochs):
+        for rows in loader:                               # (:340) one global batch
+            g = rows.numel()
+            lo, hi = dp.split_rows(g, world_size, rank)
+            e = None
+            if eps == "host":
+                e_all = torch.randn(g, Z)                 # reparameterize's randn_like (:205)
+                e = e_all[lo:hi]
+            elif eps != "philox":
+                raise ValueError("eps must be 'host' or 'philox'")
+            step.step(x_dev, idx=rows[lo:hi], eps=e, batch=hi - lo, global_batch=g)
+        sums = step.epoch_loss_sums().double().cpu().numpy()  # the only host sync of the epoch
+        means = sums / n
+        for k, v in zip(LOSS_KEYS, means):
+            loss_history[k].append(float(v))
+        if rank == 0 and log:
+            log(epoch_line(epoch, means))
+    weighted = weighted_history(loss_history, weights)
+    if rank == 0:
+        if loss_save_path:
+            p = save_loss_csv(weighted, loss_save_path)
+            if log:
+                log(f"Loss history saved to CSV: {p}")
+        if model_save_path:
+            d = os.path.dirname(model_save_path)
+            if d:
+                os.makedirs(d, exist_ok=True)
+            torch.save(cpu_state_dict(model), model_save_path)
+            if log:
+                log(f"Model saved to {model_save_path}")
+    return model, loss_history, weighted

@@ -1,0 +1,86 @@
+"""CPU stand-in for ``CVAEEngine`` built on the oracle — TEST INFRASTRUCTURE ONLY.
+
+It exposes the engine surface ``cvae_amd.train`` and ``cvae_amd.dist`` drive (flat fp32
+params/grads/m/v, device-style loss accumulators, train_step / forward_backward / adam_step),
+so the host logic (loader RNG, DP sharding, gradient weighting, epoch bookkeeping) can be
+tested on the CPU under gloo.  The arithmetic is the oracle's torch-CPU restatement of
+Training_VAE.py (oracle/cvae_oracle.py); Adam follows torch ``_single_tensor_adam`` op order
+on the flat buffer, which is elementwise-identical to the per-tensor optimizer.
+"""
+import torch
+
+from oracle.cvae_oracle import DEFAULT_WEIGHTS, OracleCVAE, oracle_loss, relative
+
+
+class OracleEngine:
+    def __init__(self, model, max_batch=1 << 30):
+        self.model = model
+        self.max_batch = max_batch
+        self.plist = list(model.parameters())
+        self.params = torch.cat([p.detach().reshape(-1) for p in self.plist]).clone()
+        n = self.params.numel()
+        self.grads = torch.zeros(n)
+        self.m = torch.zeros(n)
+        self.v = torch.zeros(n)
+        self.loss = torch.zeros(5)
+        self.loss_accum = torch.zeros(5)
+        self.step_count = 0
+        self.lr, self.betas, self.eps = 1e-3, (0.9, 0.999), 1e-8
+        self.weights = DEFAULT_WEIGHTS
+        self.calls = []
+
+    # --- engine surface
+    def set_optimizer(self, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
+        self.lr, self.betas, self.eps = lr, betas, eps
+
+    def as_input(self, x):
+        return torch.as_tensor(x, dtype=torch.float32).contiguous()
+
+    def pack(self):
+        o = 0
+        with torch.no_grad():
+            for p in self.plist:
+                p.copy_(self.params[o:o + p.numel()].view_as(p))
+                o += p.numel()
+
+    def forward_backward(self, x, idx=None, eps=None, batch=None, weights=None, accumulate=True):
+        self.calls.append(("fb", None if idx is None else idx.clone(), batch))
+        rows = x[idx] if idx is not None else x[:batch]
+        rel, start = relative(rows)
+        for p in self.plist:
+            p.grad = None
+        mu, lv, hc = self.model.encode(rel, start)
+        recon = self.model.decode(self.model.reparameterize(mu, lv, eps), hc)
+        w = dict(zip(("recon_weight", "kld_weight", "start_weight", "time_weight"), weights or self.weights))
+        ls = oracle_loss(recon, rel, mu, lv, hc, **w)
+        ls[0].backward()
+        self.grads.copy_(torch.cat([p.grad.reshape(-1) for p in self.plist]))
+        self.loss.copy_(torch.stack([v.detach() for v in ls]))
+        if accumulate:
+            self.loss_accum += self.loss * float(rows.shape[0])
+        return self.loss
+
+    def adam_step(self, grad_scale=1.0):
+        self.step_count += 1
+        b1, b2 = self.betas
+        g = self.grads * grad_scale if grad_scale != 1.0 else self.grads
+        self.m.lerp_(g, 1 - b1)
+        self.v.mul_(b2).addcmul_(g, g, value=1 - b2)
+        bc1 = 1 - b1 ** self.step_count
+        bc2 = 1 - b2 ** self.step_count
+        denom = (self.v.sqrt() / (bc2 ** 0.5)).add_(self.eps)
+        self.params.addcdiv_(self.m, denom, value=-(self.lr / bc1))
+        self.pack()
+
+    def train_step(self, x, idx=None, eps=None, batch=None, weights=None, accumulate=True):
+        self.forward_backward(x, idx=idx, eps=eps, batch=batch, weights=weights, accumulate=accumulate)
+        self.adam_step()
+        return self.loss
+
+
+class OracleModel(OracleCVAE):
+    """An OracleCVAE already 'attached' to an OracleEngine (what cvae_amd.train expects)."""
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.__dict__["_engine"] = OracleEngine(self)

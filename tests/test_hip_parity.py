@@ -291,3 +291,26 @@ def test_bf16_path_matches_bf16_emulation(cvae, B):
     g = _grads(m, eng)
     for k in cvae_np.param_keys():
         assert rel_l2(g[k], gw[k]) < 2e-2, (k, rel_l2(g[k], gw[k]))
+
+
+def test_train_loop_end_to_end_traj20(cvae, golden, tmp_path):
+    """cvae_amd.train (the Training_VAE.py __main__ loop) on device vs the reference's seeded run.
+
+    Same seed → same init, DataLoader order and host eps stream; epoch means of the reference's
+    per-step losses (:366-373) and its final parameters after 20 Adam steps.
+    """
+    from cvae_amd.train import LOSS_KEYS, train
+    d = golden("traj20_sce1.npz")
+    x = golden("sce_fixed.npz")["sce1_x"]
+    model, hist, _ = train(x, 10, 3, 8, batch_size=int(d["batch_size"]), epochs=10, weights=W,
+                           seed=int(d["seed"]), eps="host", log=None, dtype="fp32",
+                           model_save_path=str(tmp_path / "m.pth"))
+    steps = d["losses"]
+    want = np.array([(steps[2 * e] * 32 + steps[2 * e + 1] * 6) / 38 for e in range(10)])
+    got = np.array([hist[k] for k in LOSS_KEYS]).T
+    np.testing.assert_allclose(got[:, 0], want[:, 0], rtol=1e-4)
+    np.testing.assert_allclose(got, want, rtol=2e-3, atol=1e-6)
+    sd = torch.load(tmp_path / "m.pth", weights_only=True)
+    assert len(sd) == 24
+    for k in cvae_np.param_keys():
+        assert rel_l2(sd[k].numpy(), d["final/" + k]) < 1e-4, k
