@@ -30,6 +30,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 PEAK = {"bf16": 2500.0, "fp32": 157.3}  # dense TFLOP/s, MI355X_MICROARCH.md chip table
+HBM_PEAK_GBS = 8000.0                      # HBM3E peak, MI355X_MICROARCH.md
 
 
 def fwd_macs(S, D, Z, H, C=2):
@@ -44,6 +45,49 @@ def flops_per_traj(S, D, Z, H, C=2):
     return {"total": 2 * (3 * F - C * H - I * H),
             "rowchain": 2 * F + 2 * (F - C * H - I * H),  # forward + every dX
             "wgrad": 2 * F}                                # every dW
+
+
+def bytes_per_traj(S, D, Z, H, tsize, C=2, n_enc=4, n_dec=4):
+    """Algorithmic HBM bytes per trajectory: the row chain reads x and writes every
+    layer input xT and pre-activation gradient gT once (unpadded); the dW kernel reads them once."""
+    I = S * D
+    ks = [C, H] + [I] + [H] * (n_enc - 1) + [2 * H] + [Z + H] + [H] * (n_dec - 1)
+    ns = [H, H] + [H] * n_enc + [2 * Z] + [H] * (n_dec - 1) + [I]
+    arena = (sum(ks) + sum(ns)) * tsize
+    return {"rowchain": I * tsize + arena, "wgrad": arena}
+
+
+ADAM_BYTES_PER_PARAM = 28  # p, m, v read + write (24 B) + bf16/fp32 operand copies W, Wᵀ written
+
+
+def roofline(kernel, avg_ms, flop, nbytes, dtype, traffic=None):
+    """Both ceilings of one kernel; the binding one (longer time at peak) becomes the headline."""
+    t = avg_ms * 1e-3
+    mfma = {"achieved": flop / t / 1e12, "peak": PEAK[dtype], "unit": "TFLOP/s"}
+    hbm = {"achieved": nbytes / t / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+    bound = "hbm" if nbytes / (HBM_PEAK_GBS * 1e9) > flop / (PEAK[dtype] * 1e12) else "mfma"
+    head, other = (hbm, mfma) if bound == "hbm" else (mfma, hbm)
+    return {"bound": bound, "kernel": kernel, "achieved": round(head["achieved"], 3), "peak": head["peak"],
+            "unit": head["unit"], "frac": round(head["achieved"] / head["peak"], 6),
+            "traffic": traffic, "flop_per_launch": flop, "bytes_per_launch": nbytes,
+            "avg_launch_ms": round(avg_ms, 5),
+            "other_ceiling": {"bound": "mfma" if bound == "hbm" else "hbm",
+                              "achieved": round(other["achieved"], 3), "peak": other["peak"],
+                              "unit": other["unit"], "frac": round(other["achieved"] / other["peak"], 6)}}
+
+
+def measured_traffic(path, kernel, batch, dtype):
+    """Per-launch 2·FETCH_SIZE + WRITE_SIZE of `kernel` from a committed rocprofv3 pass, if it
+    was taken on this configuration (scripts/pmc_traffic.py); else None."""
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if t.get("config") != {"batch": batch, "dtype": dtype}:
+        return None
+    k = t.get("kernels", {}).get(kernel)
+    return None if k is None else k["traffic_bytes"]
 
 
 def cpu_baseline(B, S, D, Z, H, seconds):
@@ -80,8 +124,8 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-bytes", type=float, default=None,
-                    help="HBM bytes per launch of the dominant kernel from a rocprofv3 --pmc pass")
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="per-launch HBM traffic from rocprofv3 --pmc passes (scripts/pmc_traffic.py)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -133,15 +177,16 @@ def main():
 
     if rank == 0:
         fl = flops_per_traj(S, D, Z, H)
-        per_launch = {"rowchain": fl["rowchain"] * B, "wgrad": fl["wgrad"] * B, "wgrad_adam": fl["wgrad"] * B}
-        dom = max((k for k in kt if k in per_launch), key=lambda k: kt[k][0])
-        avg_ms = kt[dom][0]
-        achieved = per_launch[dom] / (avg_ms * 1e-3) / 1e12
-        roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3), "peak": PEAK[args.dtype],
-                "unit": "TFLOP/s", "frac": round(achieved / PEAK[args.dtype], 6),
-                "traffic": args.traffic_bytes,
-                "flop_per_launch": per_launch[dom], "avg_launch_ms": round(avg_ms, 5),
-                "kernels_ms": {k: round(v[0], 5) for k, v in kt.items()}}
+        tsize = 2 if args.dtype == "bf16" else 4
+        bt = bytes_per_traj(S, D, Z, H, tsize)
+        n_par = eng.n_params
+        flop = {"rowchain": fl["rowchain"] * B, "wgrad": fl["wgrad"] * B, "wgrad_adam": fl["wgrad"] * B}
+        nbytes = {"rowchain": bt["rowchain"] * B, "wgrad": bt["wgrad"] * B + 4 * n_par,
+                  "wgrad_adam": bt["wgrad"] * B + ADAM_BYTES_PER_PARAM * n_par}
+        dom = max((k for k in kt if k in flop), key=lambda k: kt[k][0])
+        traffic = measured_traffic(args.traffic_file, dom, B, args.dtype)
+        roof = roofline(dom, kt[dom][0], flop[dom], nbytes[dom], args.dtype, traffic)
+        roof["kernels_ms"] = {k: round(v[0], 5) for k, v in kt.items()}
         value = world * B * args.steps / t
         res = {"metric": "trajectories/sec per ELBO step, batch=1024 seq_len=100; 1/2/4/8 MI355X",
                "value": round(value, 1), "unit": "trajectories/s", "n_gpus": world, "steps": args.steps,

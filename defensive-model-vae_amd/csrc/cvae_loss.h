@@ -48,5 +48,5 @@ __global__ __launch_bounds__(CVAE_THREADS) void loss_partial_kernel(const float*
 }
 
 __global__ void loss_finish_kernel(LossArgs la, int S, int D, int Z) {
-  if (threadIdx.x == 0) finish_loss(la, S, D, Z);
+  if (threadIdx.x < 64) finish_loss(la, S, D, Z);
 }

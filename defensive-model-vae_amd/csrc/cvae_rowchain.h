@@ -31,8 +31,19 @@
 
 enum { RC_TRAIN = 0, RC_FWD = 1, RC_DECODE = 2 };
 
-// batch rows per workgroup (the MFMA N dimension of the swapped GEMM: a multiple of 16)
-template <typename T> struct RowsPerTile { static constexpr int R = 16; };
+// Batch rows per workgroup.  The swapped GEMM's MFMA N dimension is 16 batch columns; with
+// R < 16 (4 or 8) lanes r16 >= R recompute row r16 % R — identical values to identical
+// addresses — which wastes MFMA columns but multiplies the workgroups of a launch by 16/R:
+// the chain is latency-bound, so more concurrent row tiles is what raises throughput.
+#ifndef CVAE_ROWS
+#define CVAE_ROWS 16
+#endif
+template <typename T> struct RowsPerTile { static constexpr int R = CVAE_ROWS; };
+static_assert(CVAE_ROWS == 4 || CVAE_ROWS == 8 || CVAE_ROWS % 16 == 0, "row tile: 4, 8 or a multiple of 16");
+
+// LDS row of MFMA tile m, lane row r16
+template <int R>
+__device__ __forceinline__ int tile_row(int m, int r16) { return R >= 16 ? m * 16 + r16 : (r16 & (R - 1)); }
 
 // Diagnostic builds only (scripts/diag_*.sh): drop the arena stores to price them /
 // record per-step time stamps.  Results are wrong under NOSTORE; the shipped library
@@ -191,7 +202,7 @@ template <typename T, int R, class Epi>
 __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T* __restrict__ W, int Kp, int Np,
                                       WBlock<T>& pre, const T* nW, int nKp, int nNp, Epi&& epi) {
   using V = typename Op<T>::V;
-  constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC, MT = R / 16;
+  constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC, MT = R >= 16 ? R / 16 : 1;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, kq = (lane >> 4) * EPL;
   const int NG = Np >> 5, nk = Kp / KC, nblk = (nk + NKB - 1) / NKB;
@@ -235,7 +246,7 @@ __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T
     for (int u = 0; u < NKB; ++u) {
       const int kc = min(blk * NKB + u, nk - 1);
 #pragma unroll
-      for (int m = 0; m < MT; ++m) xa[u][m] = *(const V*)(Xs + (m * 16 + r16) * ldx + kc * KC + kq);
+      for (int m = 0; m < MT; ++m) xa[u][m] = *(const V*)(Xs + tile_row<R>(m, r16) * ldx + kc * KC + kq);
     }
 #pragma unroll
     for (int u = 0; u < NKB; ++u) {
@@ -255,7 +266,7 @@ __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
-          epi(m * 16 + r16, g * 32 + j * 16 + (lane >> 4) * 4, acc[j][m]);
+          epi(tile_row<R>(m, r16), g * 32 + j * 16 + (lane >> 4) * 4, acc[j][m]);
           acc[j][m] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
 #if CVAE_DIAG_SUB
@@ -499,6 +510,7 @@ __global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowA
   const float inv_BS1 = S > 1 ? 1.f / (Bf * (float)(S - 1)) : 0.f;
   const float inv_BZ = 1.f / (Bf * (float)Z);
   const bool use_start = a.w_start > 0.f, use_time = a.w_time > 0.f;  // Training_VAE.py:247, :256
+  const bool prim = R >= 16 || (lane & 15) < R;  // this lane's row is not a duplicate (R < 16)
   const uint8_t* mkEl = Mask + (2 + net.n_enc - 1) * R * mw;  // last encoder layer
   const uint8_t* mkC1 = Mask + 1 * R * mw;
 
@@ -579,16 +591,16 @@ __global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowA
           if (live && f0 + i < I) {
             const float r = v[i] + b4[i];
             const float diff = r - xr[i];
-            s_recon += diff * diff;
+            s_recon += prim ? diff * diff : 0.f;
             gi = a.w_recon * 2.f * diff * inv_BSD;
             if (s == 0 && (d == 1 || d == 2) && use_start) {
-              s_start += diff * diff;
+              s_start += prim ? diff * diff : 0.f;
               gi += a.w_start * 2.f * diff * inv_2B;
             }
             if (d == 0) {
               Rch0[row * S + s] = r;
               if (s == 0 && use_time) {
-                s_t0 += r * r;
+                s_t0 += prim ? r * r : 0.f;
                 gi += a.w_time * 2.f * r * inv_B;
               }
               Gd0[row * S + s] = gi;

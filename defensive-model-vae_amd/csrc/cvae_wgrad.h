@@ -107,10 +107,14 @@ __device__ __forceinline__ void apply_bias(const LayerDev& L, int o, float g, co
   L.bias[o] = w;
 }
 
+// called by one whole wave: lane-strided partial sums, then a fixed-order butterfly (deterministic)
 __device__ void finish_loss(const LossArgs& l, int S, int D, int Z) {
+  const int lane = threadIdx.x & 63;
   float s[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int t = 0; t < l.ntiles; ++t)
+  for (int t = lane; t < l.ntiles; t += 64)
     for (int k = 0; k < 5; ++k) s[k] += l.partials[t * 8 + k];
+  for (int k = 0; k < 5; ++k) s[k] = wave_sum(s[k]);
+  if (lane != 0) return;
   const float B = (float)l.batch;
   const float recon = s[0] / (B * (float)(S * D));          // mse_loss mean   (:240)
   const float kld = -0.5f * s[1] / (B * (float)Z);          // (:243)
@@ -138,7 +142,7 @@ __global__ __launch_bounds__(CVAE_THREADS) void wgrad_kernel(NetDev net, const T
   const T* G = (const T*)L.gT;
   const T* X = (const T*)L.xT;
 
-  if (blockIdx.x == 0 && tid == 0 && la.partials) finish_loss(la, net.S, net.D, net.Z);
+  if (blockIdx.x == 0 && tid < 64 && la.partials) finish_loss(la, net.S, net.D, net.Z);
 
   f32x4 acc[2][2];
 #pragma unroll
