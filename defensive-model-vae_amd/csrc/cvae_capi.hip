@@ -343,7 +343,7 @@ int launch_rowchain(cvae_handle* h, RowArgs a, hipStream_t s) {
   a.steps = h->d_steps[st];
   a.nsteps = h->n_steps[st];
   a.stamps = h->d_stamps;
-  hipLaunchKernelGGL((rowchain_kernel<T, R, MODE>), dim3(grid), dim3(CVAE_THREADS), h->lds_bytes, s, h->net, a);
+  hipLaunchKernelGGL((rowchain_kernel<T, R, MODE>), dim3(grid), dim3(RC_THREADS), h->lds_bytes, s, h->net, a);
   HIPCK(hipGetLastError());
   return CVAE_OK;
 }
@@ -622,6 +622,10 @@ int cvae_diag_set_sub(unsigned long long* dev_buf) {
 // diagnostic builds only: per-block step stamps (s_memrealtime, 100 MHz) of the next launches
 int cvae_diag_set_stamps(cvae_handle* h, unsigned long long* dev_buf) {
   h->d_stamps = dev_buf;
+  return CVAE_OK;
+}
+int cvae_diag_set_wstamps(unsigned long long* dev_buf) {
+  HIPCK(hipMemcpyToSymbol(HIP_SYMBOL(g_wstamps), &dev_buf, sizeof(dev_buf)));
   return CVAE_OK;
 }
 #endif

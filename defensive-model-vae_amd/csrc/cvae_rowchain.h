@@ -41,6 +41,23 @@ enum { RC_TRAIN = 0, RC_FWD = 1, RC_DECODE = 2 };
 template <typename T> struct RowsPerTile { static constexpr int R = CVAE_ROWS; };
 static_assert(CVAE_ROWS == 4 || CVAE_ROWS == 8 || CVAE_ROWS % 16 == 0, "row tile: 4, 8 or a multiple of 16");
 
+// Waves per row-chain workgroup.  8 = two waves per SIMD: each step's column groups are
+// spread over twice the waves (16-feature groups, one n-tile each), and the SIMD overlaps one
+// wave's load / LDS / barrier latency with the other's issue.  4 = one wave per SIMD with
+// 32-feature groups (two n-tiles).
+#ifndef CVAE_RC_WAVES
+#define CVAE_RC_WAVES 8
+#endif
+constexpr int RC_NW = CVAE_RC_WAVES;
+constexpr int RC_THREADS = 64 * RC_NW;
+constexpr int RC_NT = RC_NW >= 8 ? 1 : 2;  // n-tiles (16 output features) per column group
+constexpr int RC_GW = 16 * RC_NT;          // column-group width
+static_assert(RC_NW == 4 || RC_NW == 8, "row chain: 4 or 8 waves");
+
+// exact a / b for 0 <= a < 2^22 and small b, from a precomputed 1/b: (a + ½)/b is at least ½/b
+// away from an integer, far more than the float rounding error — no integer-division sequence
+__device__ __forceinline__ int fdiv(int a, float inv_b) { return (int)(((float)a + 0.5f) * inv_b); }
+
 // LDS row of MFMA tile m, lane row r16
 template <int R>
 __device__ __forceinline__ int tile_row(int m, int r16) { return R >= 16 ? m * 16 + r16 : (r16 & (R - 1)); }
@@ -64,7 +81,7 @@ __device__ int g_sub_step;
 #define SUBSTAMP(k)                                                                                     \
   do {                                                                                                  \
     if ((threadIdx.x & 63) == 0 && g_sub && g_sub_step < 32)                                            \
-      g_sub[((blockIdx.x * 4 + (threadIdx.x >> 6)) * 32 + g_sub_step) * 5 + (k)] = __builtin_amdgcn_s_memtime(); \
+      g_sub[((blockIdx.x * RC_NW + (threadIdx.x >> 6)) * 32 + g_sub_step) * 5 + (k)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #else
 #define SUBSTAMP(k) do { } while (0)
@@ -156,7 +173,7 @@ __host__ __device__ inline LdsPlan lds_plan(const NetDev& n, int R, int tsize) {
   p.oStart = take(R * 2 * 4);
   p.oRow = take(R * 8);
   p.oMask = take(n_masks(n) * R * p.mw);
-  p.oPart = take(CVAE_NW * 8 * 4);
+  p.oPart = take(RC_NW * 8 * 4);
   p.oBias = take((n.nbias + 4) * 4);  // + 4 zero floats: the bias of backward steps
   p.total = o;
   return p;
@@ -175,7 +192,7 @@ constexpr int NKB = 4;
 
 template <typename T>
 struct WBlock {
-  typename Op<T>::V b[NKB][2];
+  typename Op<T>::V b[NKB][RC_NT];
 };
 
 template <typename T>
@@ -183,15 +200,14 @@ __device__ __forceinline__ void load_block(WBlock<T>& wb, const T* __restrict__ 
   using V = typename Op<T>::V;
   constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC;
   const int lane = threadIdx.x & 63, r16 = lane & 15, kq = (lane >> 4) * EPL;
-  const int nk = Kp / KC, ng = Np >> 5;
+  const int nk = Kp / KC, ng = Np / RC_GW;
   g = min(g, ng - 1);
-  const T* w0 = W + (size_t)(g * 32 + r16) * Kp + kq;
-  const T* w1 = w0 + (size_t)16 * Kp;
+  const T* w0 = W + (size_t)(g * RC_GW + r16) * Kp + kq;
 #pragma unroll
   for (int u = 0; u < NKB; ++u) {
     const int kc = min(blk * NKB + u, nk - 1);
-    wb.b[u][0] = gld<V>(w0 + kc * KC);
-    wb.b[u][1] = gld<V>(w1 + kc * KC);
+#pragma unroll
+    for (int j = 0; j < RC_NT; ++j) wb.b[u][j] = gld<V>(w0 + (size_t)j * 16 * Kp + kc * KC);
   }
 }
 
@@ -205,21 +221,21 @@ __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T
   constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC, MT = R >= 16 ? R / 16 : 1;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, kq = (lane >> 4) * EPL;
-  const int NG = Np >> 5, nk = Kp / KC, nblk = (nk + NKB - 1) / NKB;
-  const int ng_mine = NG > wave ? (NG - wave + CVAE_NW - 1) / CVAE_NW : 0;
+  const int NG = Np / RC_GW, nk = Kp / KC, nblk = (nk + NKB - 1) / NKB;
+  const int ng_mine = NG > wave ? (NG - wave + RC_NW - 1) / RC_NW : 0;
   const int nitems = ng_mine * nblk;
   if (nitems == 0) {  // idle in this step: still stream the next step's first block
     if (nW) load_block(pre, nW, nKp, nNp, wave, 0);
     return;
   }
-  f32x4 acc[2][MT];
+  f32x4 acc[RC_NT][MT];
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
+  for (int j = 0; j < RC_NT; ++j)
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[j][m] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int it = 0; it < nitems; ++it) {
     const int gi = it / nblk, blk = it - gi * nblk;
-    const int g = wave + gi * CVAE_NW;
+    const int g = wave + gi * RC_NW;
     const WBlock<T> cur = pre;
 #if CVAE_DIAG_SUB
     if (it == 0) {
@@ -234,7 +250,7 @@ __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T
       const T* W2 = same ? W : (nW ? nW : W);
       const int Kp2 = same ? Kp : (nW ? nKp : Kp);
       const int Np2 = same ? Np : (nW ? nNp : Np);
-      const int g2 = same ? wave + gi2 * CVAE_NW : wave;
+      const int g2 = same ? wave + gi2 * RC_NW : wave;
       const int blk2 = same ? it2 - gi2 * nblk : 0;
       load_block(pre, W2, Kp2, Np2, g2, blk2);
     }
@@ -255,7 +271,7 @@ __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T
       for (int m = 0; m < MT; ++m) {
         const V xb = on ? xa[u][m] : V{};
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[j][m] = mfma_chunk(cur.b[u][j], xb, acc[j][m]);
+        for (int j = 0; j < RC_NT; ++j) acc[j][m] = mfma_chunk(cur.b[u][j], xb, acc[j][m]);
       }
     }
 #if CVAE_DIAG_SUB
@@ -263,10 +279,10 @@ __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T
 #endif
     if (blk == nblk - 1) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < RC_NT; ++j)
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
-          epi(tile_row<R>(m, r16), g * 32 + j * 16 + (lane >> 4) * 4, acc[j][m]);
+          epi(tile_row<R>(m, r16), g * RC_GW + j * 16 + (lane >> 4) * 4, acc[j][m]);
           acc[j][m] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
 #if CVAE_DIAG_SUB
@@ -321,7 +337,7 @@ __device__ __forceinline__ uint32_t mask4(const uint8_t* mk, int mw, int row, in
 }
 
 template <typename T, int R, int MODE>
-__global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowArgs a) {
+__global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using V = typename Op<T>::V;
   const LdsPlan P = lds_plan(net, R, (int)sizeof(T));
@@ -382,15 +398,15 @@ __global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowA
   {
     auto zero = [&](void* p, int bytes) {
       f32x4* q = (f32x4*)p;
-      for (int e = tid; e < bytes / 16; e += CVAE_THREADS) q[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int e = tid; e < bytes / 16; e += RC_THREADS) q[e] = f32x4{0.f, 0.f, 0.f, 0.f};
     };
     zero(Hc, R * P.shc * (int)sizeof(T));
     zero(Dec, R * P.sdec * (int)sizeof(T));
     zero(Cin, R * P.scin * (int)sizeof(T));
     zero(Mask, rup(n_masks(net) * R * mw, 16));
-    for (int e = tid; e < net.nbias / 4 + 1; e += CVAE_THREADS)
+    for (int e = tid; e < net.nbias / 4 + 1; e += RC_THREADS)
       ((f32x4*)BiasL)[e] = e < net.nbias / 4 ? gld<f32x4>(net.bias_all + 4 * e) : f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int r = tid; r < R; r += CVAE_THREADS) {
+    for (int r = tid; r < R; r += RC_THREADS) {
       float s0 = 0.f, s1 = 0.f;
       int64_t g = 0;
       if (r < nrows) {
@@ -411,7 +427,7 @@ __global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowA
     }
   }
   lds_barrier();
-  for (int r = tid; r < nrows; r += CVAE_THREADS) {
+  for (int r = tid; r < nrows; r += RC_THREADS) {
     Cin[r * P.scin + 0] = to_t<T>(Start[r * 2 + 0]);
     Cin[r * P.scin + 1] = to_t<T>(Start[r * 2 + 1]);
   }
@@ -423,17 +439,17 @@ __global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowA
       // 16-B loads, U per thread issued before any is consumed; clamped indices so no load is
       // conditional; the channel pattern (d = col mod D) is advanced without divisions
       const int VPR = I / EPL, NV = R * VPR;
-      for (int base = 0; base < NV; base += U * CVAE_THREADS) {
+      for (int base = 0; base < NV; base += U * RC_THREADS) {
         V bufv[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          const int v = min(base + u * CVAE_THREADS + tid, NV - 1);
+          const int v = min(base + u * RC_THREADS + tid, NV - 1);
           const int r = v / VPR, c = v - r * VPR;
           bufv[u] = gld<V>(xg + RowG[r] * I + c * EPL);  // RowG = row 0 past nrows
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          const int v = base + u * CVAE_THREADS + tid;
+          const int v = base + u * RC_THREADS + tid;
           if (v < NV) {
             const int r = v / VPR, c = v - r * VPR;
             const bool live = r < nrows;
@@ -452,13 +468,13 @@ __global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowA
         }
       }
       if (net.Ip > I) {
-        for (int e = tid; e < R * (net.Ip - I); e += CVAE_THREADS) {
+        for (int e = tid; e < R * (net.Ip - I); e += RC_THREADS) {
           const int r = e / (net.Ip - I), c = I + e % (net.Ip - I);
           Xin[r * P.sx + c] = to_t<T>(0.f);
         }
       }
     } else {
-      for (int e = tid; e < R * net.Ip; e += CVAE_THREADS) {
+      for (int e = tid; e < R * net.Ip; e += RC_THREADS) {
         const int r = e / net.Ip, c = e - r * net.Ip;
         float v = 0.f;
         if (r < nrows && c < I) {
@@ -471,13 +487,13 @@ __global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowA
     }
   } else {
     if (skip_cond) {
-      for (int e = tid; e < R * H; e += CVAE_THREADS) {
+      for (int e = tid; e < R * H; e += RC_THREADS) {
         const int r = e / H, c = e - r * H;
         Dec[r * P.sdec + Z + c] = to_t<T>(r < nrows ? gld<float>(a.hc_in + (size_t)(b0 + r) * H + c) : 0.f);
       }
     }
     if (a.z_in) {
-      for (int e = tid; e < R * Z; e += CVAE_THREADS) {
+      for (int e = tid; e < R * Z; e += RC_THREADS) {
         const int r = e / Z, j = e - r * Z;
         Dec[r * P.sdec + j] = to_t<T>(r < nrows ? gld<float>(a.z_in + (size_t)(b0 + r) * Z + j) : 0.f);
       }
@@ -491,7 +507,7 @@ __global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowA
   if (TRAIN && !CVAE_DIAG_NOSTORE) {
     auto copy_T = [&](const T* src, int ld, int ncols, T* dst) {
       constexpr int RQ = R / 4;
-      for (int t = tid; t < ncols * RQ; t += CVAE_THREADS) {
+      for (int t = tid; t < ncols * RQ; t += RC_THREADS) {
         const int c = t / RQ, q = t - c * RQ;
         f32x4 v;
 #pragma unroll
@@ -511,19 +527,24 @@ __global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowA
   const float inv_BZ = 1.f / (Bf * (float)Z);
   const bool use_start = a.w_start > 0.f, use_time = a.w_time > 0.f;  // Training_VAE.py:247, :256
   const bool prim = R >= 16 || (lane & 15) < R;  // this lane's row is not a duplicate (R < 16)
+  const float inv_D = 1.f / (float)D, inv_S = 1.f / (float)S, inv_Z = 1.f / (float)Z;
+  const float inv_Zp2 = 1.f / (float)net.Zp2;
   const uint8_t* mkEl = Mask + (2 + net.n_enc - 1) * R * mw;  // last encoder layer
   const uint8_t* mkC1 = Mask + 1 * R * mw;
 
   // ---------------------------------------------------------------- the step interpreter
+  // Descriptors are copied BY VALUE (through a reference into global memory every field would be
+  // re-loaded after each global store of the epilogue: the compiler cannot rule out aliasing),
+  // and one step AHEAD: the next step's scalar loads are issued at the top of this step, so
+  // their latency hides behind this step's GEMM instead of sitting between two barriers.
+  StepDesc nx = a.steps[0];
   for (int si = 0; si < a.nsteps; ++si) {
-    // descriptors copied BY VALUE: read through a reference into global memory, every field
-    // would be re-loaded after each global store of the epilogue (the compiler cannot rule out
-    // aliasing), serialising scalar-load latencies inside the hot loop
-    const StepDesc st = a.steps[si];
+    const StepDesc st = nx;
     const bool has_next = si + 1 < a.nsteps;
-    const void* const nW = a.steps[has_next ? si + 1 : si].W;
-    const int nKp = a.steps[has_next ? si + 1 : si].Kp;
-    const int nNp = a.steps[has_next ? si + 1 : si].Np;
+    nx = a.steps[has_next ? si + 1 : si];
+    const void* const nW = nx.W;
+    const int nKp = nx.Kp;
+    const int nNp = nx.Np;
     T* const d1 = st.dst1 >= 0 ? buf(st.dst1) : nullptr;
     T* const d2 = st.dst2 >= 0 ? buf(st.dst2) : nullptr;
     const int ld1 = st.dst1 >= 0 ? ld_of(st.dst1) : 0;
@@ -583,7 +604,7 @@ __global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowA
         // target x_rel from the resident input tile; GL overwrites it in place below
         // (same lane, same elements), so no other reader is affected
         const f32x4 xr = get4(Xin + row * P.sx + f0);
-        int s = f0 / D, d = f0 - s * D;
+        int s = fdiv(f0, inv_D), d = f0 - s * D;
         T* gcol = g1 + (size_t)f0 * Bp + b0 + row;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -651,8 +672,8 @@ __global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowA
     if (kind == E_FC && MODE != RC_DECODE) {
       // reparameterize (:199-206) + KL terms (:243)
       T* xd0 = (T*)net.L[lD(net, 0)].xT;
-      for (int e = tid; e < R * Z; e += CVAE_THREADS) {
-        const int r = e / Z, j = e - r * Z;
+      for (int e = tid; e < R * Z; e += RC_THREADS) {
+        const int r = fdiv(e, inv_Z), j = e - r * Z;
         float z = 0.f, ep = 0.f, sd = 0.f;
         if (r < nrows) {
           const float mu = MuLv[r * net.Zp2 + j], lv = MuLv[r * net.Zp2 + Z + j];
@@ -671,8 +692,8 @@ __global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowA
     } else if (kind == E_LOSS) {
       // time-monotonicity term: relu(r_s - r_{s+1}) (:261-262), ReLU'(0) = 0
       T* gl = g1;
-      for (int e = tid; e < R * S; e += CVAE_THREADS) {
-        const int r = e / S, s = e - r * S;
+      for (int e = tid; e < R * S; e += RC_THREADS) {
+        const int r = fdiv(e, inv_S), s = e - r * S;
         float g = 0.f;
         if (r < nrows) {
           g = Gd0[r * S + s];
@@ -697,8 +718,8 @@ __global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowA
     } else if (kind == E_D0B) {
       // reparameterisation + KL backward → G_fc = [dmu ‖ dlogvar] into P0 (the fc-backward input)
       T* gfc = (T*)net.L[lFC(net)].gT;
-      for (int e = tid; e < R * net.Zp2; e += CVAE_THREADS) {
-        const int r = e / net.Zp2, c = e - r * net.Zp2;
+      for (int e = tid; e < R * net.Zp2; e += RC_THREADS) {
+        const int r = fdiv(e, inv_Zp2), c = e - r * net.Zp2;
         float g = 0.f;
         if (r < nrows && c < 2 * Z) {
           const int j = c < Z ? c : c - Z;
@@ -715,7 +736,7 @@ __global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowA
       }
       // pads of the two gradient targets of the fc backward must read as zero
       if (net.Hp > H) {
-        for (int e = tid; e < R * (net.Hp - H); e += CVAE_THREADS) {
+        for (int e = tid; e < R * (net.Hp - H); e += RC_THREADS) {
           const int r = e / (net.Hp - H), c = H + e % (net.Hp - H);
           P1b[r * P.sp + c] = to_t<T>(0.f);
           Q[r * P.shc + c] = to_t<T>(0.f);
@@ -743,7 +764,7 @@ __global__ __launch_bounds__(CVAE_THREADS) void rowchain_kernel(NetDev net, RowA
   lds_barrier();
   if (tid < 5) {
     float s = 0.f;
-    for (int w = 0; w < CVAE_NW; ++w) s += Part[w * 8 + tid];
+    for (int w = 0; w < RC_NW; ++w) s += Part[w * 8 + tid];
     gst<float>(a.partials + blockIdx.x * 8 + tid, s);
   }
 }

@@ -25,6 +25,21 @@ enum { PM_GRAD = 0, PM_ADAM = 1, PM_PACK = 2 };
 #define CVAE_DIAG_NOWPACK 0
 #endif
 
+#ifndef CVAE_DIAG_STAMPS
+#define CVAE_DIAG_STAMPS 0
+#endif
+#if CVAE_DIAG_STAMPS
+// diagnostic builds only: [block][4] s_memrealtime at entry, after the MFMA loop, after the
+// cross-wave reduction barrier, at exit
+__device__ unsigned long long* g_wstamps;
+#define WSTAMP(k)                                                                         \
+  do {                                                                                    \
+    if (threadIdx.x == 0 && g_wstamps) g_wstamps[blockIdx.x * 4 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define WSTAMP(k) do { } while (0)
+#endif
+
 struct AdamArgs {
   float* params;      // flat fp32 master (state_dict order)
   float* m;
@@ -142,6 +157,7 @@ __global__ __launch_bounds__(CVAE_THREADS) void wgrad_kernel(NetDev net, const T
   const T* G = (const T*)L.gT;
   const T* X = (const T*)L.xT;
 
+  WSTAMP(0);
   if (blockIdx.x == 0 && tid < 64 && la.partials) finish_loss(la, net.S, net.D, net.Z);
 
   f32x4 acc[2][2];
@@ -182,6 +198,7 @@ __global__ __launch_bounds__(CVAE_THREADS) void wgrad_kernel(NetDev net, const T
       load(u, j + PF);
     }
   }
+  WSTAMP(1);
   float* rw = red + wave * 32 * 33;
 #pragma unroll
   for (int m = 0; m < 2; ++m)
@@ -206,6 +223,7 @@ __global__ __launch_bounds__(CVAE_THREADS) void wgrad_kernel(NetDev net, const T
     db += __shfl_xor(db, 4, 64);
   }
   __syncthreads();
+  WSTAMP(2);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int e = q * CVAE_THREADS + tid;
@@ -216,6 +234,10 @@ __global__ __launch_bounds__(CVAE_THREADS) void wgrad_kernel(NetDev net, const T
     apply_weight<T, MODE>(L, td.o0 + o, td.i0 + i, g, aa);
   }
   if (td.i0 == 0 && (tid & 7) == 0) apply_bias<MODE>(L, td.o0 + (tid >> 3), db, aa);
+#if CVAE_DIAG_STAMPS
+  __syncthreads();
+  WSTAMP(3);
+#endif
 }
 
 // Adam from a (reduced) gradient buffer, or repack of the operand copies.

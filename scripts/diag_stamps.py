@@ -22,13 +22,20 @@ eng = m.attach(dtype=dtype, max_batch=B)
 x = eng.as_input(torch.randn(B, 100, 6))
 L = lib()
 L.cvae_diag_set_stamps.argtypes = [C.c_void_p, C.c_void_p]
+L.cvae_diag_set_wstamps.argtypes = [C.c_void_p]
 R = 16
 nb = ((B + 31) // 32 * 32) // R
 dbuf = torch.zeros(nb * 64, dtype=torch.int64, device="cuda")
-L.cvae_diag_set_stamps(eng._h, C.c_void_p(dbuf.data_ptr()))
+NT = 4096
+wbuf = torch.zeros(NT * 4, dtype=torch.int64, device="cuda")
 for _ in range(30):
     eng.train_step(x)
 torch.cuda.synchronize()
+L.cvae_diag_set_stamps(eng._h, C.c_void_p(dbuf.data_ptr()))
+L.cvae_diag_set_wstamps(C.c_void_p(wbuf.data_ptr()))
+eng.train_step(x)  # the measured step: both kernels stamp their blocks
+torch.cuda.synchronize()
+L.cvae_diag_set_wstamps(C.c_void_p(0))
 st = dbuf.view(nb, 64).cpu().numpy().astype(np.int64)
 k = int((st[0] > 0).sum())
 d = np.diff(st[:, :k], axis=1) * 10  # ns
@@ -37,3 +44,17 @@ print(f"blocks={nb} stamps={k} kernel span={(st[:, k-1].max() - t0) * 10 / 1000:
 names = ["prologue", "xT copies+C0"] + [f"step{i}" for i in range(1, 64)]
 for i in range(k - 1):
     print(f"{names[i]:>14s} {i:2d}: median {np.median(d[:, i]) / 1000:7.3f} us   max {d[:, i].max() / 1000:7.3f} us")
+
+w = wbuf.view(NT, 4).cpu().numpy().astype(np.int64)
+nw = int((w[:, 0] > 0).sum())
+w = w[:nw]
+rc_end = st[:, k - 1].max()
+print(f"wgrad: blocks={nw}; first entry {(w[:, 0].min() - rc_end) * 10 / 1000:.2f} us after the last row-chain stamp;"
+      f" span {(w[:, 3].max() - w[:, 0].min()) * 10 / 1000:.2f} us")
+print(f"  entry spread {(w[:, 0].max() - w[:, 0].min()) * 10 / 1000:.2f} us;"
+      f" phases median/max us: mfma {np.median(w[:, 1] - w[:, 0]) / 100:.2f}/{(w[:, 1] - w[:, 0]).max() / 100:.2f}"
+      f"  reduce {np.median(w[:, 2] - w[:, 1]) / 100:.2f}/{(w[:, 2] - w[:, 1]).max() / 100:.2f}"
+      f"  adam {np.median(w[:, 3] - w[:, 2]) / 100:.2f}/{(w[:, 3] - w[:, 2]).max() / 100:.2f}")
+late = np.argsort(w[:, 3])[-8:]
+print("  last blocks to finish (block: entry, exit us rel. first entry):",
+      [(int(b), round((w[b, 0] - w[:, 0].min()) / 100, 2), round((w[b, 3] - w[:, 0].min()) / 100, 2)) for b in late])

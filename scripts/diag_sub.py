@@ -18,7 +18,7 @@ eng = m.attach(dtype="bf16", max_batch=B)
 x = eng.as_input(torch.randn(B, 100, 6))
 L = lib()
 L.cvae_diag_set_sub.argtypes = [C.c_void_p]
-nb = 32
+nb = (B + 31) // 32 * 32 // 16  # row-chain grid at R=16 (the kernel writes [block][wave][step][5])
 buf = torch.zeros(nb * 4 * 32 * 5, dtype=torch.int64, device="cuda")
 L.cvae_diag_set_sub(C.c_void_p(buf.data_ptr()))
 for _ in range(20):
@@ -27,7 +27,7 @@ torch.cuda.synchronize()
 st = buf.view(nb, 4, 32, 5).cpu().numpy().astype(np.int64)
 blk = int(os.environ.get("BLK", "5"))
 print("cycles (s_memtime) per step for block", blk, ": [entry->wait, wait->mfma, mfma->epi, epi->barrier, barrier->next entry]")
-for si in range(21):
+for si in range(26):
     row = []
     for w in range(4):
         t = st[blk, w, si]
