@@ -141,11 +141,30 @@ int build_plan(cvae_handle* h) {
   if (c.hidden_dim % 4 || c.latent_dim % 4)
     return fail(CVAE_E_INVALID, "hidden_dim and latent_dim must be multiples of 4 (4-feature epilogue vectors)");
 
-  // weight-gradient / parameter tiles: 32×32 over each layer's padded (Np × Kp)
-  h->tiles.clear();
-  for (int l = 0; l < n.n_layers; ++l)
-    for (int o = 0; o < n.L[l].Np; o += 32)
-      for (int i = 0; i < n.L[l].Kp; i += 32) h->tiles.push_back({l, o, i, 0});
+  // Weight-gradient / parameter tiles: 32×32 over each layer's padded (Np × Kp), laid out for
+  // the 8 XCDs.  Workgroup b runs on XCD b % 8 and every XCD has its own L2, so a tile's G rows
+  // (shared along its o-block) and X rows (shared along its i-block) are re-fetched from the
+  // fabric by every XCD that needs them.  The tiles are listed layer by layer with the longer
+  // dimension outermost, cut into 8 contiguous chunks, and chunk x is placed at blockIdx
+  // 8j + x: each XCD then covers compact regions of few layers and fetches their rows once.
+  std::vector<TileDesc> seq;
+  for (int l = 0; l < n.n_layers; ++l) {
+    const LayerDev& L = n.L[l];
+    if (L.Kp > L.Np) {
+      for (int i = 0; i < L.Kp; i += 32)
+        for (int o = 0; o < L.Np; o += 32) seq.push_back({l, o, i, 0});
+    } else {
+      for (int o = 0; o < L.Np; o += 32)
+        for (int i = 0; i < L.Kp; i += 32) seq.push_back({l, o, i, 0});
+    }
+  }
+  const int nt = (int)seq.size(), q = nt / 8, r = nt % 8;
+  h->tiles.assign(nt, TileDesc{});
+  for (int b = 0; b < nt; ++b) {
+    const int x = b % 8, j = b / 8;
+    const int start = x * q + (x < r ? x : r);  // chunk x = seq[start, start + q + (x < r))
+    h->tiles[b] = seq[start + j];
+  }
   return CVAE_OK;
 }
 

@@ -136,6 +136,11 @@ __device__ __forceinline__ float philox_normal(uint64_t seed, uint64_t offset, u
   return (j & 1) ? rad * s : rad * c;
 }
 
+// Wave index as a SCALAR: threadIdx-derived values are divergent to the compiler, so a plain
+// `threadIdx.x >> 6` puts every quantity derived from it (column group, trip counts, weight
+// addresses) in VGPRs with exec-masked loops; readfirstlane makes them SGPR/SALU work.
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
 // ------------------------------------------------------------------ wave reduction
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

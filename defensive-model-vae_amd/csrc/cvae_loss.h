@@ -15,7 +15,7 @@ __global__ __launch_bounds__(CVAE_THREADS) void loss_partial_kernel(const float*
                                                                     const float* __restrict__ lv, int B, int S,
                                                                     int D, int Z, float* partials) {
   __shared__ float part[CVAE_NW * 8];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int b0 = blockIdx.x * 32, nrows = min(32, B - b0), I = S * D;
   float s_recon = 0.f, s_kl = 0.f, s_start = 0.f, s_t0 = 0.f, s_relu = 0.f;
   for (int e = tid; e < nrows * I; e += CVAE_THREADS) {

@@ -219,7 +219,7 @@ __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T
                                       WBlock<T>& pre, const T* nW, int nKp, int nNp, Epi&& epi) {
   using V = typename Op<T>::V;
   constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC, MT = R >= 16 ? R / 16 : 1;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = wave_id();
   const int r16 = lane & 15, kq = (lane >> 4) * EPL;
   const int NG = Np / RC_GW, nk = Kp / KC, nblk = (nk + NKB - 1) / NKB;
   const int ng_mine = NG > wave ? (NG - wave + RC_NW - 1) / RC_NW : 0;
@@ -369,7 +369,7 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
     return id == B_XIN ? P.sx : (id == B_P0 || id == B_P1) ? P.sp : id == B_HC ? P.shc : id == B_DEC ? P.sdec : P.scin;
   };
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int b0 = blockIdx.x * R;
   const int nrows = max(0, min(R, a.batch - b0));  // tiles past the batch write zeros
   const int Bp = net.Bp, Z = net.Z, H = net.H, S = net.S, D = net.D, I = net.I;

@@ -151,7 +151,7 @@ __global__ __launch_bounds__(CVAE_THREADS) void wgrad_kernel(NetDev net, const T
   __shared__ __attribute__((aligned(16))) float red[CVAE_NW * 32 * 33];
   const TileDesc td = tiles[blockIdx.x];
   const LayerDev& L = net.L[td.layer];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int r16 = lane & 15, kq = (lane >> 4) * EPL;
   const int Bp = net.Bp;
   const T* G = (const T*)L.gT;

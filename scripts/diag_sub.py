@@ -19,17 +19,18 @@ x = eng.as_input(torch.randn(B, 100, 6))
 L = lib()
 L.cvae_diag_set_sub.argtypes = [C.c_void_p]
 nb = (B + 31) // 32 * 32 // 16  # row-chain grid at R=16 (the kernel writes [block][wave][step][5])
-buf = torch.zeros(nb * 4 * 32 * 5, dtype=torch.int64, device="cuda")
+NW = int(os.environ.get("NW", "8"))
+buf = torch.zeros(nb * NW * 32 * 5, dtype=torch.int64, device="cuda")
 L.cvae_diag_set_sub(C.c_void_p(buf.data_ptr()))
 for _ in range(20):
     eng.train_step(x)
 torch.cuda.synchronize()
-st = buf.view(nb, 4, 32, 5).cpu().numpy().astype(np.int64)
+st = buf.view(nb, NW, 32, 5).cpu().numpy().astype(np.int64)
 blk = int(os.environ.get("BLK", "5"))
 print("cycles (s_memtime) per step for block", blk, ": [entry->wait, wait->mfma, mfma->epi, epi->barrier, barrier->next entry]")
-for si in range(26):
+for si in range(20):
     row = []
-    for w in range(4):
+    for w in range(NW):
         t = st[blk, w, si]
         nxt = st[blk, w, si + 1, 0] if si + 1 < 32 else 0
         if t[0] == 0:
