@@ -74,6 +74,16 @@ __device__ __forceinline__ int tile_row(int m, int r16) { return R >= 16 ? m * 1
 #ifndef CVAE_DIAG_SUB
 #define CVAE_DIAG_SUB 0
 #endif
+// ablations (timing only, results wrong): no weight loads / no epilogue / no MFMAs
+#ifndef CVAE_DIAG_NOWLOAD
+#define CVAE_DIAG_NOWLOAD 0
+#endif
+#ifndef CVAE_DIAG_NOEPI
+#define CVAE_DIAG_NOEPI 0
+#endif
+#ifndef CVAE_DIAG_NOMFMA
+#define CVAE_DIAG_NOMFMA 0
+#endif
 #if CVAE_DIAG_SUB
 // [block][wave][step][5]: entry, weights arrived, MFMAs done, epilogue done, barrier passed
 __device__ unsigned long long* g_sub;
@@ -207,7 +217,7 @@ __device__ __forceinline__ void load_block(WBlock<T>& wb, const T* __restrict__ 
   for (int u = 0; u < NKB; ++u) {
     const int kc = min(blk * NKB + u, nk - 1);
 #pragma unroll
-    for (int j = 0; j < RC_NT; ++j) wb.b[u][j] = gld<V>(w0 + (size_t)j * 16 * Kp + kc * KC);
+    for (int j = 0; j < RC_NT; ++j) wb.b[u][j] = CVAE_DIAG_NOWLOAD ? V{} : gld<V>(w0 + (size_t)j * 16 * Kp + kc * KC);
   }
 }
 
@@ -271,7 +281,8 @@ __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T
       for (int m = 0; m < MT; ++m) {
         const V xb = on ? xa[u][m] : V{};
 #pragma unroll
-        for (int j = 0; j < RC_NT; ++j) acc[j][m] = mfma_chunk(cur.b[u][j], xb, acc[j][m]);
+        for (int j = 0; j < RC_NT; ++j)
+          if (!CVAE_DIAG_NOMFMA) acc[j][m] = mfma_chunk(cur.b[u][j], xb, acc[j][m]);
       }
     }
 #if CVAE_DIAG_SUB
@@ -565,6 +576,7 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
     dense<T, R>(buf(st.xbuf), ld_of(st.xbuf), (const T*)st.W, st.Kp, st.Np, pre,
                 has_next ? (const T*)nW : (const T*)nullptr, nKp, nNp,
                 [&](int row, int f0, f32x4 v) {
+      if (CVAE_DIAG_NOEPI) return;
       const f32x4 b4 = *(const f32x4*)(biasL + f0);
       const bool live = row < nrows;
       f32x4 y;
