@@ -169,33 +169,45 @@ int build_plan(cvae_handle* h) {
 }
 
 // Step tables (see cvae_rowchain.h).  Masks: C0=0, C1=1, E_i=2+i, D_i=2+n_enc+i.
-std::vector<StepDesc> build_steps(const NetDev& n, int mode) {
+std::vector<StepSpec> build_steps(const NetDev& n, int mode) {
   const bool train = mode == cvae_handle::ST_TRAIN;
   const int ne = n.n_enc, nd = n.n_dec, Z = n.Z, H = n.H;
   auto arena = [&](void* p) -> void* { return train ? p : nullptr; };
   auto blank = [&]() {
-    StepDesc s{};
+    StepSpec s{};
     s.mask_out = -1; s.mask_in = -1; s.dst1 = B_NONE; s.dst2 = B_NONE;
     return s;
   };
   auto fwd = [&](int l, int xbuf, int epi) {
-    StepDesc s = blank();
+    StepSpec s = blank();
     const LayerDev& L = n.L[l];
-    s.W = L.Wf; s.bias = L.bias; s.bias_off = n.bias_off[l]; s.Kp = L.Kp; s.Np = L.Np; s.N = L.N;
+    s.W = L.Wf; s.bias_off = n.bias_off[l]; s.Kp = L.Kp; s.Np = L.Np; s.N = L.N;
     s.xbuf = xbuf; s.epi = epi;
     return s;
   };
   auto bwd = [&](int l, int xbuf, int epi) {
-    StepDesc s = blank();
+    StepSpec s = blank();
     const LayerDev& L = n.L[l];
-    s.W = L.Wb; s.bias = n.zbias; s.bias_off = -1; s.Kp = L.Np; s.Np = L.Kp; s.N = L.K; s.xbuf = xbuf;
+    s.W = L.Wb; s.bias_off = -1; s.Kp = L.Np; s.Np = L.Kp; s.N = L.K; s.xbuf = xbuf;
     s.epi = epi;
     return s;
   };
   auto pb = [](int i) { return (i & 1) ? B_P1 : B_P0; };
-  std::vector<StepDesc> v;
+  std::vector<StepSpec> v;
+#ifdef CVAE_DIAG_SIMPLE
+  // microbenchmark (diagnostic builds only): CVAE_DIAG_SIMPLE copies of one plain 128x128
+  // forward step (encoder layer 1, ping-ponging P0 ↔ P1) — the per-step cost without special steps
+  if (train) {
+    for (int k = 0; k < CVAE_DIAG_SIMPLE; ++k) {
+      StepSpec s = fwd(lE(n, 1), pb(k), E_RELU);
+      s.mask_out = 3; s.dst1 = pb(k + 1); s.g1 = n.L[lE(n, 2)].xT;
+      v.push_back(s);
+    }
+    return v;
+  }
+#endif
   if (mode != cvae_handle::ST_DEC_HC) {
-    StepDesc s = fwd(lC0(n), B_CIN, E_RELU);
+    StepSpec s = fwd(lC0(n), B_CIN, E_RELU);
     s.mask_out = 0; s.dst1 = B_P0; s.g1 = arena(n.L[lC1(n)].xT);
     v.push_back(s);
     s = fwd(lC1(n), B_P0, E_RELU);
@@ -208,7 +220,7 @@ std::vector<StepDesc> build_steps(const NetDev& n, int mode) {
   if (mode == cvae_handle::ST_COND) return v;
   if (mode == cvae_handle::ST_TRAIN || mode == cvae_handle::ST_FWD) {
     for (int i = 0; i < ne; ++i) {
-      StepDesc s = fwd(lE(n, i), i == 0 ? B_XIN : pb(i - 1), E_RELU);
+      StepSpec s = fwd(lE(n, i), i == 0 ? B_XIN : pb(i - 1), E_RELU);
       s.mask_out = 2 + i;
       if (i == ne - 1) {
         s.dst1 = B_HC; s.off1 = 0; s.concat = 1; s.g1 = arena(n.L[lFC(n)].xT);
@@ -220,12 +232,12 @@ std::vector<StepDesc> build_steps(const NetDev& n, int mode) {
     v.push_back(fwd(lFC(n), B_HC, E_FC));
   }
   for (int i = 0; i < nd - 1; ++i) {
-    StepDesc s = fwd(lD(n, i), i == 0 ? B_DEC : pb(i - 1), E_RELU);
+    StepSpec s = fwd(lD(n, i), i == 0 ? B_DEC : pb(i - 1), E_RELU);
     s.mask_out = 2 + ne + i; s.dst1 = pb(i); s.g1 = arena(n.L[lD(n, i + 1)].xT);
     v.push_back(s);
   }
   {
-    StepDesc s = fwd(lD(n, nd - 1), nd == 1 ? B_DEC : pb(nd - 2), train ? E_LOSS : E_RECON);
+    StepSpec s = fwd(lD(n, nd - 1), nd == 1 ? B_DEC : pb(nd - 2), train ? E_LOSS : E_RECON);
     if (train) s.g1 = n.L[lD(n, nd - 1)].gT;
     v.push_back(s);
   }
@@ -233,7 +245,7 @@ std::vector<StepDesc> build_steps(const NetDev& n, int mode) {
   // backward: decoder → reparameterisation → fc → encoder / condition encoder
   int cur = B_XIN, pp = 0;
   for (int i = nd - 1; i >= 1; --i) {
-    StepDesc s = bwd(lD(n, i), cur, E_BWD);
+    StepSpec s = bwd(lD(n, i), cur, E_BWD);
     s.mask_in = 2 + ne + i - 1; s.dst1 = pp ? B_P1 : B_P0; s.g1 = n.L[lD(n, i - 1)].gT;
     v.push_back(s);
     cur = s.dst1;
@@ -241,21 +253,21 @@ std::vector<StepDesc> build_steps(const NetDev& n, int mode) {
   }
   v.push_back(bwd(lD(n, 0), cur, E_D0B));
   {
-    StepDesc s = bwd(lFC(n), B_P0, E_FCB);
+    StepSpec s = bwd(lFC(n), B_P0, E_FCB);
     s.g1 = n.L[lE(n, ne - 1)].gT; s.g2 = n.L[lC1(n)].gT;
     v.push_back(s);
   }
   cur = B_P1;
   int p = 0;
   for (int i = ne - 1; i >= 1; --i) {
-    StepDesc s = bwd(lE(n, i), cur, E_BWD);
+    StepSpec s = bwd(lE(n, i), cur, E_BWD);
     s.mask_in = 2 + i - 1; s.dst1 = i > 1 ? (p ? B_P1 : B_P0) : B_NONE; s.g1 = n.L[lE(n, i - 1)].gT;
     v.push_back(s);
     cur = s.dst1;
     p ^= 1;
   }
   {
-    StepDesc s = bwd(lC1(n), B_HC, E_BWD);
+    StepSpec s = bwd(lC1(n), B_HC, E_BWD);
     s.mask_in = 0; s.g1 = n.L[lC0(n)].gT;
     v.push_back(s);
   }
@@ -308,7 +320,13 @@ int alloc_arena(cvae_handle* h) {
   h->d_tiles = (TileDesc*)(h->arena + tile_off);
   HIPCK(hipMemcpy(h->d_tiles, h->tiles.data(), h->tiles.size() * sizeof(TileDesc), hipMemcpyHostToDevice));
   for (int m = 0; m < cvae_handle::ST_N; ++m) {
-    const std::vector<StepDesc> st = build_steps(n, m);
+    const std::vector<StepSpec> spec = build_steps(n, m);
+    std::vector<StepDesc> st;
+    for (const StepSpec& x : spec) {
+      if (x.goff1 < 0 || x.goff1 > 0xFFFF || x.goff2 < 0 || x.goff2 > 0xFFFF || x.mask_out > 62 || x.mask_in > 62)
+        return fail(CVAE_E_INVALID, "step descriptor field out of range");
+      st.push_back(encode_step(x));
+    }
     if (st.empty() || st.size() > 64) return fail(CVAE_E_INVALID, "bad step table");
     h->d_steps[m] = (StepDesc*)(h->arena + step_off[m]);
     h->n_steps[m] = (int)st.size();

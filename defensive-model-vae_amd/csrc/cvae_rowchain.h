@@ -102,11 +102,10 @@ enum { B_NONE = -1, B_XIN = 0, B_P0 = 1, B_P1 = 2, B_HC = 3, B_DEC = 4, B_CIN = 
 // epilogue kinds; post-step element-wise phases
 enum { E_RELU = 0, E_FC = 1, E_LOSS = 2, E_RECON = 3, E_BWD = 4, E_D0B = 5, E_FCB = 6 };
 
-struct StepDesc {
+// One step of the interpreter as the host builds it (cvae_capi.hip build_steps) ...
+struct StepSpec {
   const void* W;     // B operand [Np][Kp] (forward Wf or backward Wb)
-  const float* bias; // [Np] (zeros for backward)
   int bias_off;      // offset of this step's bias in the LDS bias copy (-1: zeros, backward)
-  int pad0_;
   void* g1;          // arena destination (feature-major), nullable
   void* g2;
   int Kp, Np;        // reduction / output dims (padded)
@@ -121,6 +120,33 @@ struct StepDesc {
   int concat;        // skip columns >= N (destination is part of a concatenation)
   int hc_out;        // inference: also write h_c (fp32) to RowArgs::hc_out
 };
+
+// ... and as the kernel reads it: 64 B, copied into LDS by the prologue and read back every step
+// with wave-uniform LDS reads + readfirstlane.  (Scalar loads share lgkmcnt with LDS and return
+// out of order: a descriptor fetched with s_load makes the step's first LDS wait also wait for
+// an L2 round trip, on every step of every launch.)
+struct StepDesc {
+  const void* W;
+  void* g1;
+  void* g2;
+  int Kp, Np, N, bias_off;
+  int code;          // xbuf | epi<<4 | (dst1+1)<<8 | (dst2+1)<<12 | concat<<16 | hc_out<<17 | (mask_out+1)<<20 | (mask_in+1)<<26
+  int off1, off2;
+  int goff;          // goff1 | goff2 << 16
+  int pad_[2];
+};
+static_assert(sizeof(StepDesc) == 64, "StepDesc is 4 x 16 B");
+
+inline StepDesc encode_step(const StepSpec& s) {
+  StepDesc d{};
+  d.W = s.W; d.g1 = s.g1; d.g2 = s.g2;
+  d.Kp = s.Kp; d.Np = s.Np; d.N = s.N; d.bias_off = s.bias_off;
+  d.code = s.xbuf | (s.epi << 4) | ((s.dst1 + 1) << 8) | ((s.dst2 + 1) << 12) | (s.concat << 16) |
+           (s.hc_out << 17) | ((s.mask_out + 1) << 20) | ((s.mask_in + 1) << 26);
+  d.off1 = s.off1; d.off2 = s.off2;
+  d.goff = s.goff1 | (s.goff2 << 16);
+  return d;
+}
 
 struct RowArgs {
   const void* x;          // (N_total, S, D) operand dtype
@@ -147,7 +173,7 @@ struct RowArgs {
 struct LdsPlan {
   int sx, sp, shc, sdec, scin;   // row strides (elements of T)
   int mw;                        // mask words per row
-  int oXin, oP0, oP1, oHc, oDec, oCin, oMuLv, oEps, oStd, oDz, oU, oRch0, oGd0, oStart, oRow, oMask, oPart, oBias;
+  int oXin, oP0, oP1, oHc, oDec, oCin, oMuLv, oEps, oStd, oDz, oU, oRch0, oGd0, oStart, oRow, oMask, oPart, oBias, oSteps;
   int total;
 };
 
@@ -185,6 +211,7 @@ __host__ __device__ inline LdsPlan lds_plan(const NetDev& n, int R, int tsize) {
   p.oMask = take(n_masks(n) * R * p.mw);
   p.oPart = take(RC_NW * 8 * 4);
   p.oBias = take((n.nbias + 4) * 4);  // + 4 zero floats: the bias of backward steps
+  p.oSteps = take(64 * (int)sizeof(StepDesc));
   p.total = o;
   return p;
 }
@@ -405,36 +432,96 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
   }
   stamp();
 
-  // ---------------------------------------------------------------- prologue: zero + start points
+  // ---------------------------------------------------------------- prologue: zero + start points + x tile
+  // Fast path (absolute trajectories, 16-B aligned rows, one load pass): every thread loads its
+  // x vectors straight away — the row index is read through the clamped idx itself, not through
+  // an LDS table behind a barrier — and the start points come from each row's first vector, so
+  // the tile costs one dependent global latency (two with an idx gather) instead of three.
+  constexpr int EPL = Op<T>::EPL, U = 12;
+  const int VPR = I / EPL, NV = R * VPR;
+  const bool vec = MODE != RC_DECODE && (I % EPL) == 0 && (((uintptr_t)xg) & 15) == 0;
+  const bool fast = vec && !a.x_relative && NV <= U * RC_THREADS;
+  V bufv[U];
+  // relative transform (Training_VAE.py:347-348) of the loaded vectors into the LDS tile;
+  // the channel pattern (d = col mod D) is advanced without divisions
+  auto transform = [&](int base) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int v = base + u * RC_THREADS + tid;
+      if (v < NV) {
+        const int r = v / VPR, c = v - r * VPR;
+        const bool live = r < nrows;
+        const float s0 = a.x_relative ? 0.f : Start[r * 2 + 0];
+        const float s1 = a.x_relative ? 0.f : Start[r * 2 + 1];
+        int d = (c * EPL) % D;
+        V o;
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) {
+          const float val = (float)bufv[u][e] - (d == 1 ? s0 : 0.f) - (d == 2 ? s1 : 0.f);
+          o[e] = to_t<T>(live ? val : 0.f);
+          d = d + 1 == D ? 0 : d + 1;
+        }
+        *(V*)(Xin + r * P.sx + c * EPL) = o;
+      }
+    }
+  };
   {
     auto zero = [&](void* p, int bytes) {
       f32x4* q = (f32x4*)p;
       for (int e = tid; e < bytes / 16; e += RC_THREADS) q[e] = f32x4{0.f, 0.f, 0.f, 0.f};
     };
+    if (fast) {  // loads first: everything below overlaps their latency
+      const int last = max(a.batch - 1, 0);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int v = min(u * RC_THREADS + tid, NV - 1);
+        const int r = v / VPR, c = v - r * VPR;
+        const int rr = min(b0 + r, last);  // rows past the batch re-read a valid row (zeroed later)
+        const int64_t g = a.idx ? gld<int64_t>(a.idx + rr) : (int64_t)rr;
+        bufv[u] = gld<V>(xg + g * I + c * EPL);
+      }
+    }
+    for (int e = tid; e < a.nsteps * 4; e += RC_THREADS)
+      ((u32x4*)(smem + P.oSteps))[e] = gld<u32x4>((const u32x4*)a.steps + e);
     zero(Hc, R * P.shc * (int)sizeof(T));
     zero(Dec, R * P.sdec * (int)sizeof(T));
     zero(Cin, R * P.scin * (int)sizeof(T));
     zero(Mask, rup(n_masks(net) * R * mw, 16));
     for (int e = tid; e < net.nbias / 4 + 1; e += RC_THREADS)
       ((f32x4*)BiasL)[e] = e < net.nbias / 4 ? gld<f32x4>(net.bias_all + 4 * e) : f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int r = tid; r < R; r += RC_THREADS) {
-      float s0 = 0.f, s1 = 0.f;
-      int64_t g = 0;
-      if (r < nrows) {
-        g = a.idx ? gld<int64_t>(a.idx + b0 + r) : (int64_t)(b0 + r);
-        if (MODE == RC_DECODE || a.x_relative) {
-          if (a.start_in) {  // decode(z, h_c) carries no start point
-            s0 = gld<float>(a.start_in + (size_t)(b0 + r) * 2 + 0);
-            s1 = gld<float>(a.start_in + (size_t)(b0 + r) * 2 + 1);
+    if (fast) {
+      // x[:,0,1:3] (Training_VAE.py:345) = elements 1, 2 of each row's first vector
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int v = u * RC_THREADS + tid;
+        if (v < NV) {
+          const int r = v / VPR, c = v - r * VPR;
+          if (c == 0) {
+            Start[r * 2 + 0] = r < nrows ? to_f(bufv[u][1]) : 0.f;
+            Start[r * 2 + 1] = r < nrows ? to_f(bufv[u][2]) : 0.f;
           }
-        } else {
-          s0 = to_f(gld<T>(xg + g * I + 1));  // x[:,0,1:3]  (Training_VAE.py:345)
-          s1 = to_f(gld<T>(xg + g * I + 2));
         }
       }
-      Start[r * 2 + 0] = s0;
-      Start[r * 2 + 1] = s1;
-      RowG[r] = g;
+    } else {
+      for (int r = tid; r < R; r += RC_THREADS) {
+        float s0 = 0.f, s1 = 0.f;
+        int64_t g = 0;
+        if (r < nrows) {
+          g = a.idx ? gld<int64_t>(a.idx + b0 + r) : (int64_t)(b0 + r);
+          if (MODE == RC_DECODE || a.x_relative) {
+            if (a.start_in) {  // decode(z, h_c) carries no start point
+              s0 = gld<float>(a.start_in + (size_t)(b0 + r) * 2 + 0);
+              s1 = gld<float>(a.start_in + (size_t)(b0 + r) * 2 + 1);
+            }
+          } else {
+            s0 = to_f(gld<T>(xg + g * I + 1));  // x[:,0,1:3]  (Training_VAE.py:345)
+            s1 = to_f(gld<T>(xg + g * I + 2));
+          }
+        }
+        Start[r * 2 + 0] = s0;
+        Start[r * 2 + 1] = s1;
+        RowG[r] = g;
+      }
     }
   }
   lds_barrier();
@@ -443,39 +530,20 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
     Cin[r * P.scin + 1] = to_t<T>(Start[r * 2 + 1]);
   }
   if (MODE != RC_DECODE) {
-    // relative transform fused into the tile load (Training_VAE.py:347-348)
-    constexpr int EPL = Op<T>::EPL, U = 12;
-    const bool vec = (I % EPL) == 0 && (((uintptr_t)xg) & 15) == 0;
     if (vec) {
-      // 16-B loads, U per thread issued before any is consumed; clamped indices so no load is
-      // conditional; the channel pattern (d = col mod D) is advanced without divisions
-      const int VPR = I / EPL, NV = R * VPR;
-      for (int base = 0; base < NV; base += U * RC_THREADS) {
-        V bufv[U];
+      if (fast) {
+        transform(0);
+      } else {
+        // 16-B loads, U per thread issued before any is consumed; clamped indices so no load is
+        // conditional
+        for (int base = 0; base < NV; base += U * RC_THREADS) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int v = min(base + u * RC_THREADS + tid, NV - 1);
-          const int r = v / VPR, c = v - r * VPR;
-          bufv[u] = gld<V>(xg + RowG[r] * I + c * EPL);  // RowG = row 0 past nrows
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int v = base + u * RC_THREADS + tid;
-          if (v < NV) {
+          for (int u = 0; u < U; ++u) {
+            const int v = min(base + u * RC_THREADS + tid, NV - 1);
             const int r = v / VPR, c = v - r * VPR;
-            const bool live = r < nrows;
-            const float s0 = a.x_relative ? 0.f : Start[r * 2 + 0];
-            const float s1 = a.x_relative ? 0.f : Start[r * 2 + 1];
-            int d = (c * EPL) % D;
-            V o;
-#pragma unroll
-            for (int e = 0; e < EPL; ++e) {
-              const float val = (float)bufv[u][e] - (d == 1 ? s0 : 0.f) - (d == 2 ? s1 : 0.f);
-              o[e] = to_t<T>(live ? val : 0.f);
-              d = d + 1 == D ? 0 : d + 1;
-            }
-            *(V*)(Xin + r * P.sx + c * EPL) = o;
+            bufv[u] = gld<V>(xg + RowG[r] * I + c * EPL);  // RowG = row 0 past nrows
           }
+          transform(base);
         }
       }
       if (net.Ip > I) {
@@ -544,27 +612,36 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
   const uint8_t* mkC1 = Mask + 1 * R * mw;
 
   // ---------------------------------------------------------------- the step interpreter
-  // Descriptors are copied BY VALUE (through a reference into global memory every field would be
-  // re-loaded after each global store of the epilogue: the compiler cannot rule out aliasing),
-  // and one step AHEAD: the next step's scalar loads are issued at the top of this step, so
-  // their latency hides behind this step's GEMM instead of sitting between two barriers.
-  StepDesc nx = a.steps[0];
+  const StepDesc* const StepsL = (const StepDesc*)(smem + P.oSteps);
+  auto sgpr = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); };
+  auto sptr = [&](uint32_t lo, uint32_t hi) { return (void*)(((uint64_t)sgpr(hi) << 32) | sgpr(lo)); };
   for (int si = 0; si < a.nsteps; ++si) {
-    const StepDesc st = nx;
+    // this step's descriptor and the next step's weight operand, from LDS, made scalar
+    const u32x4* dq = (const u32x4*)(StepsL + si);
+    const u32x4 q0 = dq[0], q1 = dq[1], q2 = dq[2], q3 = dq[3];
     const bool has_next = si + 1 < a.nsteps;
-    nx = a.steps[has_next ? si + 1 : si];
-    const void* const nW = nx.W;
-    const int nKp = nx.Kp;
-    const int nNp = nx.Np;
-    T* const d1 = st.dst1 >= 0 ? buf(st.dst1) : nullptr;
-    T* const d2 = st.dst2 >= 0 ? buf(st.dst2) : nullptr;
-    const int ld1 = st.dst1 >= 0 ? ld_of(st.dst1) : 0;
-    const int ld2 = st.dst2 >= 0 ? ld_of(st.dst2) : 0;
-    T* const g1 = (T*)st.g1;
-    T* const g2 = (T*)st.g2;
-    const int kind = st.epi, N = st.N;
-    uint8_t* const mko = Mask + (st.mask_out >= 0 ? st.mask_out : 0) * R * mw;
-    const uint8_t* const mki = Mask + (st.mask_in >= 0 ? st.mask_in : 0) * R * mw;
+    const u32x4* nq = (const u32x4*)(StepsL + (has_next ? si + 1 : si));
+    const u32x4 n0 = nq[0], n1 = nq[1];
+    const T* const W = (const T*)sptr(q0.x, q0.y);
+    T* const g1 = (T*)sptr(q0.z, q0.w);
+    T* const g2 = (T*)sptr(q1.x, q1.y);
+    const int Kp = (int)sgpr(q1.z), Np = (int)sgpr(q1.w), N = (int)sgpr(q2.x), bias_off = (int)sgpr(q2.y);
+    const uint32_t code = sgpr(q2.z);
+    const int off1 = (int)sgpr(q2.w), off2 = (int)sgpr(q3.x);
+    const uint32_t goff = sgpr(q3.y);
+    const int goff1 = (int)(goff & 0xFFFF), goff2 = (int)(goff >> 16);
+    const T* const nW = has_next ? (const T*)sptr(n0.x, n0.y) : (const T*)nullptr;
+    const int nKp = (int)sgpr(n1.z), nNp = (int)sgpr(n1.w);
+    const int xbuf = code & 15, kind = (code >> 4) & 15;
+    const int dst1 = (int)((code >> 8) & 15) - 1, dst2 = (int)((code >> 12) & 15) - 1;
+    const bool concat = (code >> 16) & 1, hc_o = (code >> 17) & 1;
+    const int mask_out = (int)((code >> 20) & 63) - 1, mask_in = (int)((code >> 26) & 63) - 1;
+    T* const d1 = dst1 >= 0 ? buf(dst1) : nullptr;
+    T* const d2 = dst2 >= 0 ? buf(dst2) : nullptr;
+    const int ld1 = dst1 >= 0 ? ld_of(dst1) : 0;
+    const int ld2 = dst2 >= 0 ? ld_of(dst2) : 0;
+    uint8_t* const mko = Mask + (mask_out >= 0 ? mask_out : 0) * R * mw;
+    const uint8_t* const mki = Mask + (mask_in >= 0 ? mask_in : 0) * R * mw;
 
 #if CVAE_DIAG_SUB
     g_sub_step = si;
@@ -572,109 +649,142 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
 #endif
     // the step's bias lives in LDS (copied once in the prologue): the epilogue issues no
     // global loads, so it never waits behind the weight prefetch (vmcnt retires in order)
-    const float* const biasL = BiasL + (st.bias_off >= 0 ? st.bias_off : net.nbias);
-    dense<T, R>(buf(st.xbuf), ld_of(st.xbuf), (const T*)st.W, st.Kp, st.Np, pre,
-                has_next ? (const T*)nW : (const T*)nullptr, nKp, nNp,
-                [&](int row, int f0, f32x4 v) {
+    const float* const biasL = BiasL + (bias_off >= 0 ? bias_off : net.nbias);
+
+    // One dense instance per epilogue kind (the switch is wave-uniform): each epilogue compiles
+    // straight-line with only its own live values.
+    auto run = [&](auto&& epi) {
+      dense<T, R>(buf(xbuf), ld_of(xbuf), W, Kp, Np, pre, nW, nKp, nNp, epi);
+    };
+    // forward hidden layer: ReLU, mask nibble, LDS dst(s), arena xT of consumers
+    auto epi_relu = [&](int row, int f0, f32x4 v) {
       if (CVAE_DIAG_NOEPI) return;
       const f32x4 b4 = *(const f32x4*)(biasL + f0);
       const bool live = row < nrows;
       f32x4 y;
-      if (kind == E_RELU) {  // forward hidden layer: ReLU, mask nibble, LDS dst(s), arena xT of consumers
-        uint32_t nib = 0;
+      uint32_t nib = 0;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          y[i] = live ? fmaxf(v[i] + b4[i], 0.f) : 0.f;  // zero-padded bias: pad features come out 0
-          nib |= (y[i] > 0.f ? 1u : 0u) << i;
-        }
-        mko[row * mw + (f0 >> 2)] = (uint8_t)nib;  // this lane owns (row, f0..f0+3): no atomics
-        if (st.concat && f0 >= N) return;  // part of a concatenation: never write its pads
-        put4(d1 + row * ld1 + st.off1 + f0, y);
-        if (d2) put4(d2 + row * ld2 + st.off2 + f0, y);
-        if (g1) put4T(g1 + (size_t)(st.goff1 + f0) * Bp + b0 + row, Bp, y);
-        if (g2) put4T(g2 + (size_t)(st.goff2 + f0) * Bp + b0 + row, Bp, y);
-        if (st.hc_out && a.hc_out && live && f0 < N) gst<f32x4>(a.hc_out + (size_t)(b0 + row) * H + f0, y);
-      } else if (kind == E_BWD) {  // backward: mask with the producer's ReLU bits
-        const uint32_t nib = mask4(mki, mw, row, f0);
+      for (int i = 0; i < 4; ++i) {
+        y[i] = live ? fmaxf(v[i] + b4[i], 0.f) : 0.f;  // zero-padded bias: pad features come out 0
+        nib |= (y[i] > 0.f ? 1u : 0u) << i;
+      }
+      mko[row * mw + (f0 >> 2)] = (uint8_t)nib;  // this lane owns (row, f0..f0+3): no atomics
+      if (concat && f0 >= N) return;  // part of a concatenation: never write its pads
+      put4(d1 + row * ld1 + off1 + f0, y);
+      if (d2) put4(d2 + row * ld2 + off2 + f0, y);
+      if (g1) put4T(g1 + (size_t)(goff1 + f0) * Bp + b0 + row, Bp, y);
+      if (g2) put4T(g2 + (size_t)(goff2 + f0) * Bp + b0 + row, Bp, y);
+      if (!TRAIN && hc_o && a.hc_out && live && f0 < N) gst<f32x4>(a.hc_out + (size_t)(b0 + row) * H + f0, y);
+    };
+    // backward: mask with the producer's ReLU bits
+    auto epi_bwd = [&](int row, int f0, f32x4 v) {
+      if (CVAE_DIAG_NOEPI) return;
+      const uint32_t nib = mask4(mki, mw, row, f0);
+      f32x4 y;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) y[i] = (nib >> i) & 1u ? v[i] : 0.f;
-        if (d1) put4(d1 + row * ld1 + f0, y);
-        put4T(g1 + (size_t)f0 * Bp + b0 + row, Bp, y);
-      } else if (kind == E_FC) {  // mu ‖ logvar, fp32 in LDS
+      for (int i = 0; i < 4; ++i) y[i] = (nib >> i) & 1u ? v[i] : 0.f;
+      if (d1) put4(d1 + row * ld1 + f0, y);
+      put4T(g1 + (size_t)f0 * Bp + b0 + row, Bp, y);
+    };
+    // mu ‖ logvar, fp32 in LDS
+    auto epi_fc = [&](int row, int f0, f32x4 v) {
+      if (CVAE_DIAG_NOEPI) return;
+      const f32x4 b4 = *(const f32x4*)(biasL + f0);
+      const bool live = row < nrows;
+      f32x4 y;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) y[i] = live ? v[i] + b4[i] : 0.f;
-        *(f32x4*)(MuLv + row * net.Zp2 + f0) = y;
-        if (MODE == RC_FWD && live) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int c = f0 + i;
-            if (c < Z) { if (a.mu_out) gst<float>(a.mu_out + (size_t)(b0 + row) * Z + c, y[i]); }
-            else if (c < 2 * Z && a.lv_out) gst<float>(a.lv_out + (size_t)(b0 + row) * Z + c - Z, y[i]);
-          }
-        }
-      } else if (kind == E_LOSS) {  // recon r = acc + bias (fp32); dL/dr → GL (LDS) + gT
-        // target x_rel from the resident input tile; GL overwrites it in place below
-        // (same lane, same elements), so no other reader is affected
-        const f32x4 xr = get4(Xin + row * P.sx + f0);
-        int s = fdiv(f0, inv_D), d = f0 - s * D;
-        T* gcol = g1 + (size_t)f0 * Bp + b0 + row;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float gi = 0.f;
-          if (live && f0 + i < I) {
-            const float r = v[i] + b4[i];
-            const float diff = r - xr[i];
-            s_recon += prim ? diff * diff : 0.f;
-            gi = a.w_recon * 2.f * diff * inv_BSD;
-            if (s == 0 && (d == 1 || d == 2) && use_start) {
-              s_start += prim ? diff * diff : 0.f;
-              gi += a.w_start * 2.f * diff * inv_2B;
-            }
-            if (d == 0) {
-              Rch0[row * S + s] = r;
-              if (s == 0 && use_time) {
-                s_t0 += prim ? r * r : 0.f;
-                gi += a.w_time * 2.f * r * inv_B;
-              }
-              Gd0[row * S + s] = gi;
-            }
-          }
-          y[i] = gi;
-          // the time channel (d == 0) is finished by the fix-up pass once its neighbours exist
-          if (!CVAE_DIAG_NOSTORE && (d != 0 || f0 + i >= I)) gst<T>(gcol + (size_t)i * Bp, to_t<T>(gi));
-          if (++d == D) { d = 0; ++s; }
-        }
-        put4(GL + row * P.sx + f0, y);  // d == 0 entries are overwritten by the fix-up pass
-      } else if (kind == E_RECON) {
-        if (!a.recon_out || !live) return;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (f0 + i < I) gst<float>(a.recon_out + (size_t)(b0 + row) * I + f0 + i, v[i] + b4[i]);
-      } else if (kind == E_D0B) {  // decoder L0 backward: dz and the decoder's share of dh_c
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int c = f0 + i;
-          if (c < Z) Dz[row * Z + c] = v[i];
-          else if (c < Z + H) Dhc2[row * H + c - Z] = v[i];
-        }
-      } else {  // E_FCB: dh = G_fc·W_fc → [dh_traj ‖ dh_c(fc share)]   (H % 4 == 0: no straddle)
-        if (f0 < H) {
-          const uint32_t nib = mask4(mkEl, mw, row, f0);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) y[i] = (nib >> i) & 1u ? v[i] : 0.f;
-          put4(P1b + row * P.sp + f0, y);
-          put4T(g1 + (size_t)f0 * Bp + b0 + row, Bp, y);
-        } else if (f0 < 2 * H) {
-          const int c = f0 - H;
-          const uint32_t nib = mask4(mkC1, mw, row, c);
-          const f32x4 dh2 = *(const f32x4*)(Dhc2 + row * H + c);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) y[i] = (nib >> i) & 1u ? v[i] + dh2[i] : 0.f;
-          put4(Q + row * P.shc + c, y);
-          put4T(g2 + (size_t)c * Bp + b0 + row, Bp, y);
+      for (int i = 0; i < 4; ++i) y[i] = live ? v[i] + b4[i] : 0.f;
+      *(f32x4*)(MuLv + row * net.Zp2 + f0) = y;
+      if (MODE == RC_FWD && live) {  // Z % 4 == 0: a 4-feature group is all mu or all logvar
+        if (f0 < Z) {
+          if (a.mu_out) gst<f32x4>(a.mu_out + (size_t)(b0 + row) * Z + f0, y);
+        } else if (f0 < 2 * Z && a.lv_out) {
+          gst<f32x4>(a.lv_out + (size_t)(b0 + row) * Z + f0 - Z, y);
         }
       }
-    });
+    };
+    // recon r = acc + bias (fp32); dL/dr → GL (LDS) + gT
+    auto epi_loss = [&](int row, int f0, f32x4 v) {
+      if (CVAE_DIAG_NOEPI) return;
+      const f32x4 b4 = *(const f32x4*)(biasL + f0);
+      const bool live = row < nrows;
+      f32x4 y;
+      // target x_rel from the resident input tile; GL overwrites it in place below
+      // (same lane, same elements), so no other reader is affected
+      const f32x4 xr = get4(Xin + row * P.sx + f0);
+      int s = fdiv(f0, inv_D), d = f0 - s * D;
+      T* gcol = g1 + (size_t)f0 * Bp + b0 + row;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float gi = 0.f;
+        if (live && f0 + i < I) {
+          const float r = v[i] + b4[i];
+          const float diff = r - xr[i];
+          s_recon += prim ? diff * diff : 0.f;
+          gi = a.w_recon * 2.f * diff * inv_BSD;
+          if (s == 0 && (d == 1 || d == 2) && use_start) {
+            s_start += prim ? diff * diff : 0.f;
+            gi += a.w_start * 2.f * diff * inv_2B;
+          }
+          if (d == 0) {
+            Rch0[row * S + s] = r;
+            if (s == 0 && use_time) {
+              s_t0 += prim ? r * r : 0.f;
+              gi += a.w_time * 2.f * r * inv_B;
+            }
+            Gd0[row * S + s] = gi;
+          }
+        }
+        y[i] = gi;
+        // the time channel (d == 0) is finished by the fix-up pass once its neighbours exist
+        if (!CVAE_DIAG_NOSTORE && (d != 0 || f0 + i >= I)) gst<T>(gcol + (size_t)i * Bp, to_t<T>(gi));
+        if (++d == D) { d = 0; ++s; }
+      }
+      put4(GL + row * P.sx + f0, y);  // d == 0 entries are overwritten by the fix-up pass
+    };
+    auto epi_recon = [&](int row, int f0, f32x4 v) {
+      if (CVAE_DIAG_NOEPI) return;
+      if (!a.recon_out || row >= nrows) return;
+      const f32x4 b4 = *(const f32x4*)(biasL + f0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (f0 + i < I) gst<float>(a.recon_out + (size_t)(b0 + row) * I + f0 + i, v[i] + b4[i]);
+    };
+    // decoder L0 backward: dz and the decoder's share of dh_c (Z, H multiples of 4: no straddle)
+    auto epi_d0b = [&](int row, int f0, f32x4 v) {
+      if (CVAE_DIAG_NOEPI) return;
+      if (f0 < Z) *(f32x4*)(Dz + row * Z + f0) = v;
+      else if (f0 < Z + H) *(f32x4*)(Dhc2 + row * H + f0 - Z) = v;
+    };
+    // dh = G_fc·W_fc → [dh_traj ‖ dh_c(fc share)]   (H % 4 == 0: no straddle)
+    auto epi_fcb = [&](int row, int f0, f32x4 v) {
+      if (CVAE_DIAG_NOEPI) return;
+      f32x4 y;
+      if (f0 < H) {
+        const uint32_t nib = mask4(mkEl, mw, row, f0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) y[i] = (nib >> i) & 1u ? v[i] : 0.f;
+        put4(P1b + row * P.sp + f0, y);
+        put4T(g1 + (size_t)f0 * Bp + b0 + row, Bp, y);
+      } else if (f0 < 2 * H) {
+        const int c = f0 - H;
+        const uint32_t nib = mask4(mkC1, mw, row, c);
+        const f32x4 dh2 = *(const f32x4*)(Dhc2 + row * H + c);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) y[i] = (nib >> i) & 1u ? v[i] + dh2[i] : 0.f;
+        put4(Q + row * P.shc + c, y);
+        put4T(g2 + (size_t)c * Bp + b0 + row, Bp, y);
+      }
+    };
+    switch (kind) {
+      case E_RELU: run(epi_relu); break;
+      case E_FC: if constexpr (MODE != RC_DECODE) run(epi_fc); break;
+      case E_LOSS: if constexpr (TRAIN) run(epi_loss); break;
+      case E_RECON: if constexpr (!TRAIN) run(epi_recon); break;
+      case E_BWD: if constexpr (TRAIN) run(epi_bwd); break;
+      case E_D0B: if constexpr (TRAIN) run(epi_d0b); break;
+      default: if constexpr (TRAIN) run(epi_fcb); break;
+    }
     lds_barrier();
 #if CVAE_DIAG_SUB
     SUBSTAMP(4);
