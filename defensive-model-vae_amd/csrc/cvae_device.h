@@ -3,9 +3,10 @@
 //
 // Layout conventions:
 //  * Every Linear layer l has padded dims Kp = roundup(in, 32), Np = roundup(out, 32).
-//  * Device weight copies in the operand dtype T (fp32 or bf16):
-//      Wf[Np][Kp]  (= nn.Linear (out,in) zero-padded) — B operand of the forward GEMM
-//      Wb[Kp][Np]  (= Wᵀ zero-padded)                  — B operand of the dX GEMM
+//  * Device weight copies in the operand dtype T (fp32 or bf16), in MFMA fragment order
+//    (frag_off below):
+//      Wf ~ [Np][Kp]  (= nn.Linear (out,in) zero-padded) — operand of the forward GEMM
+//      Wb ~ [Kp][Np]  (= Wᵀ zero-padded)                  — operand of the dX GEMM
 //    plus a padded fp32 bias[Np].  The fp32 master parameters stay in the
 //    caller's flat state_dict-ordered buffer.
 //  * Activation arena, feature-major ("transposed") [features][Bp] in T:
@@ -84,6 +85,18 @@ __device__ __forceinline__ f32x4 mfma_chunk(f32x4 a, f32x4 b, f32x4 c) {
 }
 __device__ __forceinline__ f32x4 mfma_chunk(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// Operand copies (Wf, Wb) are stored in MFMA FRAGMENT ORDER: for n-tile t (16 output rows) and
+// K chunk kc, the 64 lanes' 16-B fragments are contiguous — 1 KB per (t, kc) — so one wave load
+// instruction reads 8 full 128-B lines.  (Row-major [Np][Kp] makes each instruction 16 rows x
+// 64 B: texture-address bound at ~38 GB/s per CU, measured 3.7x slower — scripts/ubench/wload.hip.)
+// Element (n, k) of an operand matrix with padded K extent Kp:
+template <typename T>
+__host__ __device__ inline size_t frag_off(int n, int k, int Kp) {
+  constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC;
+  const int t = n >> 4, r = n & 15, kc = k / KC, kk = k - kc * KC, q = kk / EPL, e = kk - q * EPL;
+  return ((size_t)(t * (Kp / KC) + kc) * 64 + q * 16 + r) * EPL + e;
 }
 
 template <typename T> __device__ __forceinline__ T to_t(float v);

@@ -84,6 +84,15 @@ __device__ __forceinline__ int tile_row(int m, int r16) { return R >= 16 ? m * 1
 #ifndef CVAE_DIAG_NOMFMA
 #define CVAE_DIAG_NOMFMA 0
 #endif
+#ifndef CVAE_DIAG_NOLDSW
+#define CVAE_DIAG_NOLDSW 0
+#endif
+#ifndef CVAE_DIAG_NOBAR
+#define CVAE_DIAG_NOBAR 0
+#endif
+#ifndef CVAE_DIAG_NOBIAS
+#define CVAE_DIAG_NOBIAS 0
+#endif
 #if CVAE_DIAG_SUB
 // [block][wave][step][5]: entry, weights arrived, MFMAs done, epilogue done, barrier passed
 __device__ unsigned long long* g_sub;
@@ -104,7 +113,7 @@ enum { E_RELU = 0, E_FC = 1, E_LOSS = 2, E_RECON = 3, E_BWD = 4, E_D0B = 5, E_FC
 
 // One step of the interpreter as the host builds it (cvae_capi.hip build_steps) ...
 struct StepSpec {
-  const void* W;     // B operand [Np][Kp] (forward Wf or backward Wb)
+  const void* W;     // weight operand ~[Np][Kp] in fragment order (forward Wf or backward Wb)
   int bias_off;      // offset of this step's bias in the LDS bias copy (-1: zeros, backward)
   void* g1;          // arena destination (feature-major), nullable
   void* g2;
@@ -226,6 +235,9 @@ __host__ __device__ inline LdsPlan lds_plan(const NetDev& n, int R, int tsize) {
 // issued before the epilogue's global stores, so waiting for them never waits for those
 // stores (vmcnt retires in order).
 constexpr int NKB = 4;
+#ifndef CVAE_LATE_PREFETCH
+#define CVAE_LATE_PREFETCH 0
+#endif
 
 template <typename T>
 struct WBlock {
@@ -236,24 +248,31 @@ template <typename T>
 __device__ __forceinline__ void load_block(WBlock<T>& wb, const T* __restrict__ W, int Kp, int Np, int g, int blk) {
   using V = typename Op<T>::V;
   constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC;
-  const int lane = threadIdx.x & 63, r16 = lane & 15, kq = (lane >> 4) * EPL;
+  const int lane = threadIdx.x & 63;
   const int nk = Kp / KC, ng = Np / RC_GW;
   g = min(g, ng - 1);
-  const T* w0 = W + (size_t)(g * RC_GW + r16) * Kp + kq;
+  // fragment order (frag_off): n-tile t, chunk kc → 1 KB at ((t * nk + kc) * 64 + lane) * EPL
+  const T* w0 = W + (size_t)lane * EPL;
 #pragma unroll
   for (int u = 0; u < NKB; ++u) {
     const int kc = min(blk * NKB + u, nk - 1);
 #pragma unroll
-    for (int j = 0; j < RC_NT; ++j) wb.b[u][j] = CVAE_DIAG_NOWLOAD ? V{} : gld<V>(w0 + (size_t)j * 16 * Kp + kc * KC);
+    for (int j = 0; j < RC_NT; ++j) {
+      const int t = g * RC_NT + j;
+      wb.b[u][j] = CVAE_DIAG_NOWLOAD ? V{} : gld<V>(w0 + (size_t)(t * nk + kc) * 64 * EPL);
+    }
   }
 }
 
 // epi(row, f0, v) receives v[i] = Y[row][f0 + i], i = 0..3: the MFMA computes Yᵀ = W·Xᵀ
 // (A = weights, B = activations), so a lane's accumulator holds FOUR CONSECUTIVE FEATURES of
 // one row — one 8/16-B LDS store, one float4 bias and one 4-bit mask nibble per call.
-template <typename T, int R, class Epi>
+// BIAS: the group's 4 bias values are read from LDS at the top of the item — before the X reads
+// and MFMAs — so their latency hides there instead of opening the epilogue.
+template <typename T, int R, bool BIAS, class Epi>
 __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T* __restrict__ W, int Kp, int Np,
-                                      WBlock<T>& pre, const T* nW, int nKp, int nNp, Epi&& epi) {
+                                      WBlock<T>& pre, const T* nW, int nKp, int nNp, const float* biasL,
+                                      Epi&& epi) {
   using V = typename Op<T>::V;
   constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC, MT = R >= 16 ? R / 16 : 1;
   const int lane = threadIdx.x & 63, wave = wave_id();
@@ -273,6 +292,10 @@ __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T
   for (int it = 0; it < nitems; ++it) {
     const int gi = it / nblk, blk = it - gi * nblk;
     const int g = wave + gi * RC_NW;
+    f32x4 b4[RC_NT];
+#pragma unroll
+    for (int j = 0; j < RC_NT; ++j)
+      b4[j] = BIAS ? *(const f32x4*)(biasL + g * RC_GW + j * 16 + (lane >> 4) * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
     const WBlock<T> cur = pre;
 #if CVAE_DIAG_SUB
     if (it == 0) {
@@ -280,7 +303,8 @@ __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T
       SUBSTAMP(1);
     }
 #endif
-    {  // next item: this step's next block/group, else the next step's first block
+    // next item: this step's next block/group, else the next step's first block
+    auto prefetch = [&]() {
       const int it2 = it + 1;
       const bool same = it2 < nitems;
       const int gi2 = it2 / nblk;
@@ -290,7 +314,8 @@ __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T
       const int g2 = same ? wave + gi2 * RC_NW : wave;
       const int blk2 = same ? it2 - gi2 * nblk : 0;
       load_block(pre, W2, Kp2, Np2, g2, blk2);
-    }
+    };
+    if (!CVAE_LATE_PREFETCH) prefetch();
     // all LDS reads of the block first (one lgkmcnt wait per block, not per chunk), then the
     // MFMAs unconditionally: chunks past K read a clamped (valid) address and are zeroed, so a
     // short block costs a few idle MFMAs instead of branches and per-chunk waits
@@ -312,6 +337,10 @@ __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T
           if (!CVAE_DIAG_NOMFMA) acc[j][m] = mfma_chunk(cur.b[u][j], xb, acc[j][m]);
       }
     }
+    // issued behind the MFMAs: all waves issue their loads right after a barrier, and the CU's
+    // vector-memory path (~64 B/clk) takes hundreds of cycles to accept them; placed here the
+    // wave's MFMAs already run while its load instructions queue
+    if (CVAE_LATE_PREFETCH) prefetch();
 #if CVAE_DIAG_SUB
     if (it == 0) SUBSTAMP(2);
 #endif
@@ -320,7 +349,7 @@ __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T
       for (int j = 0; j < RC_NT; ++j)
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
-          epi(tile_row<R>(m, r16), g * RC_GW + j * 16 + (lane >> 4) * 4, acc[j][m]);
+          epi(tile_row<R>(m, r16), g * RC_GW + j * 16 + (lane >> 4) * 4, acc[j][m], b4[j]);
           acc[j][m] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
 #if CVAE_DIAG_SUB
@@ -333,7 +362,8 @@ __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T
 // Workgroup barrier for LDS hand-offs only: no vmcnt drain, so global stores and the weight
 // prefetch stay in flight across it (nothing in this kernel reads back its global stores).
 __device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if (CVAE_DIAG_NOBAR) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 template <typename T>
@@ -369,6 +399,58 @@ __device__ __forceinline__ void put4T(T* base, int Bp, f32x4 v) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) gst<T>(base + (size_t)i * Bp, to_t<T>(v[i]));
 }
+// Feature-major arena store of one lane's 4 consecutive features as ONE wide store.  The 4
+// lanes q = lane & 3 of a quad hold rows r0..r0+3 (r0 = row & ~3) of the same 4 features; a 4x4
+// transpose across the quad (two DPP quad_perm exchanges) leaves lane q with feature f0+q of
+// rows r0..r0+3, contiguous in the arena: one 8-B (bf16) / 16-B (fp32) store instead of four
+// 2/4-B ones.  Per-CU store issue is ~one wave store instruction per 25 cycles whatever its width
+// (MI355X_MICROARCH.md, plain-store rate), so the instruction count is what costs.
+__device__ __forceinline__ uint32_t dpp_xor1(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+}
+__device__ __forceinline__ uint32_t dpp_xor2(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+}
+__device__ __forceinline__ uint32_t pack_bf16(float a, float b) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  bf16x2 h;
+  h[0] = (__bf16)a;
+  h[1] = (__bf16)b;
+  return __builtin_bit_cast(uint32_t, h);
+}
+// base = arena row of feature f0 (+ b0); row = this lane's tile row (row & 3 == lane & 3)
+__device__ __forceinline__ void put4Tq(__bf16* base, int Bp, int row, f32x4 y) {
+  if (CVAE_DIAG_NOSTORE) return;
+  const int lane = threadIdx.x & 63;
+  const bool b1 = lane & 1, b2 = lane & 2;
+  const uint32_t P0 = pack_bf16(y[0], y[1]), P1 = pack_bf16(y[2], y[3]);
+  // distance 2: rows {0,1} keep features {0,1} and take rows {2,3}'s; rows {2,3} the converse
+  const uint32_t R = dpp_xor2(b2 ? P0 : P1);
+  const uint32_t D0 = b2 ? R : P0, D1 = b2 ? P1 : R;
+  // distance 1, 16-bit halves: even lanes send (hi D0, hi D1), odd lanes (lo D0, lo D1)
+  const uint32_t R2 = dpp_xor1(b1 ? __builtin_amdgcn_perm(D1, D0, 0x05040100u)
+                                  : __builtin_amdgcn_perm(D1, D0, 0x07060302u));
+  const uint32_t Q0 = b1 ? __builtin_amdgcn_perm(D0, R2, 0x07060100u) : __builtin_amdgcn_perm(R2, D0, 0x05040100u);
+  const uint32_t Q1 = b1 ? __builtin_amdgcn_perm(D1, R2, 0x07060302u) : __builtin_amdgcn_perm(R2, D1, 0x07060100u);
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  gst<u32x2>(base + (size_t)(lane & 3) * Bp + (row & ~3), u32x2{Q0, Q1});
+}
+__device__ __forceinline__ void put4Tq(float* base, int Bp, int row, f32x4 y) {
+  if (CVAE_DIAG_NOSTORE) return;
+  const int lane = threadIdx.x & 63;
+  const bool b1 = lane & 1, b2 = lane & 2;
+  auto u = [](float f) { return __builtin_bit_cast(uint32_t, f); };
+  auto f = [](uint32_t v) { return __builtin_bit_cast(float, v); };
+  // distance 2: rows {0,1} send features {2,3}, rows {2,3} send features {0,1}
+  const uint32_t Ra = dpp_xor2(u(b2 ? y[0] : y[2])), Rb = dpp_xor2(u(b2 ? y[1] : y[3]));
+  const float A0 = b2 ? f(Ra) : y[0], A1 = b2 ? f(Rb) : y[1];
+  const float A2 = b2 ? y[2] : f(Ra), A3 = b2 ? y[3] : f(Rb);
+  // distance 1: even lanes send (A1, A3), odd lanes (A0, A2)
+  const uint32_t Rc = dpp_xor1(u(b1 ? A0 : A1)), Rd = dpp_xor1(u(b1 ? A2 : A3));
+  const f32x4 q = b1 ? f32x4{f(Rc), A1, f(Rd), A3} : f32x4{A0, f(Rc), A2, f(Rd)};
+  gst<f32x4>(base + (size_t)(lane & 3) * Bp + (row & ~3), q);
+}
+
 // the 4 ReLU bits of features f0..f0+3 (f0 % 4 == 0) of one row: one byte per 4-feature group
 __device__ __forceinline__ uint32_t mask4(const uint8_t* mk, int mw, int row, int f0) {
   return mk[row * mw + (f0 >> 2)];
@@ -654,12 +736,14 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
     // One dense instance per epilogue kind (the switch is wave-uniform): each epilogue compiles
     // straight-line with only its own live values.
     auto run = [&](auto&& epi) {
-      dense<T, R>(buf(xbuf), ld_of(xbuf), W, Kp, Np, pre, nW, nKp, nNp, epi);
+      dense<T, R, true>(buf(xbuf), ld_of(xbuf), W, Kp, Np, pre, nW, nKp, nNp, biasL, epi);
+    };
+    auto run_nb = [&](auto&& epi) {  // backward steps: no bias
+      dense<T, R, false>(buf(xbuf), ld_of(xbuf), W, Kp, Np, pre, nW, nKp, nNp, biasL, epi);
     };
     // forward hidden layer: ReLU, mask nibble, LDS dst(s), arena xT of consumers
-    auto epi_relu = [&](int row, int f0, f32x4 v) {
+    auto epi_relu = [&](int row, int f0, f32x4 v, f32x4 b4) {
       if (CVAE_DIAG_NOEPI) return;
-      const f32x4 b4 = *(const f32x4*)(biasL + f0);
       const bool live = row < nrows;
       f32x4 y;
       uint32_t nib = 0;
@@ -668,28 +752,27 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
         y[i] = live ? fmaxf(v[i] + b4[i], 0.f) : 0.f;  // zero-padded bias: pad features come out 0
         nib |= (y[i] > 0.f ? 1u : 0u) << i;
       }
-      mko[row * mw + (f0 >> 2)] = (uint8_t)nib;  // this lane owns (row, f0..f0+3): no atomics
+      if (!CVAE_DIAG_NOLDSW) mko[row * mw + (f0 >> 2)] = (uint8_t)nib;  // this lane owns (row, f0..f0+3): no atomics
       if (concat && f0 >= N) return;  // part of a concatenation: never write its pads
-      put4(d1 + row * ld1 + off1 + f0, y);
-      if (d2) put4(d2 + row * ld2 + off2 + f0, y);
-      if (g1) put4T(g1 + (size_t)(goff1 + f0) * Bp + b0 + row, Bp, y);
-      if (g2) put4T(g2 + (size_t)(goff2 + f0) * Bp + b0 + row, Bp, y);
+      if (!CVAE_DIAG_NOLDSW) put4(d1 + row * ld1 + off1 + f0, y);
+      if (d2 && !CVAE_DIAG_NOLDSW) put4(d2 + row * ld2 + off2 + f0, y);
+      if (g1) put4Tq(g1 + (size_t)(goff1 + f0) * Bp + b0, Bp, row, y);
+      if (g2) put4Tq(g2 + (size_t)(goff2 + f0) * Bp + b0, Bp, row, y);
       if (!TRAIN && hc_o && a.hc_out && live && f0 < N) gst<f32x4>(a.hc_out + (size_t)(b0 + row) * H + f0, y);
     };
     // backward: mask with the producer's ReLU bits
-    auto epi_bwd = [&](int row, int f0, f32x4 v) {
+    auto epi_bwd = [&](int row, int f0, f32x4 v, f32x4) {
       if (CVAE_DIAG_NOEPI) return;
       const uint32_t nib = mask4(mki, mw, row, f0);
       f32x4 y;
 #pragma unroll
       for (int i = 0; i < 4; ++i) y[i] = (nib >> i) & 1u ? v[i] : 0.f;
       if (d1) put4(d1 + row * ld1 + f0, y);
-      put4T(g1 + (size_t)f0 * Bp + b0 + row, Bp, y);
+      put4Tq(g1 + (size_t)f0 * Bp + b0, Bp, row, y);
     };
     // mu ‖ logvar, fp32 in LDS
-    auto epi_fc = [&](int row, int f0, f32x4 v) {
+    auto epi_fc = [&](int row, int f0, f32x4 v, f32x4 b4) {
       if (CVAE_DIAG_NOEPI) return;
-      const f32x4 b4 = *(const f32x4*)(biasL + f0);
       const bool live = row < nrows;
       f32x4 y;
 #pragma unroll
@@ -704,9 +787,8 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
       }
     };
     // recon r = acc + bias (fp32); dL/dr → GL (LDS) + gT
-    auto epi_loss = [&](int row, int f0, f32x4 v) {
+    auto epi_loss = [&](int row, int f0, f32x4 v, f32x4 b4) {
       if (CVAE_DIAG_NOEPI) return;
-      const f32x4 b4 = *(const f32x4*)(biasL + f0);
       const bool live = row < nrows;
       f32x4 y;
       // target x_rel from the resident input tile; GL overwrites it in place below
@@ -742,22 +824,21 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
       }
       put4(GL + row * P.sx + f0, y);  // d == 0 entries are overwritten by the fix-up pass
     };
-    auto epi_recon = [&](int row, int f0, f32x4 v) {
+    auto epi_recon = [&](int row, int f0, f32x4 v, f32x4 b4) {
       if (CVAE_DIAG_NOEPI) return;
       if (!a.recon_out || row >= nrows) return;
-      const f32x4 b4 = *(const f32x4*)(biasL + f0);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         if (f0 + i < I) gst<float>(a.recon_out + (size_t)(b0 + row) * I + f0 + i, v[i] + b4[i]);
     };
     // decoder L0 backward: dz and the decoder's share of dh_c (Z, H multiples of 4: no straddle)
-    auto epi_d0b = [&](int row, int f0, f32x4 v) {
+    auto epi_d0b = [&](int row, int f0, f32x4 v, f32x4) {
       if (CVAE_DIAG_NOEPI) return;
       if (f0 < Z) *(f32x4*)(Dz + row * Z + f0) = v;
       else if (f0 < Z + H) *(f32x4*)(Dhc2 + row * H + f0 - Z) = v;
     };
     // dh = G_fc·W_fc → [dh_traj ‖ dh_c(fc share)]   (H % 4 == 0: no straddle)
-    auto epi_fcb = [&](int row, int f0, f32x4 v) {
+    auto epi_fcb = [&](int row, int f0, f32x4 v, f32x4) {
       if (CVAE_DIAG_NOEPI) return;
       f32x4 y;
       if (f0 < H) {
@@ -765,7 +846,7 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
 #pragma unroll
         for (int i = 0; i < 4; ++i) y[i] = (nib >> i) & 1u ? v[i] : 0.f;
         put4(P1b + row * P.sp + f0, y);
-        put4T(g1 + (size_t)f0 * Bp + b0 + row, Bp, y);
+        put4Tq(g1 + (size_t)f0 * Bp + b0, Bp, row, y);
       } else if (f0 < 2 * H) {
         const int c = f0 - H;
         const uint32_t nib = mask4(mkC1, mw, row, c);
@@ -773,7 +854,7 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
 #pragma unroll
         for (int i = 0; i < 4; ++i) y[i] = (nib >> i) & 1u ? v[i] + dh2[i] : 0.f;
         put4(Q + row * P.shc + c, y);
-        put4T(g2 + (size_t)c * Bp + b0 + row, Bp, y);
+        put4Tq(g2 + (size_t)c * Bp + b0, Bp, row, y);
       }
     };
     switch (kind) {
@@ -781,9 +862,9 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
       case E_FC: if constexpr (MODE != RC_DECODE) run(epi_fc); break;
       case E_LOSS: if constexpr (TRAIN) run(epi_loss); break;
       case E_RECON: if constexpr (!TRAIN) run(epi_recon); break;
-      case E_BWD: if constexpr (TRAIN) run(epi_bwd); break;
-      case E_D0B: if constexpr (TRAIN) run(epi_d0b); break;
-      default: if constexpr (TRAIN) run(epi_fcb); break;
+      case E_BWD: if constexpr (TRAIN) run_nb(epi_bwd); break;
+      case E_D0B: if constexpr (TRAIN) run_nb(epi_d0b); break;
+      default: if constexpr (TRAIN) run_nb(epi_fcb); break;
     }
     lds_barrier();
 #if CVAE_DIAG_SUB

@@ -98,8 +98,8 @@ __device__ __forceinline__ void apply_weight(const LayerDev& L, int o, int i, fl
     return;
   }
   if (CVAE_DIAG_NOWPACK && MODE == PM_ADAM) return;
-  ((T*)L.Wf)[(size_t)o * L.Kp + i] = to_t<T>(w);
-  ((T*)L.Wb)[(size_t)i * L.Np + o] = to_t<T>(w);
+  ((T*)L.Wf)[frag_off<T>(o, i, L.Kp)] = to_t<T>(w);  // forward operand: rows o, K = inputs
+  ((T*)L.Wb)[frag_off<T>(i, o, L.Np)] = to_t<T>(w);  // dX operand (Wᵀ): rows i, K = outputs
 }
 
 template <int MODE>
