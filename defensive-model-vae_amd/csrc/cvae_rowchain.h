@@ -289,8 +289,11 @@ __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T
   for (int j = 0; j < RC_NT; ++j)
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[j][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // (group, block) of the current and the next item, advanced without integer division
+  int gi = 0, blk = 0;
   for (int it = 0; it < nitems; ++it) {
-    const int gi = it / nblk, blk = it - gi * nblk;
+    const bool wrap = blk + 1 == nblk;
+    const int gi_n = wrap ? gi + 1 : gi, blk_n = wrap ? 0 : blk + 1;
     const int g = wave + gi * RC_NW;
     f32x4 b4[RC_NT];
 #pragma unroll
@@ -305,14 +308,12 @@ __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T
 #endif
     // next item: this step's next block/group, else the next step's first block
     auto prefetch = [&]() {
-      const int it2 = it + 1;
-      const bool same = it2 < nitems;
-      const int gi2 = it2 / nblk;
+      const bool same = it + 1 < nitems;
       const T* W2 = same ? W : (nW ? nW : W);
       const int Kp2 = same ? Kp : (nW ? nKp : Kp);
       const int Np2 = same ? Np : (nW ? nNp : Np);
-      const int g2 = same ? wave + gi2 * RC_NW : wave;
-      const int blk2 = same ? it2 - gi2 * nblk : 0;
+      const int g2 = same ? wave + gi_n * RC_NW : wave;
+      const int blk2 = same ? blk_n : 0;
       load_block(pre, W2, Kp2, Np2, g2, blk2);
     };
     if (!CVAE_LATE_PREFETCH) prefetch();
@@ -356,6 +357,8 @@ __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T
       if (it == nblk - 1) SUBSTAMP(3);
 #endif
     }
+    gi = gi_n;
+    blk = blk_n;
   }
 }
 
@@ -514,127 +517,117 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
   }
   stamp();
 
-  // ---------------------------------------------------------------- prologue: zero + start points + x tile
-  // Fast path (absolute trajectories, 16-B aligned rows, one load pass): every thread loads its
-  // x vectors straight away — the row index is read through the clamped idx itself, not through
-  // an LDS table behind a barrier — and the start points come from each row's first vector, so
-  // the tile costs one dependent global latency (two with an idx gather) instead of three.
-  constexpr int EPL = Op<T>::EPL, U = 12;
+  // ---------------------------------------------------------------- prologue: x tile, start points, LDS state
+  auto zero = [&](void* p, int bytes) {
+    f32x4* q = (f32x4*)p;
+    for (int e = tid; e < bytes / 16; e += RC_THREADS) q[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  auto setup_lds = [&]() {  // step table, biases, zeroed concatenation buffers and masks
+    for (int e = tid; e < a.nsteps * 4; e += RC_THREADS)
+      ((u32x4*)(smem + P.oSteps))[e] = gld<u32x4>((const u32x4*)a.steps + e);
+    for (int e = tid; e < net.nbias / 4 + 1; e += RC_THREADS)
+      ((f32x4*)BiasL)[e] = e < net.nbias / 4 ? gld<f32x4>(net.bias_all + 4 * e) : f32x4{0.f, 0.f, 0.f, 0.f};
+    zero(Hc, R * P.shc * (int)sizeof(T));
+    zero(Dec, R * P.sdec * (int)sizeof(T));
+    zero(Mask, rup(n_masks(net) * R * mw, 16));
+  };
+  // Fast path (absolute trajectories, 16-B aligned rows): task v = one 16-B vector of one row,
+  // the 4 lanes of a quad holding the same vector of 4 consecutive rows.  Every lane loads its
+  // vector and its row's first vector (the start point x[:,0,1:3], Training_VAE.py:345) at once
+  // — no LDS round trip or barrier before the relative transform (:347-348) — writes the LDS
+  // tile, and stores the feature-major arena copy of the tile as quad-transposed 8/16-B stores.
+  constexpr int EPL = Op<T>::EPL, U = 5;
   const int VPR = I / EPL, NV = R * VPR;
   const bool vec = MODE != RC_DECODE && (I % EPL) == 0 && (((uintptr_t)xg) & 15) == 0;
   const bool fast = vec && !a.x_relative && NV <= U * RC_THREADS;
-  V bufv[U];
-  // relative transform (Training_VAE.py:347-348) of the loaded vectors into the LDS tile;
-  // the channel pattern (d = col mod D) is advanced without divisions
-  auto transform = [&](int base) {
+  if (fast) {
+    const float inv_VPR = 1.f / (float)VPR, inv_Dd = 1.f / (float)D;
+    const int last = max(a.batch - 1, 0);
+    V xv[U], x0[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int v = base + u * RC_THREADS + tid;
-      if (v < NV) {
-        const int r = v / VPR, c = v - r * VPR;
-        const bool live = r < nrows;
-        const float s0 = a.x_relative ? 0.f : Start[r * 2 + 0];
-        const float s1 = a.x_relative ? 0.f : Start[r * 2 + 1];
-        int d = (c * EPL) % D;
+      if (u * RC_THREADS < NV) {  // wave-uniform
+        const int v = min(u * RC_THREADS + tid, NV - 1);
+        const int w = v >> 2, rq = fdiv(w, inv_VPR), c = w - rq * VPR, row = 4 * rq + (v & 3);
+        const int rr = min(b0 + row, last);  // rows past the batch re-read a valid row (zeroed below)
+        const int64_t g = a.idx ? gld<int64_t>(a.idx + rr) : (int64_t)rr;
+        xv[u] = gld<V>(xg + g * I + c * EPL);
+        x0[u] = gld<V>(xg + g * I);
+      }
+    }
+    setup_lds();  // overlaps the loads
+    if (net.Ip > I) {
+      for (int e = tid; e < R * (net.Ip - I); e += RC_THREADS) {
+        const int r = e / (net.Ip - I), c = I + e % (net.Ip - I);
+        Xin[r * P.sx + c] = to_t<T>(0.f);
+      }
+    }
+    T* const xe0 = (T*)net.L[lE(net, 0)].xT;
+    T* const xc0 = (T*)net.L[lC0(net)].xT;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int v = u * RC_THREADS + tid;
+      if (u * RC_THREADS < NV && v < NV) {  // NV % 4 == 0: quads are whole
+        const int w = v >> 2, rq = fdiv(w, inv_VPR), c = w - rq * VPR, row = 4 * rq + (v & 3);
+        const bool live = row < nrows;
+        const float s0 = live ? to_f(x0[u][1]) : 0.f, s1 = live ? to_f(x0[u][2]) : 0.f;
+        const int f0 = c * EPL;
+        int d = f0 - fdiv(f0, inv_Dd) * D;
         V o;
+        float q[EPL];
 #pragma unroll
         for (int e = 0; e < EPL; ++e) {
-          const float val = (float)bufv[u][e] - (d == 1 ? s0 : 0.f) - (d == 2 ? s1 : 0.f);
+          const float val = to_f(xv[u][e]) - (d == 1 ? s0 : 0.f) - (d == 2 ? s1 : 0.f);
           o[e] = to_t<T>(live ? val : 0.f);
+          q[e] = to_f(o[e]);
           d = d + 1 == D ? 0 : d + 1;
         }
-        *(V*)(Xin + r * P.sx + c * EPL) = o;
-      }
-    }
-  };
-  {
-    auto zero = [&](void* p, int bytes) {
-      f32x4* q = (f32x4*)p;
-      for (int e = tid; e < bytes / 16; e += RC_THREADS) q[e] = f32x4{0.f, 0.f, 0.f, 0.f};
-    };
-    if (fast) {  // loads first: everything below overlaps their latency
-      const int last = max(a.batch - 1, 0);
+        *(V*)(Xin + row * P.sx + f0) = o;
+        if (TRAIN) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int v = min(u * RC_THREADS + tid, NV - 1);
-        const int r = v / VPR, c = v - r * VPR;
-        const int rr = min(b0 + r, last);  // rows past the batch re-read a valid row (zeroed later)
-        const int64_t g = a.idx ? gld<int64_t>(a.idx + rr) : (int64_t)rr;
-        bufv[u] = gld<V>(xg + g * I + c * EPL);
+          for (int e = 0; e < EPL; e += 4)
+            put4Tq(xe0 + (size_t)(f0 + e) * Bp + b0, Bp, row, f32x4{q[e], q[e + 1], q[e + 2], q[e + 3]});
+        }
+        if (c == 0) {  // quad-uniform: the condition input of this row (and its arena copy)
+#pragma unroll
+          for (int k = 0; k < 32; k += EPL) {
+            V cv;
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) cv[e] = to_t<T>(k + e == 0 ? s0 : k + e == 1 ? s1 : 0.f);
+            *(V*)(Cin + row * P.scin + k) = cv;
+          }
+          if (TRAIN) put4Tq(xc0 + b0, Bp, row, f32x4{to_f(to_t<T>(s0)), to_f(to_t<T>(s1)), 0.f, 0.f});
+        }
       }
     }
-    for (int e = tid; e < a.nsteps * 4; e += RC_THREADS)
-      ((u32x4*)(smem + P.oSteps))[e] = gld<u32x4>((const u32x4*)a.steps + e);
-    zero(Hc, R * P.shc * (int)sizeof(T));
-    zero(Dec, R * P.sdec * (int)sizeof(T));
+  } else {
+    setup_lds();
     zero(Cin, R * P.scin * (int)sizeof(T));
-    zero(Mask, rup(n_masks(net) * R * mw, 16));
-    for (int e = tid; e < net.nbias / 4 + 1; e += RC_THREADS)
-      ((f32x4*)BiasL)[e] = e < net.nbias / 4 ? gld<f32x4>(net.bias_all + 4 * e) : f32x4{0.f, 0.f, 0.f, 0.f};
-    if (fast) {
-      // x[:,0,1:3] (Training_VAE.py:345) = elements 1, 2 of each row's first vector
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int v = u * RC_THREADS + tid;
-        if (v < NV) {
-          const int r = v / VPR, c = v - r * VPR;
-          if (c == 0) {
-            Start[r * 2 + 0] = r < nrows ? to_f(bufv[u][1]) : 0.f;
-            Start[r * 2 + 1] = r < nrows ? to_f(bufv[u][2]) : 0.f;
+    for (int r = tid; r < R; r += RC_THREADS) {
+      float s0 = 0.f, s1 = 0.f;
+      int64_t g = 0;
+      if (r < nrows) {
+        g = a.idx ? gld<int64_t>(a.idx + b0 + r) : (int64_t)(b0 + r);
+        if (MODE == RC_DECODE || a.x_relative) {
+          if (a.start_in) {  // decode(z, h_c) carries no start point
+            s0 = gld<float>(a.start_in + (size_t)(b0 + r) * 2 + 0);
+            s1 = gld<float>(a.start_in + (size_t)(b0 + r) * 2 + 1);
           }
+        } else {
+          s0 = to_f(gld<T>(xg + g * I + 1));  // x[:,0,1:3]  (Training_VAE.py:345)
+          s1 = to_f(gld<T>(xg + g * I + 2));
         }
       }
-    } else {
-      for (int r = tid; r < R; r += RC_THREADS) {
-        float s0 = 0.f, s1 = 0.f;
-        int64_t g = 0;
-        if (r < nrows) {
-          g = a.idx ? gld<int64_t>(a.idx + b0 + r) : (int64_t)(b0 + r);
-          if (MODE == RC_DECODE || a.x_relative) {
-            if (a.start_in) {  // decode(z, h_c) carries no start point
-              s0 = gld<float>(a.start_in + (size_t)(b0 + r) * 2 + 0);
-              s1 = gld<float>(a.start_in + (size_t)(b0 + r) * 2 + 1);
-            }
-          } else {
-            s0 = to_f(gld<T>(xg + g * I + 1));  // x[:,0,1:3]  (Training_VAE.py:345)
-            s1 = to_f(gld<T>(xg + g * I + 2));
-          }
-        }
-        Start[r * 2 + 0] = s0;
-        Start[r * 2 + 1] = s1;
-        RowG[r] = g;
-      }
+      Start[r * 2 + 0] = s0;
+      Start[r * 2 + 1] = s1;
+      RowG[r] = g;
     }
-  }
-  lds_barrier();
-  for (int r = tid; r < nrows; r += RC_THREADS) {
-    Cin[r * P.scin + 0] = to_t<T>(Start[r * 2 + 0]);
-    Cin[r * P.scin + 1] = to_t<T>(Start[r * 2 + 1]);
-  }
-  if (MODE != RC_DECODE) {
-    if (vec) {
-      if (fast) {
-        transform(0);
-      } else {
-        // 16-B loads, U per thread issued before any is consumed; clamped indices so no load is
-        // conditional
-        for (int base = 0; base < NV; base += U * RC_THREADS) {
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const int v = min(base + u * RC_THREADS + tid, NV - 1);
-            const int r = v / VPR, c = v - r * VPR;
-            bufv[u] = gld<V>(xg + RowG[r] * I + c * EPL);  // RowG = row 0 past nrows
-          }
-          transform(base);
-        }
-      }
-      if (net.Ip > I) {
-        for (int e = tid; e < R * (net.Ip - I); e += RC_THREADS) {
-          const int r = e / (net.Ip - I), c = I + e % (net.Ip - I);
-          Xin[r * P.sx + c] = to_t<T>(0.f);
-        }
-      }
-    } else {
+    lds_barrier();
+    for (int r = tid; r < nrows; r += RC_THREADS) {
+      Cin[r * P.scin + 0] = to_t<T>(Start[r * 2 + 0]);
+      Cin[r * P.scin + 1] = to_t<T>(Start[r * 2 + 1]);
+    }
+    if (MODE != RC_DECODE) {
       for (int e = tid; e < R * net.Ip; e += RC_THREADS) {
         const int r = e / net.Ip, c = e - r * net.Ip;
         float v = 0.f;
@@ -645,27 +638,27 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
         }
         Xin[r * P.sx + c] = to_t<T>(v);
       }
-    }
-  } else {
-    if (skip_cond) {
-      for (int e = tid; e < R * H; e += RC_THREADS) {
-        const int r = e / H, c = e - r * H;
-        Dec[r * P.sdec + Z + c] = to_t<T>(r < nrows ? gld<float>(a.hc_in + (size_t)(b0 + r) * H + c) : 0.f);
+    } else {
+      if (skip_cond) {
+        for (int e = tid; e < R * H; e += RC_THREADS) {
+          const int r = e / H, c = e - r * H;
+          Dec[r * P.sdec + Z + c] = to_t<T>(r < nrows ? gld<float>(a.hc_in + (size_t)(b0 + r) * H + c) : 0.f);
+        }
       }
-    }
-    if (a.z_in) {
-      for (int e = tid; e < R * Z; e += RC_THREADS) {
-        const int r = e / Z, j = e - r * Z;
-        Dec[r * P.sdec + j] = to_t<T>(r < nrows ? gld<float>(a.z_in + (size_t)(b0 + r) * Z + j) : 0.f);
+      if (a.z_in) {
+        for (int e = tid; e < R * Z; e += RC_THREADS) {
+          const int r = e / Z, j = e - r * Z;
+          Dec[r * P.sdec + j] = to_t<T>(r < nrows ? gld<float>(a.z_in + (size_t)(b0 + r) * Z + j) : 0.f);
+        }
       }
     }
   }
   lds_barrier();
   stamp();
 
-  // feature-major copy of the input tiles for the weight-gradient kernel: one 4-row × 1-column
-  // quad per task → one 8-B (bf16) / 16-B (fp32) store
-  if (TRAIN && !CVAE_DIAG_NOSTORE) {
+  // slow path only: feature-major copy of the input tiles for the weight-gradient kernel (one
+  // 4-row × 1-column quad per task → one 8-B / 16-B store; the arena pads stay zero from creation)
+  if (TRAIN && !fast && !CVAE_DIAG_NOSTORE) {
     auto copy_T = [&](const T* src, int ld, int ncols, T* dst) {
       constexpr int RQ = R / 4;
       for (int t = tid; t < ncols * RQ; t += RC_THREADS) {
@@ -676,8 +669,8 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
         gstore4(dst + (size_t)c * Bp + b0 + 4 * q, v);
       }
     };
-    copy_T(Cin, P.scin, net.Cp, (T*)net.L[lC0(net)].xT);
-    copy_T(Xin, P.sx, net.Ip, (T*)net.L[lE(net, 0)].xT);
+    copy_T(Cin, P.scin, 2, (T*)net.L[lC0(net)].xT);
+    copy_T(Xin, P.sx, I, (T*)net.L[lE(net, 0)].xT);
   }
 
   const float Bf = (float)a.batch;

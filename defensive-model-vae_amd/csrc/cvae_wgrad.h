@@ -5,7 +5,8 @@
 // K = batch), both operands batch-contiguous in the activation arena, MFMA
 // 16x16x32 bf16 (or 4×16x16x4 f32) with the K range split over the 4 waves
 // and combined through LDS in a fixed order (deterministic).  Tiles with
-// i0 == 0 also reduce the bias gradient db = Σ_b G.
+// i0 == 0 also reduce the bias gradient db = Σ_b G from the G fragments the
+// MFMA loop already holds (no second pass over the rows).
 //
 // The epilogue either writes the fp32 gradient into the flat state_dict-ordered
 // buffer (data-parallel path: all-reduce comes next) or applies torch's Adam
@@ -14,6 +15,11 @@
 // Wf/Wb/bias that the row-chain kernel reads — the gradient never round-trips
 // through HBM.  param_kernel does the same update from a gradient buffer
 // (after the all-reduce) or just repacks the copies (PACK).
+//
+// Epilogue shape: a thread owns 4 consecutive inputs (o, i..i+3) of one output row and issues
+// all its p/m/v loads before any store; the new weights go through an LDS image of the tile so
+// that each operand copy is written as whole 16-B MFMA fragments (1 KB per wave instruction)
+// instead of 2-B element stores scattered over the fragment layout.
 #pragma once
 #include "cvae_device.h"
 
@@ -64,8 +70,8 @@ struct LossArgs {
   float* loss_accum;      // [5] nullable, += loss * batch
 };
 
-__device__ __forceinline__ float adam_update(float p, float g, int64_t idx, const AdamArgs& a) {
-  float m = a.m[idx], v = a.v[idx];
+// One element of torch's Adam, in its op order; m and v are updated in place.
+__device__ __forceinline__ float adam_math(float p, float g, float& m, float& v, const AdamArgs& a) {
   // exp_avg.lerp_(grad, 1 - beta1): weight < 0.5 branch of at::lerp
   m = a.beta1_w < 0.5f ? m + a.beta1_w * (g - m) : g - (g - m) * (1.f - a.beta1_w);
   // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, value=1 - beta2)
@@ -73,33 +79,53 @@ __device__ __forceinline__ float adam_update(float p, float g, int64_t idx, cons
   v = v + a.one_m_beta2 * g * g;
   // denom = exp_avg_sq.sqrt() / bias_correction2_sqrt + eps;  param.addcdiv_(exp_avg, denom, -step_size)
   const float denom = sqrtf(v) / a.bc2_sqrt + a.eps;
-  p = p + a.lr_neg_step * m / denom;
-  a.m[idx] = m;
-  a.v[idx] = v;
-  return p;
+  return p + a.lr_neg_step * m / denom;
 }
 
-// weight element (o, i) of layer L in padded coordinates; g valid for PM_GRAD / fused PM_ADAM
-template <typename T, int MODE>
-__device__ __forceinline__ void apply_weight(const LayerDev& L, int o, int i, float g, const AdamArgs& a) {
-  if (o >= L.Np || i >= L.Kp) return;
-  float w = 0.f;
-  if (o < L.N && i < L.K) {
-    const int seg = (L.nseg == 2 && o >= L.seg_rows0) ? 1 : 0;
-    const int orow = seg ? o - L.seg_rows0 : o;
-    const int64_t idx = L.pw[seg] + (int64_t)orow * L.K + i;
-    if (MODE == PM_GRAD) { a.grads[idx] = g; return; }
-    w = a.params[idx];
-    if (MODE == PM_ADAM) {
-      w = adam_update(w, g, idx, a);
-      a.params[idx] = w;
-    }
-  } else if (MODE == PM_GRAD) {
-    return;
+// LDS image of one 32×32 tile: fp32 rows padded to 36 floats (16-B aligned rows)
+constexpr int WT_LD = 36;
+
+// Weights (o, i..i+3) of layer L (padded coordinates) with gradient g4: write the gradient
+// (GRAD), apply Adam (ADAM) or read (PACK) the fp32 master.  Returns the values for the operand
+// copies (0 in the padding).  All loads are issued before the first store.
+template <int MODE>
+__device__ __forceinline__ f32x4 update4(const LayerDev& L, int o, int i, f32x4 g4, const AdamArgs& a) {
+  f32x4 w = {0.f, 0.f, 0.f, 0.f};
+  if (o >= L.N || i >= L.K) return w;
+  const int seg = (L.nseg == 2 && o >= L.seg_rows0) ? 1 : 0;
+  const int orow = seg ? o - L.seg_rows0 : o;
+  const int64_t base = L.pw[seg] + (int64_t)orow * L.K + i;
+  const int nv = min(4, L.K - i);
+  if (MODE == PM_GRAD) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (c < nv) a.grads[base + c] = g4[c];
+    return w;
   }
-  if (CVAE_DIAG_NOWPACK && MODE == PM_ADAM) return;
-  ((T*)L.Wf)[frag_off<T>(o, i, L.Kp)] = to_t<T>(w);  // forward operand: rows o, K = inputs
-  ((T*)L.Wb)[frag_off<T>(i, o, L.Np)] = to_t<T>(w);  // dX operand (Wᵀ): rows i, K = outputs
+  float p[4], m[4], v[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    p[c] = c < nv ? a.params[base + c] : 0.f;
+    if (MODE == PM_ADAM) {
+      m[c] = c < nv ? a.m[base + c] : 0.f;
+      v[c] = c < nv ? a.v[base + c] : 0.f;
+    }
+  }
+  if (MODE == PM_ADAM) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) p[c] = adam_math(p[c], g4[c], m[c], v[c], a);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (c < nv) {
+        a.params[base + c] = p[c];
+        a.m[base + c] = m[c];
+        a.v[base + c] = v[c];
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) w[c] = c < nv ? p[c] : 0.f;
+  return w;
 }
 
 template <int MODE>
@@ -112,14 +138,65 @@ __device__ __forceinline__ void apply_bias(const LayerDev& L, int o, float g, co
     if (MODE == PM_GRAD) { a.grads[idx] = g; return; }
     w = a.params[idx];
     if (MODE == PM_ADAM) {
-      w = adam_update(w, g, idx, a);
+      float m = a.m[idx], v = a.v[idx];
+      w = adam_math(w, g, m, v, a);
       a.params[idx] = w;
+      a.m[idx] = m;
+      a.v[idx] = v;
     }
   } else if (MODE == PM_GRAD) {
     return;
   }
   if (CVAE_DIAG_NOWPACK && MODE == PM_ADAM) return;
   L.bias[o] = w;
+}
+
+// Both operand copies of one 32×32 tile from its LDS image, as whole MFMA fragments.  Fragment
+// (n-tile t, chunk kc) lane ln holds elements (16t + (ln & 15), KC·kc + EPL·(ln >> 4) + e), so a
+// tile is 2 n-tiles × 32/KC chunks of contiguous 1-KB blocks per copy (frag_off).
+template <typename T>
+__device__ __forceinline__ void store_operands(const LayerDev& L, int o0, int i0, const float* wt) {
+  using V = typename Op<T>::V;
+  constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC, CPT = 32 / KC;
+  constexpr int PER_COPY = 2 * CPT * 64;
+#pragma unroll
+  for (int j0 = 0; j0 < 2 * PER_COPY; j0 += CVAE_THREADS) {
+    const int j = j0 + (int)threadIdx.x;
+    const bool wb = j >= PER_COPY;  // wave-uniform: PER_COPY is a multiple of 64
+    const int jj = wb ? j - PER_COPY : j;
+    const int blk = jj >> 6, ln = jj & 63;
+    const int bt = blk / CPT, bk = blk - bt * CPT;
+    const int nl = bt * 16 + (ln & 15), kl = bk * KC + (ln >> 4) * EPL;
+    V val;
+    if (wb) {  // Wb = Wᵀ: rows = inputs i, K = outputs o
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) val[e] = to_t<T>(wt[(kl + e) * WT_LD + nl]);
+      gst<V>((T*)L.Wb + frag_off<T>(i0 + nl, o0 + kl, L.Np), val);
+    } else {
+#pragma unroll
+      for (int e = 0; e < EPL; e += 4) {
+        const f32x4 q = *(const f32x4*)(wt + nl * WT_LD + kl + e);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) val[e + c] = to_t<T>(q[c]);
+      }
+      gst<V>((T*)L.Wf + frag_off<T>(o0 + nl, i0 + kl, L.Kp), val);
+    }
+  }
+}
+
+// Shared by wgrad_kernel and param_kernel: thread (o = tid/8, i = 4·(tid%8)) of the tile owns the
+// gradient g4 of weights (o0+o, i0+i..+3); threads < 32 own bias o0+tid (tiles with i0 == 0).
+// wt: an LDS tile image (32 × WT_LD floats) the caller no longer needs.
+template <typename T, int MODE>
+__device__ __forceinline__ void tile_epilogue(const LayerDev& L, int o0, int i0, f32x4 g4, float db,
+                                              const AdamArgs& aa, float* wt) {
+  const int tid = threadIdx.x, o = tid >> 3, i4 = (tid & 7) * 4;
+  const f32x4 w = update4<MODE>(L, o0 + o, i0 + i4, g4, aa);
+  if (i0 == 0 && tid < 32) apply_bias<MODE>(L, o0 + tid, db, aa);
+  if (MODE == PM_GRAD || (CVAE_DIAG_NOWPACK && MODE == PM_ADAM)) return;
+  *(f32x4*)(wt + o * WT_LD + i4) = w;
+  __syncthreads();
+  store_operands<T>(L, o0, i0, wt);
 }
 
 // called by one whole wave: lane-strided partial sums, then a fixed-order butterfly (deterministic)
@@ -148,7 +225,8 @@ __global__ __launch_bounds__(CVAE_THREADS) void wgrad_kernel(NetDev net, const T
                                                              int Bk, AdamArgs aa, LossArgs la) {
   using V = typename Op<T>::V;
   constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC;
-  __shared__ __attribute__((aligned(16))) float red[CVAE_NW * 32 * 33];
+  __shared__ __attribute__((aligned(16))) float red[CVAE_NW * 32 * WT_LD];
+  __shared__ float dbp[CVAE_NW * 32];
   const TileDesc td = tiles[blockIdx.x];
   const LayerDev& L = net.L[td.layer];
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
@@ -156,6 +234,7 @@ __global__ __launch_bounds__(CVAE_THREADS) void wgrad_kernel(NetDev net, const T
   const int Bp = net.Bp;
   const T* G = (const T*)L.gT;
   const T* X = (const T*)L.xT;
+  const bool bias_tile = td.i0 == 0;
 
   WSTAMP(0);
   if (blockIdx.x == 0 && tid < 64 && la.partials) finish_loss(la, net.S, net.D, net.Z);
@@ -165,6 +244,7 @@ __global__ __launch_bounds__(CVAE_THREADS) void wgrad_kernel(NetDev net, const T
   for (int m = 0; m < 2; ++m)
 #pragma unroll
     for (int n = 0; n < 2; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float gs[2] = {0.f, 0.f};  // bias partials: Σ of this lane's G fragment elements
   const T* gp[2];
   const T* xp[2];
 #pragma unroll
@@ -179,9 +259,9 @@ __global__ __launch_bounds__(CVAE_THREADS) void wgrad_kernel(NetDev net, const T
   auto load = [&](int u, int j) {  // unconditional, clamped to this wave's last chunk
     const int c = (wave + CVAE_NW * min(j, nmine > 0 ? nmine - 1 : 0)) * KC;
 #pragma unroll
-    for (int m = 0; m < 2; ++m) ga[u][m] = *(const V*)(gp[m] + c);
+    for (int m = 0; m < 2; ++m) ga[u][m] = gld<V>(gp[m] + c);
 #pragma unroll
-    for (int n = 0; n < 2; ++n) xb[u][n] = *(const V*)(xp[n] + c);
+    for (int n = 0; n < 2; ++n) xb[u][n] = gld<V>(xp[n] + c);
   };
 #pragma unroll
   for (int u = 0; u < PF; ++u) load(u, u);
@@ -194,46 +274,45 @@ __global__ __launch_bounds__(CVAE_THREADS) void wgrad_kernel(NetDev net, const T
         for (int m = 0; m < 2; ++m)
 #pragma unroll
           for (int n = 0; n < 2; ++n) acc[m][n] = mfma_chunk(ga[u][m], xb[u][n], acc[m][n]);
+        if (bias_tile) {
+#pragma unroll
+          for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) gs[m] += (float)ga[u][m][e];
+        }
       }
       load(u, j + PF);
     }
   }
   WSTAMP(1);
-  float* rw = red + wave * 32 * 33;
+  float* rw = red + wave * 32 * WT_LD;
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
     for (int n = 0; n < 2; ++n)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) rw[(m * 16 + (lane >> 4) * 4 + i) * 33 + n * 16 + r16] = acc[m][n][i];
-
-  // bias gradient: 8 threads per output row, 16-B loads along the batch
-  float db = 0.f;
-  if (td.i0 == 0) {
-    const int o = tid >> 3, part = tid & 7;
-    const T* gr = G + (size_t)(td.o0 + o) * Bp;
-#pragma unroll 4
-    for (int c = part * EPL; c < Bk; c += 8 * EPL) {
-      const V v = *(const V*)(gr + c);
+      for (int i = 0; i < 4; ++i) rw[(m * 16 + (lane >> 4) * 4 + i) * WT_LD + n * 16 + r16] = acc[m][n][i];
+  if (bias_tile) {
 #pragma unroll
-      for (int e = 0; e < EPL; ++e) db += (float)v[e];
+    for (int m = 0; m < 2; ++m) {
+      gs[m] += __shfl_xor(gs[m], 16, 64);
+      gs[m] += __shfl_xor(gs[m], 32, 64);
+      if (lane < 16) dbp[wave * 32 + m * 16 + lane] = gs[m];
     }
-    db += __shfl_xor(db, 1, 64);
-    db += __shfl_xor(db, 2, 64);
-    db += __shfl_xor(db, 4, 64);
   }
   __syncthreads();
   WSTAMP(2);
+  const int o = tid >> 3, i4 = (tid & 7) * 4;
+  f32x4 g4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int e = q * CVAE_THREADS + tid;
-    const int o = e >> 5, i = e & 31;
-    float g = 0.f;
+  for (int w = 0; w < CVAE_NW; ++w) g4 += *(const f32x4*)(red + w * 32 * WT_LD + o * WT_LD + i4);
+  float db = 0.f;
+  if (bias_tile && tid < 32) {
 #pragma unroll
-    for (int w = 0; w < CVAE_NW; ++w) g += red[w * 32 * 33 + o * 33 + i];
-    apply_weight<T, MODE>(L, td.o0 + o, td.i0 + i, g, aa);
+    for (int w = 0; w < CVAE_NW; ++w) db += dbp[w * 32 + tid];
   }
-  if (td.i0 == 0 && (tid & 7) == 0) apply_bias<MODE>(L, td.o0 + (tid >> 3), db, aa);
+  __syncthreads();  // red becomes the image of the new weights
+  tile_epilogue<T, MODE>(L, td.o0, td.i0, g4, db, aa, red);
 #if CVAE_DIAG_STAMPS
   __syncthreads();
   WSTAMP(3);
@@ -244,27 +323,26 @@ __global__ __launch_bounds__(CVAE_THREADS) void wgrad_kernel(NetDev net, const T
 template <typename T, int MODE>
 __global__ __launch_bounds__(CVAE_THREADS) void param_kernel(NetDev net, const TileDesc* __restrict__ tiles,
                                                              AdamArgs aa) {
+  __shared__ __attribute__((aligned(16))) float wt[32 * WT_LD];
   const TileDesc td = tiles[blockIdx.x];
   const LayerDev& L = net.L[td.layer];
   const int tid = threadIdx.x;
+  const int o = td.o0 + (tid >> 3), i = td.i0 + (tid & 7) * 4;
+  f32x4 g4 = {0.f, 0.f, 0.f, 0.f};
+  float db = 0.f;
+  if (MODE == PM_ADAM) {
+    if (o < L.N && i < L.K) {
+      const int seg = (L.nseg == 2 && o >= L.seg_rows0) ? 1 : 0;
+      const int64_t base = L.pw[seg] + (int64_t)(seg ? o - L.seg_rows0 : o) * L.K + i;
+      const int nv = min(4, L.K - i);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int e = q * CVAE_THREADS + tid;
-    const int o = td.o0 + (e >> 5), i = td.i0 + (e & 31);
-    float g = 0.f;
-    if (MODE == PM_ADAM && o < L.N && i < L.K) {
-      const int seg = (L.nseg == 2 && o >= L.seg_rows0) ? 1 : 0;
-      g = aa.grads[L.pw[seg] + (int64_t)(seg ? o - L.seg_rows0 : o) * L.K + i] * aa.grad_scale;
+      for (int c = 0; c < 4; ++c) g4[c] = c < nv ? aa.grads[base + c] * aa.grad_scale : 0.f;
     }
-    apply_weight<T, MODE>(L, o, i, g, aa);
-  }
-  if (td.i0 == 0 && tid < 32) {
-    const int o = td.o0 + tid;
-    float g = 0.f;
-    if (MODE == PM_ADAM && o < L.N) {
-      const int seg = (L.nseg == 2 && o >= L.seg_rows0) ? 1 : 0;
-      g = aa.grads[L.pb[seg] + (seg ? o - L.seg_rows0 : o)] * aa.grad_scale;
+    const int ob = td.o0 + tid;
+    if (td.i0 == 0 && tid < 32 && ob < L.N) {
+      const int seg = (L.nseg == 2 && ob >= L.seg_rows0) ? 1 : 0;
+      db = aa.grads[L.pb[seg] + (seg ? ob - L.seg_rows0 : ob)] * aa.grad_scale;
     }
-    apply_bias<MODE>(L, o, g, aa);
   }
+  tile_epilogue<T, MODE>(L, td.o0, td.i0, g4, db, aa, wt);
 }
