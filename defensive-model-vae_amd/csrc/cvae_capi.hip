@@ -6,6 +6,8 @@
 #include <cstdio>
 #include <algorithm>
 #include <cstring>
+#include <cstdlib>
+#include <type_traits>
 #include <string>
 #include <vector>
 
@@ -14,6 +16,7 @@
 #include "cvae_rowchain.h"
 #include "cvae_wgrad.h"
 #include "cvae_loss.h"
+#include "cvae_fastchain.h"
 
 namespace {
 
@@ -58,6 +61,8 @@ struct cvae_handle {
   int n_steps[ST_N] = {};
   unsigned long long* d_stamps = nullptr;  // diagnostic builds only
   int lds_bytes = 0;
+  int fast_nki = 0;         // > 0: bf16 training runs fchain::fastchain_kernel<fast_nki>
+  int fast_lds = 0;
   bool timing = false;
   // timing: per call, a chain of events on the caller's stream; segment i of a
   // call spans ev[i] → ev[i+1] and is named by the kernel launched after ev[i]
@@ -409,6 +414,31 @@ AdamArgs make_adam(float* params, float* grads, float* m, float* v, int step, fl
   return a;
 }
 
+// The specialised bf16 training chain (cvae_fastchain.h) covers the reference architecture:
+// hidden 128, latent 8, 4+4 layers, S·D a multiple of 8 padding to one of the instantiated chunk
+// counts.  CVAE_GENERIC=1 in the environment forces the interpreter (A/B comparisons).
+constexpr int kFastNki[] = {19};
+int plan_fast(cvae_handle* h) {
+  const cvae_config& c = h->cfg;
+  const NetDev& n = h->net;
+  h->fast_nki = 0;
+  const char* env = std::getenv("CVAE_GENERIC");
+  if ((env && env[0] == '1') || c.dtype != CVAE_BF16 || c.hidden_dim != fchain::H || c.latent_dim != fchain::Z ||
+      c.n_enc != 4 || c.n_dec != 4 || n.I % 8 != 0)
+    return CVAE_OK;
+  for (int nki : kFastNki) {
+    if (n.Ip != 32 * nki) continue;
+    const fchain::Lds lp = fchain::lds_layout(n.Ip, n.S, n.nbias);
+    if (lp.total > 160 * 1024) return CVAE_OK;
+    h->fast_nki = nki;
+    h->fast_lds = lp.total;
+    if (nki == 19)
+      HIPCK(hipFuncSetAttribute((const void*)fchain::fastchain_kernel<19>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lp.total));
+  }
+  return CVAE_OK;
+}
+
 template <typename T>
 int train_fwd_bwd_impl(cvae_handle* h, const void* x, const int64_t* idx, int batch, const float* eps,
                        uint64_t seed, uint64_t offset, const cvae_loss_weights* w, hipStream_t s,
@@ -420,6 +450,16 @@ int train_fwd_bwd_impl(cvae_handle* h, const void* x, const int64_t* idx, int ba
   ra.partials = h->d_partials;
   int rc = tmark(h, s, "rowchain");
   if (rc) return rc;
+  if (std::is_same<T, __bf16>::value && h->fast_nki > 0 && (((uintptr_t)x) & 15) == 0) {
+    ra.steps = h->d_steps[cvae_handle::ST_TRAIN];
+    ra.nsteps = h->n_steps[cvae_handle::ST_TRAIN];
+    ra.stamps = h->d_stamps;
+    const int grid = rup_i(batch, 32) / fchain::R;
+    if (h->fast_nki == 19)
+      hipLaunchKernelGGL(fchain::fastchain_kernel<19>, dim3(grid), dim3(fchain::NT), h->fast_lds, s, h->net, ra);
+    HIPCK(hipGetLastError());
+    return CVAE_OK;
+  }
   return launch_rowchain<T, RC_TRAIN>(h, ra, s);
 }
 
@@ -456,6 +496,7 @@ int cvae_create(const cvae_config* cfg, int device, cvae_handle** out) {
   if (e != hipSuccess) { delete h; return fail(CVAE_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e)); }
   rc = alloc_arena(h);
   if (!rc) rc = h->cfg.dtype == CVAE_BF16 ? set_lds_attrs<__bf16>(h) : set_lds_attrs<float>(h);
+  if (!rc) rc = plan_fast(h);
   if (rc) { cvae_destroy(h); return rc; }
   *out = h;
   return CVAE_OK;

@@ -91,11 +91,22 @@ __device__ __forceinline__ f32x4 mfma_chunk(bf16x8 a, bf16x8 b, f32x4 c) {
 // K chunk kc, the 64 lanes' 16-B fragments are contiguous — 1 KB per (t, kc) — so one wave load
 // instruction reads 8 full 128-B lines.  (Row-major [Np][Kp] makes each instruction 16 rows x
 // 64 B: texture-address bound at ~38 GB/s per CU, measured 3.7x slower — scripts/ubench/wload.hip.)
+// Lane (r, q) of a fragment holds row 16t + r and the chunk-relative K positions frag_k(q, e):
+//   bf16: 4q + e for e < 4, 16 + 4q + (e - 4) for e >= 4 — the K order two transposed LDS block
+//         reads of a feature-major activation image deliver (ds_read_b64_tr_b16, cvae_fastchain.h);
+//         the MFMA sums over all 32 positions, so any order works as long as A and B agree;
+//   fp32: 4q + e.
+template <typename T>
+__host__ __device__ inline int frag_k(int q, int e) {
+  return Op<T>::EPL == 8 ? (e < 4 ? 4 * q + e : 12 + 4 * q + e) : 4 * q + e;
+}
 // Element (n, k) of an operand matrix with padded K extent Kp:
 template <typename T>
 __host__ __device__ inline size_t frag_off(int n, int k, int Kp) {
   constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC;
-  const int t = n >> 4, r = n & 15, kc = k / KC, kk = k - kc * KC, q = kk / EPL, e = kk - q * EPL;
+  const int t = n >> 4, r = n & 15, kc = k / KC, kk = k - kc * KC;
+  const int q = EPL == 8 ? (kk & 15) >> 2 : kk >> 2;
+  const int e = EPL == 8 ? (kk & 3) + ((kk >> 4) << 2) : kk & 3;
   return ((size_t)(t * (Kp / KC) + kc) * 64 + q * 16 + r) * EPL + e;
 }
 
@@ -148,6 +159,26 @@ __device__ __forceinline__ float philox_normal(uint64_t seed, uint64_t offset, u
   float s, c;
   sincosf(6.283185307179586f * f1, &s, &c);
   return (j & 1) ? rad * s : rad * c;
+}
+
+// the 4 normals j = j0 .. j0+3 (j0 % 4 == 0) of philox_normal from ONE Philox block — the same
+// counter, words and Box-Muller pairs, so bit-identical to four philox_normal calls
+__device__ __forceinline__ f32x4 philox_normal4(uint64_t seed, uint64_t offset, uint32_t b, uint32_t j0) {
+  const uint4 r = philox4x32_10(make_uint4(b, j0 >> 2, (uint32_t)offset, (uint32_t)(offset >> 32)),
+                                make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+  f32x4 out;
+  const uint32_t us[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const float f0 = ((float)us[2 * h] + 1.0f) * 2.3283064365386963e-10f;  // (0,1]
+    const float f1 = (float)us[2 * h + 1] * 2.3283064365386963e-10f;
+    const float rad = sqrtf(-2.0f * logf(f0));
+    float s, c;
+    sincosf(6.283185307179586f * f1, &s, &c);
+    out[2 * h] = rad * c;
+    out[2 * h + 1] = rad * s;
+  }
+  return out;
 }
 
 // Wave index as a SCALAR: threadIdx-derived values are divergent to the compiler, so a plain

@@ -1,0 +1,581 @@
+// cvae_fastchain.h — the bf16 training row chain, specialised for the reference architecture
+// (Training_VAE.py:118-167 at hidden_dim=128, latent_dim=8, 4 encoder + 4 decoder Linears).
+//
+// Same work and same arena outputs as rowchain_kernel<bf16, 16, RC_TRAIN> (relative transform,
+// forward, reparameterisation, conditional_vae_loss and dL/drecon, every dX; the feature-major
+// xT/gT arena rows the dW kernel reduces), for one 16-row batch tile per workgroup, written as
+// straight-line code instead of a step interpreter:
+//  * UN-SWAPPED MFMA, acc = X·Wᵀ: the activations live in LDS as FEATURE-MAJOR images (feature f
+//    = 16 batch rows, 32 B) and the X operand is read with ds_read_b64_tr_b16 (hardware
+//    transpose), so each lane's accumulator is 4 consecutive batch rows of ONE feature — the
+//    feature-major arena copy and the next layer's image are one 8-B store each, with no
+//    cross-lane transposition and one bias value per lane;
+//  * every step's shapes, LDS buffers and epilogue are compile-time; one s_barrier per step
+//    (two independent GEMMs share a step where the reference graph allows it);
+//  * weights are prefetched into registers two steps ahead, and because the code is straight-line
+//    the compiler counts vmcnt exactly: a weight wait never waits for the epilogue's stores.
+// Selected by the host (cvae_capi.hip) for bf16 training at H=128, Z=8, 4+4 layers and
+// ceil(S·D/32) == NKI; every other configuration runs the generic interpreter.
+//
+// Layer / mask indices: C0 C1 E0 E1 E2 E3 FC D0 D1 D2 D3 = 0..10; ReLU masks C0 C1 E0..E3 D0..D2
+// = 0..8.  LDS images: feature-major bf16, row quad q of feature f at slot q ^ ((f >> 2) & 3)
+// (conflict-free 8-B writes and transposed reads).
+#pragma once
+#include "cvae_device.h"
+#include "cvae_rowchain.h"
+
+namespace fchain {
+
+constexpr int R = 16, NW = 8, NT = 64 * NW, H = 128, Z = 8;
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+#define FC_LDS __attribute__((address_space(3)))
+
+enum { LC0 = 0, LC1, LE0, LE1, LE2, LE3, LFC, LD0, LD1, LD2, LD3 };
+enum { MC0 = 0, MC1, ME0, ME1, ME2, ME3, MD0, MD1, MD2 };
+
+struct Lds {  // byte offsets
+  int xin, cin, cb, a0, a1, hcat, dcat, gfc, mask, mulv, eps, stdv, rch0, gd0, dhc2, bias, part, total;
+};
+__host__ __device__ inline Lds lds_layout(int Ip, int S, int nbias) {
+  Lds p;
+  int o = 0;
+  auto take = [&](int b) { const int r = o; o += (b + 15) / 16 * 16; return r; };
+  p.xin = take(Ip * 32);        // x_rel image, then dL/drecon (GL) in place
+  p.cin = take(32 * 32);        // condition input [start x, start y, 0...]
+  p.cb = take(H * 32);          // condition layer-0 output; later dh_c (C1 pre-activation gradient)
+  p.a0 = take(H * 32);          // ping-pong hidden images
+  p.a1 = take(H * 32);
+  p.hcat = take(2 * H * 32);    // [h_traj ‖ h_c]  (fc input)
+  p.dcat = take(160 * 32);      // [z ‖ h_c ‖ 0]  (decoder input, K padded to 160)
+  p.gfc = take(32 * 32);        // [dmu ‖ dlogvar ‖ 0]
+  p.mask = take(9 * H * 4);     // ReLU bits: [mask][feature][row quad] nibbles
+  p.mulv = take(2 * Z * R * 4); // fp32 [j][row]: mu j, logvar Z + j
+  p.eps = take(Z * R * 4);
+  p.stdv = take(Z * R * 4);
+  p.rch0 = take(S * R * 4);     // fp32 [s][row]: recon time channel
+  p.gd0 = take(S * R * 4);      // fp32 [s][row]: its dL/drecon before the monotonicity term
+  p.dhc2 = take(H * R * 4);     // fp32 [c][row]: decoder share of dh_c
+  p.bias = take(nbias * 4);
+  p.part = take(NW * 8 * 4);
+  p.total = o;
+  return p;
+}
+
+__device__ __forceinline__ int ioff(int f, int quad) { return f * 16 + 4 * (quad ^ ((f >> 2) & 3)); }
+
+// A-operand fragment of K chunk kc from a feature-major image: lane (r = lane & 15, q = lane >> 4)
+// gets X[r][32kc + frag_k(q, e)] — two transposed 4-feature × 16-row block reads
+__device__ __forceinline__ bf16x8 xfrag(const __bf16* img, int kc) {
+  const int lane = threadIdx.x & 63;
+  const int f = kc * 32 + 4 * (lane >> 4) + ((lane & 15) >> 2);
+  const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((FC_LDS i16x4*)(img + ioff(f, lane & 3)));
+  const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((FC_LDS i16x4*)(img + ioff(f + 16, lane & 3)));
+  typedef short i16x8 __attribute__((ext_vector_type(8)));
+  const i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// this wave's fragments of n-tile t, chunks kc0 .. kc0+NC-1, of an operand with padded K extent Kp
+template <int NC>
+__device__ __forceinline__ void wload(bf16x8 (&w)[NC], const void* W, int Kp, int t, int kc0 = 0) {
+  const int lane = threadIdx.x & 63;
+  const __bf16* p = (const __bf16*)W + ((size_t)(t * (Kp >> 5) + kc0) * 64 + lane) * 8;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) w[c] = gld<bf16x8>(p + (size_t)c * 512);
+}
+
+template <int NC>
+__device__ __forceinline__ f32x4 mm(const __bf16* img, const bf16x8 (&w)[NC], int kc0 = 0) {
+  bf16x8 x[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) x[c] = xfrag(img, kc0 + c);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < NC; ++c) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[c], w[c], acc, 0, 0, 0);
+  return acc;
+}
+
+__device__ __forceinline__ bf16x4 to_bf4(f32x4 v) {
+  return bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+}
+__device__ __forceinline__ f32x4 from_bf4(bf16x4 h) {
+  return f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+}
+// 4 rows (b0 + 4q ..) of feature row f of an arena matrix
+__device__ __forceinline__ void arena4(void* base, int f, int Bp, int b0, int q, bf16x4 h) {
+  gst<bf16x4>((__bf16*)base + (size_t)f * Bp + b0 + 4 * q, h);
+}
+
+// lane q (= lane & 3) of a quad holding row r0+q's values y[0..3] gets value q of rows r0..r0+3
+__device__ __forceinline__ f32x4 quad_t(f32x4 y) {
+  const int lane = threadIdx.x & 63;
+  const bool b1 = lane & 1, b2 = lane & 2;
+  auto u = [](float f) { return __builtin_bit_cast(uint32_t, f); };
+  auto f = [](uint32_t v) { return __builtin_bit_cast(float, v); };
+  const uint32_t Ra = dpp_xor2(u(b2 ? y[0] : y[2])), Rb = dpp_xor2(u(b2 ? y[1] : y[3]));
+  const float A0 = b2 ? f(Ra) : y[0], A1 = b2 ? f(Rb) : y[1];
+  const float A2 = b2 ? y[2] : f(Ra), A3 = b2 ? y[3] : f(Rb);
+  const uint32_t Rc = dpp_xor1(u(b1 ? A0 : A1)), Rd = dpp_xor1(u(b1 ? A2 : A3));
+  return b1 ? f32x4{f(Rc), A1, f(Rd), A3} : f32x4{A0, f(Rc), A2, f(Rd)};
+}
+
+__device__ __forceinline__ void lbar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int NKI>
+__global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int Ip = NKI * 32, NG3 = NKI * 2;                 // D3 output n-tiles
+  constexpr int G3 = (NG3 + NW - 1) / NW;                     // D3 n-tiles per wave (max)
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+  const int n16 = lane & 15, q = lane >> 4;
+  const int b0 = blockIdx.x * R, nrows = max(0, min(R, a.batch - b0));
+  const int Bp = net.Bp, S = net.S, D = net.D, I = net.I;
+  const Lds P = lds_layout(Ip, S, net.nbias);
+  __bf16* const XIN = (__bf16*)(smem + P.xin);
+  __bf16* const CIN = (__bf16*)(smem + P.cin);
+  __bf16* const CB = (__bf16*)(smem + P.cb);
+  __bf16* const A0 = (__bf16*)(smem + P.a0);
+  __bf16* const A1 = (__bf16*)(smem + P.a1);
+  __bf16* const HCAT = (__bf16*)(smem + P.hcat);
+  __bf16* const DCAT = (__bf16*)(smem + P.dcat);
+  __bf16* const GFC = (__bf16*)(smem + P.gfc);
+  uint8_t* const MASK = (uint8_t*)(smem + P.mask);
+  float* const MULV = (float*)(smem + P.mulv);
+  float* const EPS = (float*)(smem + P.eps);
+  float* const STDV = (float*)(smem + P.stdv);
+  float* const RCH0 = (float*)(smem + P.rch0);
+  float* const GD0 = (float*)(smem + P.gd0);
+  float* const DHC2 = (float*)(smem + P.dhc2);
+  float* const BIAS = (float*)(smem + P.bias);
+  float* const PART = (float*)(smem + P.part);
+  const LayerDev* const L = net.L;
+  auto Wf = [&](int l) { return (const void*)L[l].Wf; };
+  auto Wb = [&](int l) { return (const void*)L[l].Wb; };
+  auto bias = [&](int l, int n) { return BIAS[net.bias_off[l] + n]; };
+  int stamp_i = 0;
+  auto stamp = [&]() {
+    if (CVAE_DIAG_STAMPS && a.stamps && tid == 0)
+      gst<unsigned long long>(a.stamps + blockIdx.x * 64 + (stamp_i < 63 ? stamp_i : 63), __builtin_amdgcn_s_memrealtime());
+    ++stamp_i;
+  };
+
+  // ---- hidden-layer epilogues (lane: feature n, rows 4q..4q+3)
+  auto relu = [&](f32x4 acc, float b, int mask, int n, uint32_t& nib) {
+    f32x4 y;
+    nib = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      y[i] = fmaxf(acc[i] + b, 0.f);
+      nib |= (y[i] > 0.f ? 1u : 0u) << i;
+    }
+    MASK[(mask * H + n) * 4 + q] = (uint8_t)nib;
+    return to_bf4(y);
+  };
+  auto masked = [&](f32x4 acc, int mask, int n) {
+    const uint32_t nib = MASK[(mask * H + n) * 4 + q];
+    f32x4 y;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) y[i] = (nib >> i) & 1u ? acc[i] : 0.f;
+    return to_bf4(y);
+  };
+
+  // ---- weights of the first two steps, before anything else
+  const int n = 16 * wave + n16;  // this lane's feature in the 128-wide layers (n-tile = wave)
+  bf16x8 wC0[1], wE0[NKI], wC1[4], wE1[4];
+  wload(wC0, Wf(LC0), L[LC0].Kp, wave);
+  wload(wE0, Wf(LE0), Ip, wave);
+  wload(wC1, Wf(LC1), H, wave);
+  wload(wE1, Wf(LE1), H, wave);
+  stamp();
+
+  // ---- prologue: x tile (relative transform, Training_VAE.py:345-348), eps, LDS state
+  float s_recon = 0.f, s_kl = 0.f, s_start = 0.f, s_t0 = 0.f, s_relu = 0.f;
+  {
+    constexpr int U = (R * NKI * 4 + NT - 1) / NT;  // 16-B vectors per thread (I <= Ip)
+    const int VPR = I >> 3, NV = R * VPR;
+    const float inv_VPR = 1.f / (float)VPR, inv_D = 1.f / (float)D;
+    const int last = max(a.batch - 1, 0);
+    const __bf16* xg = (const __bf16*)a.x;
+    bf16x8 xv[U], x0[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {  // task v: vector c of row 4rq + (v & 3) — quads = 4 rows, same c
+      const int v = min(u * NT + tid, NV - 1);
+      const int w = v >> 2, rq = fdiv(w, inv_VPR), c = w - rq * VPR, row = 4 * rq + (v & 3);
+      const int rr = min(b0 + row, last);
+      const int64_t g = a.idx ? gld<int64_t>(a.idx + rr) : (int64_t)rr;
+      xv[u] = gld<bf16x8>(xg + g * I + c * 8);
+      x0[u] = gld<bf16x8>(xg + g * I);  // the row's start point x[:,0,1:3] (Training_VAE.py:345)
+    }
+    // eps: 8 latents × 16 rows, 4 per thread (host-given, or Philox as philox_normal)
+    if (tid < 2 * R) {
+      const int row = tid >> 1, j0 = (tid & 1) * 4;
+      f32x4 e = {0.f, 0.f, 0.f, 0.f};
+      if (row < nrows)
+        e = a.eps ? gld<f32x4>(a.eps + (size_t)(b0 + row) * Z + j0)
+                  : philox_normal4(a.seed, a.offset, (uint32_t)(b0 + row), (uint32_t)j0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) EPS[(j0 + k) * R + row] = e[k];
+    }
+    for (int e = tid; e < net.nbias / 4; e += NT) ((f32x4*)BIAS)[e] = gld<f32x4>(net.bias_all + 4 * e);
+    // zero padding features read as MFMA K padding: CIN 4..31, XIN I..Ip-1, DCAT 136..159, GFC 16..31
+    for (int e = tid; e < 28 * 4; e += NT) *(uint64_t*)(CIN + (4 + e / 4) * 16 + 4 * (e & 3)) = 0ull;
+    for (int e = tid; e < (Ip - I) * 4; e += NT) *(uint64_t*)(XIN + (I + e / 4) * 16 + 4 * (e & 3)) = 0ull;
+    for (int e = tid; e < (160 - Z - H) * 4; e += NT) *(uint64_t*)(DCAT + (Z + H + e / 4) * 16 + 4 * (e & 3)) = 0ull;
+    for (int e = tid; e < 16 * 4; e += NT) *(uint64_t*)(GFC + (16 + e / 4) * 16 + 4 * (e & 3)) = 0ull;
+    void* const xe0 = L[LE0].xT;
+    void* const xc0 = L[LC0].xT;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int v = u * NT + tid;
+      if (v < NV) {  // NV % 4 == 0: quads are whole
+        const int w = v >> 2, rq = fdiv(w, inv_VPR), c = w - rq * VPR, row = 4 * rq + (v & 3);
+        const bool live = row < nrows;
+        const float s0 = live ? (float)x0[u][1] : 0.f, s1 = live ? (float)x0[u][2] : 0.f;
+        const int f0 = c * 8;
+        int d = f0 - fdiv(f0, inv_D) * D;
+        float val[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float xr = (float)xv[u][e] - (d == 1 ? s0 : 0.f) - (d == 2 ? s1 : 0.f);
+          val[e] = live ? (float)(__bf16)xr : 0.f;
+          d = d + 1 == D ? 0 : d + 1;
+        }
+        const int qd = lane & 3, r0q = rq;  // this lane ends with features f0+qd, f0+4+qd of rows 4rq..
+        const bf16x4 lo = to_bf4(quad_t(f32x4{val[0], val[1], val[2], val[3]}));
+        const bf16x4 hi = to_bf4(quad_t(f32x4{val[4], val[5], val[6], val[7]}));
+        *(bf16x4*)(XIN + ioff(f0 + qd, r0q)) = lo;
+        *(bf16x4*)(XIN + ioff(f0 + 4 + qd, r0q)) = hi;
+        arena4(xe0, f0 + qd, Bp, b0, r0q, lo);
+        arena4(xe0, f0 + 4 + qd, Bp, b0, r0q, hi);
+        if (c == 0) {  // quad-uniform: condition input features 0..3 (x, y, 0, 0) of these rows
+          const bf16x4 cs = to_bf4(quad_t(f32x4{(float)(__bf16)s0, (float)(__bf16)s1, 0.f, 0.f}));
+          *(bf16x4*)(CIN + ioff(qd, r0q)) = cs;
+          arena4(xc0, qd, Bp, b0, r0q, cs);
+        }
+      }
+    }
+  }
+  lbar();
+  stamp();
+
+  const float Bf = (float)a.batch;
+  const float inv_BSD = 1.f / (Bf * (float)(S * D)), inv_2B = 1.f / (2.f * Bf), inv_B = 1.f / Bf;
+  const float inv_BS1 = S > 1 ? 1.f / (Bf * (float)(S - 1)) : 0.f, inv_BZ = 1.f / (Bf * (float)Z);
+  const bool use_start = a.w_start > 0.f, use_time = a.w_time > 0.f;  // Training_VAE.py:247, :256
+
+  // ================================================================ forward
+  bf16x8 wE2[4];
+  wload(wE2, Wf(LE2), H, wave);
+  {  // C0 ‖ E0 (independent inputs)
+    uint32_t nib;
+    const bf16x4 hc = relu(mm(CIN, wC0), bias(LC0, n), MC0, n, nib);
+    *(bf16x4*)(CB + ioff(n, q)) = hc;
+    arena4(L[LC1].xT, n, Bp, b0, q, hc);
+    const bf16x4 he = relu(mm(XIN, wE0), bias(LE0, n), ME0, n, nib);
+    *(bf16x4*)(A0 + ioff(n, q)) = he;
+    arena4(L[LE1].xT, n, Bp, b0, q, he);
+  }
+  lbar();
+  stamp();
+  bf16x8 wE3[4];
+  wload(wE3, Wf(LE3), H, wave);
+  {  // C1 ‖ E1: h_c goes to both concatenations (fc input at H+n, decoder input at Z+n)
+    uint32_t nib;
+    const bf16x4 hc = relu(mm(CB, wC1), bias(LC1, n), MC1, n, nib);
+    *(bf16x4*)(HCAT + ioff(H + n, q)) = hc;
+    *(bf16x4*)(DCAT + ioff(Z + n, q)) = hc;
+    arena4(L[LFC].xT, H + n, Bp, b0, q, hc);
+    arena4(L[LD0].xT, Z + n, Bp, b0, q, hc);
+    const bf16x4 he = relu(mm(A0, wE1), bias(LE1, n), ME1, n, nib);
+    *(bf16x4*)(A1 + ioff(n, q)) = he;
+    arena4(L[LE2].xT, n, Bp, b0, q, he);
+  }
+  lbar();
+  stamp();
+  bf16x8 wFC[8];  // fc_mu ‖ fc_logvar: one real n-tile (every wave loads it; wave 0 computes)
+  wload(wFC, Wf(LFC), 2 * H, 0);
+  {  // E2
+    uint32_t nib;
+    const bf16x4 he = relu(mm(A1, wE2), bias(LE2, n), ME2, n, nib);
+    *(bf16x4*)(A0 + ioff(n, q)) = he;
+    arena4(L[LE3].xT, n, Bp, b0, q, he);
+  }
+  lbar();
+  stamp();
+  bf16x8 wD0[5];
+  wload(wD0, Wf(LD0), 160, wave);
+  {  // E3 → h_traj
+    uint32_t nib;
+    const bf16x4 he = relu(mm(A0, wE3), bias(LE3, n), ME3, n, nib);
+    *(bf16x4*)(HCAT + ioff(n, q)) = he;
+    arena4(L[LFC].xT, n, Bp, b0, q, he);
+  }
+  lbar();
+  stamp();
+  bf16x8 wD1[4];
+  wload(wD1, Wf(LD1), H, wave);
+  if (wave == 0) {  // fc_mu ‖ fc_logvar (:195-196) + reparameterize (:199-206) + KL terms (:243)
+    const f32x4 acc = mm(HCAT, wFC);
+    f32x4 y, lv;
+    const float b = bias(LFC, n16);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) y[i] = acc[i] + b;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) lv[i] = __shfl_xor(y[i], 8, 64);  // logvar j sits at feature 8 + j
+    if (n16 < Z) {
+      const int j = n16;
+      const f32x4 ep = *(const f32x4*)(EPS + j * R + 4 * q);
+      f32x4 sd, z;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        sd[i] = expf(0.5f * lv[i]);
+        z[i] = y[i] + ep[i] * sd[i];
+        if (4 * q + i < nrows) s_kl += 1.f + lv[i] - y[i] * y[i] - expf(lv[i]);
+      }
+      *(f32x4*)(MULV + j * R + 4 * q) = y;
+      *(f32x4*)(MULV + (Z + j) * R + 4 * q) = lv;
+      *(f32x4*)(STDV + j * R + 4 * q) = sd;
+      const bf16x4 zh = to_bf4(z);
+      *(bf16x4*)(DCAT + ioff(j, q)) = zh;
+      arena4(L[LD0].xT, j, Bp, b0, q, zh);
+    }
+  }
+  lbar();
+  stamp();
+  bf16x8 wD2[4];
+  wload(wD2, Wf(LD2), H, wave);
+  {  // D0
+    uint32_t nib;
+    const bf16x4 h = relu(mm(DCAT, wD0), bias(LD0, n), MD0, n, nib);
+    *(bf16x4*)(A0 + ioff(n, q)) = h;
+    arena4(L[LD1].xT, n, Bp, b0, q, h);
+  }
+  lbar();
+  stamp();
+  bf16x8 wD3[G3][4];  // D3's n-tiles of this wave (clamped: waves with fewer reload their last)
+#pragma unroll
+  for (int g = 0; g < G3; ++g) wload(wD3[g], Wf(LD3), H, min(wave + NW * g, NG3 - 1));
+  {  // D1
+    uint32_t nib;
+    const bf16x4 h = relu(mm(A0, wD1), bias(LD1, n), MD1, n, nib);
+    *(bf16x4*)(A1 + ioff(n, q)) = h;
+    arena4(L[LD2].xT, n, Bp, b0, q, h);
+  }
+  lbar();
+  stamp();
+  {  // D2
+    uint32_t nib;
+    const bf16x4 h = relu(mm(A1, wD2), bias(LD2, n), MD2, n, nib);
+    *(bf16x4*)(A0 + ioff(n, q)) = h;
+    arena4(L[LD3].xT, n, Bp, b0, q, h);
+  }
+  lbar();
+  stamp();
+  bf16x8 wD3b[NKI];
+  wload(wD3b, Wb(LD3), Ip, wave);
+  {  // D3 + conditional_vae_loss (:229-268) + dL/drecon, written over x_rel in place
+    const float inv_D = 1.f / (float)D;
+#pragma unroll
+    for (int g = 0; g < G3; ++g) {
+      const int t = wave + NW * g;
+      if (t < NG3) {
+        const f32x4 acc = mm(A0, wD3[g]);
+        const int f = 16 * t + n16;
+        f32x4 gi = {0.f, 0.f, 0.f, 0.f};
+        if (f < I) {
+          const float b = bias(LD3, f);
+          const f32x4 xr = from_bf4(*(const bf16x4*)(XIN + ioff(f, q)));
+          const int s = fdiv(f, inv_D), d = f - s * D;
+          f32x4 r;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const bool live = 4 * q + i < nrows;
+            r[i] = acc[i] + b;
+            const float diff = r[i] - xr[i];
+            if (!live) continue;
+            s_recon += diff * diff;
+            float gg = a.w_recon * 2.f * diff * inv_BSD;
+            if (s == 0 && (d == 1 || d == 2) && use_start) {
+              s_start += diff * diff;
+              gg += a.w_start * 2.f * diff * inv_2B;
+            }
+            if (d == 0 && s == 0 && use_time) {
+              s_t0 += r[i] * r[i];
+              gg += a.w_time * 2.f * r[i] * inv_B;
+            }
+            gi[i] = gg;
+          }
+          if (d == 0) {
+            *(f32x4*)(RCH0 + s * R + 4 * q) = r;
+            *(f32x4*)(GD0 + s * R + 4 * q) = gi;
+          }
+        }
+        *(bf16x4*)(XIN + ioff(f, q)) = to_bf4(gi);  // pad features f >= I: 0
+      }
+    }
+  }
+  lbar();
+  // time-monotonicity term relu(r_s − r_{s+1}) (:261-262, ReLU'(0) = 0) into the time channel of
+  // dL/drecon, then the feature-major arena copy gT(D3) of the whole tile
+  {
+    constexpr int UF = (Ip * 4 + NT - 1) / NT;
+    const float inv_D = 1.f / (float)D, wt = a.w_time * inv_BS1;
+    void* const gd3 = L[LD3].gT;
+#pragma unroll
+    for (int u = 0; u < UF; ++u) {
+      const int e = u * NT + tid;
+      if (e < Ip * 4) {
+        const int f = e >> 2, qq = e & 3;
+        bf16x4 h = *(const bf16x4*)(XIN + ioff(f, qq));
+        const int s = fdiv(f, inv_D);
+        if (use_time && f < I && f == s * D) {
+          f32x4 gv = *(const f32x4*)(GD0 + s * R + 4 * qq);  // fp32: dL/drecon is rounded once
+          const f32x4 rs = *(const f32x4*)(RCH0 + s * R + 4 * qq);
+          const f32x4 rn = s < S - 1 ? *(const f32x4*)(RCH0 + (s + 1) * R + 4 * qq) : rs;
+          const f32x4 rp = s > 0 ? *(const f32x4*)(RCH0 + (s - 1) * R + 4 * qq) : rs;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (4 * qq + i >= nrows) continue;
+            const float u1 = rs[i] - rn[i], u0 = rp[i] - rs[i];
+            if (u1 > 0.f) {
+              gv[i] += wt;
+              s_relu += u1;
+            }
+            if (u0 > 0.f) gv[i] -= wt;
+          }
+          h = to_bf4(gv);
+          *(bf16x4*)(XIN + ioff(f, qq)) = h;
+        }
+        arena4(gd3, f, Bp, b0, qq, h);
+      }
+    }
+  }
+  lbar();
+  stamp();
+
+  // ================================================================ backward
+  bf16x8 wD2b[4], wD1b[4];
+  wload(wD2b, Wb(LD2), H, wave);
+  wload(wD1b, Wb(LD1), H, wave);
+  {  // D3ᵀ: dL/d h_D2 = GL · W_D3, ReLU mask of D2
+    const bf16x4 h = masked(mm(XIN, wD3b), MD2, n);
+    *(bf16x4*)(A1 + ioff(n, q)) = h;
+    arena4(L[LD2].gT, n, Bp, b0, q, h);
+  }
+  lbar();
+  stamp();
+  bf16x8 wD0b[2][4];  // decoder layer 0's input has 160 (136 real) features: n-tiles wave, wave + 8
+  wload(wD0b[0], Wb(LD0), H, wave);
+  wload(wD0b[1], Wb(LD0), H, min(wave + NW, 9));
+  {
+    const bf16x4 h = masked(mm(A1, wD2b), MD1, n);
+    *(bf16x4*)(A0 + ioff(n, q)) = h;
+    arena4(L[LD1].gT, n, Bp, b0, q, h);
+  }
+  lbar();
+  stamp();
+  bf16x8 wFCb[2][1];  // fc input features 0..255: n-tiles wave (h_traj) and wave + 8 (h_c)
+  wload(wFCb[0], Wb(LFC), 32, wave);
+  wload(wFCb[1], Wb(LFC), 32, wave + NW);
+  {
+    const bf16x4 h = masked(mm(A0, wD1b), MD0, n);
+    *(bf16x4*)(A1 + ioff(n, q)) = h;
+    arena4(L[LD0].gT, n, Bp, b0, q, h);
+  }
+  lbar();
+  stamp();
+  bf16x8 wE3b[4];
+  wload(wE3b, Wb(LE3), H, wave);
+  {  // D0ᵀ: [dz ‖ dh_c(decoder share)]; dz → KL/reparameterisation backward → G_fc
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      const int t = wave + NW * h2;
+      if (h2 == 0 || t < 10) {
+        const f32x4 acc = mm(A1, wD0b[h2]);
+        const int f = 16 * t + n16;
+        if (f < Z) {
+          const int j = f;
+          const f32x4 mu = *(const f32x4*)(MULV + j * R + 4 * q), lv = *(const f32x4*)(MULV + (Z + j) * R + 4 * q);
+          const f32x4 ep = *(const f32x4*)(EPS + j * R + 4 * q), sd = *(const f32x4*)(STDV + j * R + 4 * q);
+          f32x4 gm, gl;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const bool live = 4 * q + i < nrows;
+            gm[i] = live ? a.w_kld * mu[i] * inv_BZ + acc[i] : 0.f;
+            gl[i] = live ? a.w_kld * 0.5f * (expf(lv[i]) - 1.f) * inv_BZ + acc[i] * ep[i] * 0.5f * sd[i] : 0.f;
+          }
+          const bf16x4 hm = to_bf4(gm), hl = to_bf4(gl);
+          *(bf16x4*)(GFC + ioff(j, q)) = hm;
+          *(bf16x4*)(GFC + ioff(Z + j, q)) = hl;
+          arena4(L[LFC].gT, j, Bp, b0, q, hm);
+          arena4(L[LFC].gT, Z + j, Bp, b0, q, hl);
+        } else if (f < Z + H) {
+          *(f32x4*)(DHC2 + (f - Z) * R + 4 * q) = acc;
+        }
+      }
+    }
+  }
+  lbar();
+  stamp();
+  bf16x8 wE2b[4];
+  wload(wE2b, Wb(LE2), H, wave);
+  {  // fcᵀ: dh = G_fc · W_fc → h_traj gradient (mask E3) and h_c gradient (+ decoder share, mask C1)
+    const bf16x4 ht = masked(mm(GFC, wFCb[0]), ME3, n);
+    *(bf16x4*)(A0 + ioff(n, q)) = ht;
+    arena4(L[LE3].gT, n, Bp, b0, q, ht);
+    f32x4 acc = mm(GFC, wFCb[1]);
+    const f32x4 d2 = *(const f32x4*)(DHC2 + n * R + 4 * q);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] += d2[i];
+    const bf16x4 hc = masked(acc, MC1, n);
+    *(bf16x4*)(CB + ioff(n, q)) = hc;
+    arena4(L[LC1].gT, n, Bp, b0, q, hc);
+  }
+  lbar();
+  stamp();
+  bf16x8 wE1b[4], wC1b[4];
+  wload(wE1b, Wb(LE1), H, wave);
+  wload(wC1b, Wb(LC1), H, wave);
+  {  // E3ᵀ
+    const bf16x4 h = masked(mm(A0, wE3b), ME2, n);
+    *(bf16x4*)(A1 + ioff(n, q)) = h;
+    arena4(L[LE2].gT, n, Bp, b0, q, h);
+  }
+  lbar();
+  stamp();
+  {  // E2ᵀ
+    const bf16x4 h = masked(mm(A1, wE2b), ME1, n);
+    *(bf16x4*)(A0 + ioff(n, q)) = h;
+    arena4(L[LE1].gT, n, Bp, b0, q, h);
+  }
+  lbar();
+  stamp();
+  {  // E1ᵀ ‖ C1ᵀ: the last two gradients only feed the dW kernel
+    arena4(L[LE0].gT, n, Bp, b0, q, masked(mm(A0, wE1b), ME0, n));
+    arena4(L[LC0].gT, n, Bp, b0, q, masked(mm(CB, wC1b), MC0, n));
+  }
+
+  // ---- loss partial sums (deterministic order)
+  s_recon = wave_sum(s_recon);
+  s_kl = wave_sum(s_kl);
+  s_start = wave_sum(s_start);
+  s_t0 = wave_sum(s_t0);
+  s_relu = wave_sum(s_relu);
+  if (lane == 0) {
+    PART[wave * 8 + 0] = s_recon;
+    PART[wave * 8 + 1] = s_kl;
+    PART[wave * 8 + 2] = s_start;
+    PART[wave * 8 + 3] = s_t0;
+    PART[wave * 8 + 4] = s_relu;
+  }
+  lbar();
+  stamp();
+  if (tid < 5) {
+    float s = 0.f;
+    for (int w = 0; w < NW; ++w) s += PART[w * 8 + tid];
+    gst<float>(a.partials + blockIdx.x * 8 + tid, s);
+  }
+}
+
+}  // namespace fchain

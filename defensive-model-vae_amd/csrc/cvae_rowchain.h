@@ -264,6 +264,19 @@ __device__ __forceinline__ void load_block(WBlock<T>& wb, const T* __restrict__ 
   }
 }
 
+// B-operand fragment of one row-major activation row for K chunk starting at p: lane group q takes
+// the chunk positions frag_k(q, e) (two 8-B halves for bf16, matching the weight fragments)
+template <typename T>
+__device__ __forceinline__ typename Op<T>::V xchunk(const T* p, int q);
+template <>
+__device__ __forceinline__ f32x4 xchunk<float>(const float* p, int q) { return *(const f32x4*)(p + 4 * q); }
+template <>
+__device__ __forceinline__ bf16x8 xchunk<__bf16>(const __bf16* p, int q) {
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  const bf16x4 lo = *(const bf16x4*)(p + 4 * q), hi = *(const bf16x4*)(p + 16 + 4 * q);
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
 // epi(row, f0, v) receives v[i] = Y[row][f0 + i], i = 0..3: the MFMA computes Yᵀ = W·Xᵀ
 // (A = weights, B = activations), so a lane's accumulator holds FOUR CONSECUTIVE FEATURES of
 // one row — one 8/16-B LDS store, one float4 bias and one 4-bit mask nibble per call.
@@ -276,7 +289,7 @@ __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T
   using V = typename Op<T>::V;
   constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC, MT = R >= 16 ? R / 16 : 1;
   const int lane = threadIdx.x & 63, wave = wave_id();
-  const int r16 = lane & 15, kq = (lane >> 4) * EPL;
+  const int r16 = lane & 15;
   const int NG = Np / RC_GW, nk = Kp / KC, nblk = (nk + NKB - 1) / NKB;
   const int ng_mine = NG > wave ? (NG - wave + RC_NW - 1) / RC_NW : 0;
   const int nitems = ng_mine * nblk;
@@ -325,7 +338,7 @@ __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T
     for (int u = 0; u < NKB; ++u) {
       const int kc = min(blk * NKB + u, nk - 1);
 #pragma unroll
-      for (int m = 0; m < MT; ++m) xa[u][m] = *(const V*)(Xs + tile_row<R>(m, r16) * ldx + kc * KC + kq);
+      for (int m = 0; m < MT; ++m) xa[u][m] = xchunk<T>(Xs + tile_row<R>(m, r16) * ldx + kc * KC, lane >> 4);
     }
 #pragma unroll
     for (int u = 0; u < NKB; ++u) {

@@ -152,8 +152,9 @@ __device__ __forceinline__ void apply_bias(const LayerDev& L, int o, float g, co
 }
 
 // Both operand copies of one 32×32 tile from its LDS image, as whole MFMA fragments.  Fragment
-// (n-tile t, chunk kc) lane ln holds elements (16t + (ln & 15), KC·kc + EPL·(ln >> 4) + e), so a
-// tile is 2 n-tiles × 32/KC chunks of contiguous 1-KB blocks per copy (frag_off).
+// (n-tile t, chunk kc) lane ln holds elements (16t + (ln & 15), KC·kc + frag_k(ln >> 4, e)) at
+// ((t·Kp/KC + kc)·64 + ln)·EPL (frag_off), so a tile is 2 n-tiles × 32/KC chunks of contiguous
+// 1-KB blocks per copy.
 template <typename T>
 __device__ __forceinline__ void store_operands(const LayerDev& L, int o0, int i0, const float* wt) {
   using V = typename Op<T>::V;
@@ -166,20 +167,20 @@ __device__ __forceinline__ void store_operands(const LayerDev& L, int o0, int i0
     const int jj = wb ? j - PER_COPY : j;
     const int blk = jj >> 6, ln = jj & 63;
     const int bt = blk / CPT, bk = blk - bt * CPT;
-    const int nl = bt * 16 + (ln & 15), kl = bk * KC + (ln >> 4) * EPL;
+    const int nl = bt * 16 + (ln & 15), kl = bk * KC, q = ln >> 4;  // lane (nl, q) of chunk kl
     V val;
     if (wb) {  // Wb = Wᵀ: rows = inputs i, K = outputs o
 #pragma unroll
-      for (int e = 0; e < EPL; ++e) val[e] = to_t<T>(wt[(kl + e) * WT_LD + nl]);
-      gst<V>((T*)L.Wb + frag_off<T>(i0 + nl, o0 + kl, L.Np), val);
+      for (int e = 0; e < EPL; ++e) val[e] = to_t<T>(wt[(kl + frag_k<T>(q, e)) * WT_LD + nl]);
+      gst<V>((T*)L.Wb + ((size_t)(((i0 >> 4) + bt) * (L.Np / KC) + (o0 + kl) / KC) * 64 + ln) * EPL, val);
     } else {
 #pragma unroll
-      for (int e = 0; e < EPL; e += 4) {
-        const f32x4 q = *(const f32x4*)(wt + nl * WT_LD + kl + e);
+      for (int e = 0; e < EPL; e += 4) {  // 4 consecutive K positions per half-fragment
+        const f32x4 v4 = *(const f32x4*)(wt + nl * WT_LD + kl + frag_k<T>(q, e));
 #pragma unroll
-        for (int c = 0; c < 4; ++c) val[e + c] = to_t<T>(q[c]);
+        for (int c = 0; c < 4; ++c) val[e + c] = to_t<T>(v4[c]);
       }
-      gst<V>((T*)L.Wf + frag_off<T>(o0 + nl, i0 + kl, L.Kp), val);
+      gst<V>((T*)L.Wf + ((size_t)(((o0 >> 4) + bt) * (L.Kp / KC) + (i0 + kl) / KC) * 64 + ln) * EPL, val);
     }
   }
 }
