@@ -327,7 +327,18 @@ int alloc_arena(cvae_handle* h) {
   for (int m = 0; m < cvae_handle::ST_N; ++m) {
     const std::vector<StepSpec> spec = build_steps(n, m);
     std::vector<StepDesc> st;
-    for (const StepSpec& x : spec) {
+    for (StepSpec x : spec) {
+      // feature rows of the arena matrices g1 / g2 point into (xT: Kp, gT: Np of their layer)
+      auto kf_of = [&](const void* g) {
+        for (int l = 0; l < n.n_layers; ++l) {
+          if (g == n.L[l].xT) return n.L[l].Kp;
+          if (g == n.L[l].gT) return n.L[l].Np;
+        }
+        return 0;
+      };
+      x.kf1 = x.g1 ? kf_of(x.g1) : 0;
+      x.kf2 = x.g2 ? kf_of(x.g2) : 0;
+      if ((x.g1 && !x.kf1) || (x.g2 && !x.kf2)) return fail(CVAE_E_INVALID, "step arena target is not a layer matrix");
       if (x.goff1 < 0 || x.goff1 > 0xFFFF || x.goff2 < 0 || x.goff2 > 0xFFFF || x.mask_out > 62 || x.mask_in > 62)
         return fail(CVAE_E_INVALID, "step descriptor field out of range");
       st.push_back(encode_step(x));
@@ -424,7 +435,7 @@ int plan_fast(cvae_handle* h) {
   h->fast_nki = 0;
   const char* env = std::getenv("CVAE_GENERIC");
   if ((env && env[0] == '1') || c.dtype != CVAE_BF16 || c.hidden_dim != fchain::H || c.latent_dim != fchain::Z ||
-      c.n_enc != 4 || c.n_dec != 4 || n.I % 8 != 0)
+      c.n_enc != 4 || c.n_dec != 4 || n.I % 8 != 0 || n.nbias > 16 * fchain::NT)
     return CVAE_OK;
   for (int nki : kFastNki) {
     if (n.Ip != 32 * nki) continue;
@@ -615,10 +626,10 @@ int cvae_train_fwd_bwd(cvae_handle* h, const void* x, const int64_t* idx, int ba
   const int nt = (int)h->tiles.size();
   if ((rc = tmark(h, s, "wgrad"))) return rc;
   if (h->cfg.dtype == CVAE_BF16)
-    hipLaunchKernelGGL((wgrad_kernel<__bf16, PM_GRAD>), dim3(nt), dim3(CVAE_THREADS), 0, s, h->net, h->d_tiles,
+    hipLaunchKernelGGL((wgrad_kernel<__bf16, PM_GRAD>), dim3(nt), dim3(WG_THREADS), 0, s, h->net, h->d_tiles,
                        bk_of(h, batch), aa, la);
   else
-    hipLaunchKernelGGL((wgrad_kernel<float, PM_GRAD>), dim3(nt), dim3(CVAE_THREADS), 0, s, h->net, h->d_tiles,
+    hipLaunchKernelGGL((wgrad_kernel<float, PM_GRAD>), dim3(nt), dim3(WG_THREADS), 0, s, h->net, h->d_tiles,
                        bk_of(h, batch), aa, la);
   HIPCK(hipGetLastError());
   return tmark(h, s, "end");
@@ -660,10 +671,10 @@ int cvae_train_step(cvae_handle* h, const void* x, const int64_t* idx, int batch
   const int nt = (int)h->tiles.size();
   if ((rc = tmark(h, s, "wgrad_adam"))) return rc;
   if (h->cfg.dtype == CVAE_BF16)
-    hipLaunchKernelGGL((wgrad_kernel<__bf16, PM_ADAM>), dim3(nt), dim3(CVAE_THREADS), 0, s, h->net, h->d_tiles,
+    hipLaunchKernelGGL((wgrad_kernel<__bf16, PM_ADAM>), dim3(nt), dim3(WG_THREADS), 0, s, h->net, h->d_tiles,
                        bk_of(h, batch), aa, la);
   else
-    hipLaunchKernelGGL((wgrad_kernel<float, PM_ADAM>), dim3(nt), dim3(CVAE_THREADS), 0, s, h->net, h->d_tiles,
+    hipLaunchKernelGGL((wgrad_kernel<float, PM_ADAM>), dim3(nt), dim3(WG_THREADS), 0, s, h->net, h->d_tiles,
                        bk_of(h, batch), aa, la);
   HIPCK(hipGetLastError());
   return tmark(h, s, "end");

@@ -9,10 +9,12 @@
 //      Wb ~ [Kp][Np]  (= Wᵀ zero-padded)                  — operand of the dX GEMM
 //    plus a padded fp32 bias[Np].  The fp32 master parameters stay in the
 //    caller's flat state_dict-ordered buffer.
-//  * Activation arena, feature-major ("transposed") [features][Bp] in T:
+//  * Activation arena, TILE-MAJOR feature-major in T: a matrix with Kf feature rows (Kf = Kp for
+//    xT, Np for gT) is [Bp/16 row tiles][Kf features][16 batch rows] (aoff below):
 //      xT(l) = input of layer l, gT(l) = dL/d(pre-activation) of layer l.
-//    The weight-gradient kernel reduces over the batch with both operands
-//    batch-contiguous: dW_l = gT(l) · xT(l)ᵀ.
+//    A row-chain workgroup (16 batch rows) writes one contiguous [Kf][16] slab, so its epilogue
+//    stores are whole 512-B runs; the weight-gradient kernel reduces over the batch with both
+//    operands batch-contiguous in 16-row runs: dW_l = gT(l) · xT(l)ᵀ.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -59,6 +61,11 @@ __host__ __device__ inline int lFC(const NetDev& n) { return 2 + n.n_enc; }
 __host__ __device__ inline int lD(const NetDev& n, int i) { return 3 + n.n_enc + i; }
 
 struct TileDesc { int layer, o0, i0, pad_; };
+
+// element (feature f, batch row b) of an arena matrix with Kf feature rows
+__host__ __device__ inline size_t aoff(int f, int b, int Kf) {
+  return ((size_t)(b >> 4) * Kf + f) * 16 + (b & 15);
+}
 
 // ------------------------------------------------------------------ operand types
 template <typename T> struct Op;
@@ -148,17 +155,17 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
   return c;
 }
 
-// standard normal eps for (row b, latent j): Box-Muller on Philox(seed; b, j/4, offset)
+// standard normal eps for (row b, latent j): Box-Muller on Philox(seed; b, j/4, offset), with the
+// hardware log/sin/cos (v_log_f32, v_sin_f32, v_cos_f32: ~1e-6 relative; eps is a random draw)
 __device__ __forceinline__ float philox_normal(uint64_t seed, uint64_t offset, uint32_t b, uint32_t j) {
   const uint4 r = philox4x32_10(make_uint4(b, j >> 2, (uint32_t)offset, (uint32_t)(offset >> 32)),
                                 make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
   const uint32_t u0 = (j & 2) ? r.z : r.x, u1 = (j & 2) ? r.w : r.y;
   const float f0 = ((float)u0 + 1.0f) * 2.3283064365386963e-10f;  // (0,1]
   const float f1 = (float)u1 * 2.3283064365386963e-10f;
-  const float rad = sqrtf(-2.0f * logf(f0));
-  float s, c;
-  sincosf(6.283185307179586f * f1, &s, &c);
-  return (j & 1) ? rad * s : rad * c;
+  const float rad = sqrtf(-2.0f * __logf(f0));
+  const float ang = 6.283185307179586f * f1;
+  return (j & 1) ? rad * __sinf(ang) : rad * __cosf(ang);
 }
 
 // the 4 normals j = j0 .. j0+3 (j0 % 4 == 0) of philox_normal from ONE Philox block — the same
@@ -172,11 +179,10 @@ __device__ __forceinline__ f32x4 philox_normal4(uint64_t seed, uint64_t offset, 
   for (int h = 0; h < 2; ++h) {
     const float f0 = ((float)us[2 * h] + 1.0f) * 2.3283064365386963e-10f;  // (0,1]
     const float f1 = (float)us[2 * h + 1] * 2.3283064365386963e-10f;
-    const float rad = sqrtf(-2.0f * logf(f0));
-    float s, c;
-    sincosf(6.283185307179586f * f1, &s, &c);
-    out[2 * h] = rad * c;
-    out[2 * h + 1] = rad * s;
+    const float rad = sqrtf(-2.0f * __logf(f0));
+    const float ang = 6.283185307179586f * f1;
+    out[2 * h] = rad * __cosf(ang);
+    out[2 * h + 1] = rad * __sinf(ang);
   }
   return out;
 }

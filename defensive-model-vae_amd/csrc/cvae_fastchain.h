@@ -82,7 +82,16 @@ __device__ __forceinline__ void wload(bf16x8 (&w)[NC], const void* W, int Kp, in
   const int lane = threadIdx.x & 63;
   const __bf16* p = (const __bf16*)W + ((size_t)(t * (Kp >> 5) + kc0) * 64 + lane) * 8;
 #pragma unroll
-  for (int c = 0; c < NC; ++c) w[c] = gld<bf16x8>(p + (size_t)c * 512);
+  for (int c = 0; c < NC; ++c) w[c] = CVAE_DIAG_NOWLOAD ? bf16x8{} : gld<bf16x8>(p + (size_t)c * 512);
+}
+
+// elements [C0, C1) of a whole-K fragment array
+template <int C0, int C1, int NC>
+__device__ __forceinline__ void wload_part(bf16x8 (&w)[NC], const void* W, int Kp, int t) {
+  const int lane = threadIdx.x & 63;
+  const __bf16* p = (const __bf16*)W + ((size_t)(t * (Kp >> 5)) * 64 + lane) * 8;
+#pragma unroll
+  for (int c = C0; c < C1; ++c) w[c] = CVAE_DIAG_NOWLOAD ? bf16x8{} : gld<bf16x8>(p + (size_t)c * 512);
 }
 
 template <int NC>
@@ -102,9 +111,10 @@ __device__ __forceinline__ bf16x4 to_bf4(f32x4 v) {
 __device__ __forceinline__ f32x4 from_bf4(bf16x4 h) {
   return f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
 }
-// 4 rows (b0 + 4q ..) of feature row f of an arena matrix
-__device__ __forceinline__ void arena4(void* base, int f, int Bp, int b0, int q, bf16x4 h) {
-  gst<bf16x4>((__bf16*)base + (size_t)f * Bp + b0 + 4 * q, h);
+// rows b0 + 4q .. +3 of feature f of an arena matrix with Kf feature rows (aoff; b0 % 16 == 0):
+// the 16 features × 4 row quads of one wave instruction are 512 contiguous bytes
+__device__ __forceinline__ void arena4(void* base, int Kf, int f, int b0, int q, bf16x4 h) {
+  if (!CVAE_DIAG_NOSTORE) gst<bf16x4>((__bf16*)base + aoff(f, b0 + 4 * q, Kf), h);
 }
 
 // lane q (= lane & 3) of a quad holding row r0+q's values y[0..3] gets value q of rows r0..r0+3
@@ -180,13 +190,15 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
     return to_bf4(y);
   };
 
-  // ---- weights of the first two steps, before anything else
   const int n = 16 * wave + n16;  // this lane's feature in the 128-wide layers (n-tile = wave)
-  bf16x8 wC0[1], wE0[NKI], wC1[4], wE1[4];
-  wload(wC0, Wf(LC0), L[LC0].Kp, wave);
-  wload(wE0, Wf(LE0), Ip, wave);
-  wload(wC1, Wf(LC1), H, wave);
-  wload(wE1, Wf(LE1), H, wave);
+  // Weight registers of every step.  Issue schedule (loads per wave, after the step's own stores so
+  // a burst never holds an epilogue store back; big sets spread over several steps, >= 2 steps
+  // ahead where registers allow):
+  //   prologue: x, biases, C0, E0[0:10) | end: E0[10:), C1 | S0: E1 E2 | S1: E3 FC | S2: D0 D1 |
+  //   S3: D2 D3[g0-1] | S4: D3[g2-4] | S5: D3b[0:NKI/2) | S6: D3b[NKI/2:) | S8 (after D3's tiles):
+  //   D2b D1b | S8 end: D0b FCb | S9: E3b E2b | S10: E1b C1b
+  bf16x8 wC0[1], wE0[NKI], wC1[4], wE1[4], wE2[4], wE3[4], wFC[8], wD0[5], wD1[4], wD2[4];
+  bf16x8 wD3[G3][4], wD3b[NKI], wD2b[4], wD1b[4], wD0b[2][4], wFCb[2][1], wE3b[4], wE2b[4], wE1b[4], wC1b[4];
   stamp();
 
   // ---- prologue: x tile (relative transform, Training_VAE.py:345-348), eps, LDS state
@@ -198,15 +210,35 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
     const int last = max(a.batch - 1, 0);
     const __bf16* xg = (const __bf16*)a.x;
     bf16x8 xv[U], x0[U];
+    int64_t gr[U];  // source row of each task (all idx loads in flight together)
+    int cc[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {  // task v: vector c of row 4rq + (v & 3) — quads = 4 rows, same c
       const int v = min(u * NT + tid, NV - 1);
       const int w = v >> 2, rq = fdiv(w, inv_VPR), c = w - rq * VPR, row = 4 * rq + (v & 3);
-      const int rr = min(b0 + row, last);
-      const int64_t g = a.idx ? gld<int64_t>(a.idx + rr) : (int64_t)rr;
-      xv[u] = gld<bf16x8>(xg + g * I + c * 8);
-      x0[u] = gld<bf16x8>(xg + g * I);  // the row's start point x[:,0,1:3] (Training_VAE.py:345)
+      gr[u] = min(b0 + row, last);
+      cc[u] = c;
     }
+    if (a.idx) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) gr[u] = gld<int64_t>(a.idx + gr[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      xv[u] = gld<bf16x8>(xg + gr[u] * I + cc[u] * 8);
+      x0[u] = gld<bf16x8>(xg + gr[u] * I);  // the row's start point x[:,0,1:3] (Training_VAE.py:345)
+    }
+    constexpr int UB = 4;  // biases: nbias/4 <= UB*NT float4
+    f32x4 bv[UB];
+#pragma unroll
+    for (int k = 0; k < UB; ++k) {
+      const int e = min(k * NT + tid, net.nbias / 4 - 1);
+      bv[k] = gld<f32x4>(net.bias_all + 4 * e);
+    }
+    // the weights of the first step queue behind the x tile and the biases (vmcnt retires in order)
+    wload(wC0, Wf(LC0), L[LC0].Kp, wave);
+    wload_part<0, NKI / 2>(wE0, Wf(LE0), Ip, wave);
+    stamp();
     // eps: 8 latents × 16 rows, 4 per thread (host-given, or Philox as philox_normal)
     if (tid < 2 * R) {
       const int row = tid >> 1, j0 = (tid & 1) * 4;
@@ -217,12 +249,17 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) EPS[(j0 + k) * R + row] = e[k];
     }
-    for (int e = tid; e < net.nbias / 4; e += NT) ((f32x4*)BIAS)[e] = gld<f32x4>(net.bias_all + 4 * e);
+    stamp();
     // zero padding features read as MFMA K padding: CIN 4..31, XIN I..Ip-1, DCAT 136..159, GFC 16..31
-    for (int e = tid; e < 28 * 4; e += NT) *(uint64_t*)(CIN + (4 + e / 4) * 16 + 4 * (e & 3)) = 0ull;
-    for (int e = tid; e < (Ip - I) * 4; e += NT) *(uint64_t*)(XIN + (I + e / 4) * 16 + 4 * (e & 3)) = 0ull;
-    for (int e = tid; e < (160 - Z - H) * 4; e += NT) *(uint64_t*)(DCAT + (Z + H + e / 4) * 16 + 4 * (e & 3)) = 0ull;
-    for (int e = tid; e < 16 * 4; e += NT) *(uint64_t*)(GFC + (16 + e / 4) * 16 + 4 * (e & 3)) = 0ull;
+    // (each count <= 4 * 32 features < NT: one store per thread)
+    if (tid < 28 * 4) *(uint64_t*)(CIN + (4 + tid / 4) * 16 + 4 * (tid & 3)) = 0ull;
+    if (tid < (Ip - I) * 4) *(uint64_t*)(XIN + (I + tid / 4) * 16 + 4 * (tid & 3)) = 0ull;
+    if (tid < (160 - Z - H) * 4) *(uint64_t*)(DCAT + (Z + H + tid / 4) * 16 + 4 * (tid & 3)) = 0ull;
+    if (tid < 16 * 4) *(uint64_t*)(GFC + (16 + tid / 4) * 16 + 4 * (tid & 3)) = 0ull;
+#pragma unroll
+    for (int k = 0; k < UB; ++k)
+      if (k * NT + tid < net.nbias / 4) ((f32x4*)BIAS)[k * NT + tid] = bv[k];
+    stamp();
     void* const xe0 = L[LE0].xT;
     void* const xc0 = L[LC0].xT;
 #pragma unroll
@@ -241,21 +278,24 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
           val[e] = live ? (float)(__bf16)xr : 0.f;
           d = d + 1 == D ? 0 : d + 1;
         }
-        const int qd = lane & 3, r0q = rq;  // this lane ends with features f0+qd, f0+4+qd of rows 4rq..
+        const int qd = lane & 3;  // this lane ends with features f0+qd, f0+4+qd of rows 4rq..4rq+3
         const bf16x4 lo = to_bf4(quad_t(f32x4{val[0], val[1], val[2], val[3]}));
         const bf16x4 hi = to_bf4(quad_t(f32x4{val[4], val[5], val[6], val[7]}));
-        *(bf16x4*)(XIN + ioff(f0 + qd, r0q)) = lo;
-        *(bf16x4*)(XIN + ioff(f0 + 4 + qd, r0q)) = hi;
-        arena4(xe0, f0 + qd, Bp, b0, r0q, lo);
-        arena4(xe0, f0 + 4 + qd, Bp, b0, r0q, hi);
+        *(bf16x4*)(XIN + ioff(f0 + qd, rq)) = lo;
+        *(bf16x4*)(XIN + ioff(f0 + 4 + qd, rq)) = hi;
+        arena4(xe0, L[LE0].Kp, f0 + qd, b0, rq, lo);
+        arena4(xe0, L[LE0].Kp, f0 + 4 + qd, b0, rq, hi);
         if (c == 0) {  // quad-uniform: condition input features 0..3 (x, y, 0, 0) of these rows
           const bf16x4 cs = to_bf4(quad_t(f32x4{(float)(__bf16)s0, (float)(__bf16)s1, 0.f, 0.f}));
-          *(bf16x4*)(CIN + ioff(qd, r0q)) = cs;
-          arena4(xc0, qd, Bp, b0, r0q, cs);
+          *(bf16x4*)(CIN + ioff(qd, rq)) = cs;
+          arena4(xc0, L[LC0].Kp, qd, b0, rq, cs);
         }
       }
     }
   }
+  stamp();
+  wload_part<NKI / 2, NKI>(wE0, Wf(LE0), Ip, wave);
+  wload(wC1, Wf(LC1), H, wave);
   lbar();
   stamp();
 
@@ -265,57 +305,57 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
   const bool use_start = a.w_start > 0.f, use_time = a.w_time > 0.f;  // Training_VAE.py:247, :256
 
   // ================================================================ forward
-  bf16x8 wE2[4];
-  wload(wE2, Wf(LE2), H, wave);
-  {  // C0 ‖ E0 (independent inputs)
+  {  // S0: C0 ‖ E0 (independent inputs)
     uint32_t nib;
     const bf16x4 hc = relu(mm(CIN, wC0), bias(LC0, n), MC0, n, nib);
     *(bf16x4*)(CB + ioff(n, q)) = hc;
-    arena4(L[LC1].xT, n, Bp, b0, q, hc);
+    arena4(L[LC1].xT, L[LC1].Kp, n, b0, q, hc);
     const bf16x4 he = relu(mm(XIN, wE0), bias(LE0, n), ME0, n, nib);
     *(bf16x4*)(A0 + ioff(n, q)) = he;
-    arena4(L[LE1].xT, n, Bp, b0, q, he);
+    arena4(L[LE1].xT, L[LE1].Kp, n, b0, q, he);
   }
+  wload(wE1, Wf(LE1), H, wave);
+  wload(wE2, Wf(LE2), H, wave);
   lbar();
   stamp();
-  bf16x8 wE3[4];
-  wload(wE3, Wf(LE3), H, wave);
-  {  // C1 ‖ E1: h_c goes to both concatenations (fc input at H+n, decoder input at Z+n)
+  {  // S1: C1 ‖ E1: h_c goes to both concatenations (fc input at H+n, decoder input at Z+n)
     uint32_t nib;
     const bf16x4 hc = relu(mm(CB, wC1), bias(LC1, n), MC1, n, nib);
     *(bf16x4*)(HCAT + ioff(H + n, q)) = hc;
     *(bf16x4*)(DCAT + ioff(Z + n, q)) = hc;
-    arena4(L[LFC].xT, H + n, Bp, b0, q, hc);
-    arena4(L[LD0].xT, Z + n, Bp, b0, q, hc);
+    arena4(L[LFC].xT, L[LFC].Kp, H + n, b0, q, hc);
+    arena4(L[LD0].xT, L[LD0].Kp, Z + n, b0, q, hc);
     const bf16x4 he = relu(mm(A0, wE1), bias(LE1, n), ME1, n, nib);
     *(bf16x4*)(A1 + ioff(n, q)) = he;
-    arena4(L[LE2].xT, n, Bp, b0, q, he);
+    arena4(L[LE2].xT, L[LE2].Kp, n, b0, q, he);
   }
+  wload(wE3, Wf(LE3), H, wave);
+  if (wave == 0) wload(wFC, Wf(LFC), 2 * H, 0);  // fc_mu ‖ fc_logvar: one real n-tile
   lbar();
   stamp();
-  bf16x8 wFC[8];  // fc_mu ‖ fc_logvar: one real n-tile (every wave loads it; wave 0 computes)
-  wload(wFC, Wf(LFC), 2 * H, 0);
-  {  // E2
+  {  // S2: E2
     uint32_t nib;
     const bf16x4 he = relu(mm(A1, wE2), bias(LE2, n), ME2, n, nib);
     *(bf16x4*)(A0 + ioff(n, q)) = he;
-    arena4(L[LE3].xT, n, Bp, b0, q, he);
+    arena4(L[LE3].xT, L[LE3].Kp, n, b0, q, he);
   }
+  wload(wD0, Wf(LD0), 160, wave);
+  wload(wD1, Wf(LD1), H, wave);
   lbar();
   stamp();
-  bf16x8 wD0[5];
-  wload(wD0, Wf(LD0), 160, wave);
-  {  // E3 → h_traj
+  {  // S3: E3 → h_traj
     uint32_t nib;
     const bf16x4 he = relu(mm(A0, wE3), bias(LE3, n), ME3, n, nib);
     *(bf16x4*)(HCAT + ioff(n, q)) = he;
-    arena4(L[LFC].xT, n, Bp, b0, q, he);
+    arena4(L[LFC].xT, L[LFC].Kp, n, b0, q, he);
   }
+  wload(wD2, Wf(LD2), H, wave);
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+    if (wave + NW * g < NG3) wload(wD3[g], Wf(LD3), H, wave + NW * g);
   lbar();
   stamp();
-  bf16x8 wD1[4];
-  wload(wD1, Wf(LD1), H, wave);
-  if (wave == 0) {  // fc_mu ‖ fc_logvar (:195-196) + reparameterize (:199-206) + KL terms (:243)
+  if (wave == 0) {  // S4: fc_mu ‖ fc_logvar (:195-196) + reparameterize (:199-206) + KL terms (:243)
     const f32x4 acc = mm(HCAT, wFC);
     f32x4 y, lv;
     const float b = bias(LFC, n16);
@@ -338,43 +378,41 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
       *(f32x4*)(STDV + j * R + 4 * q) = sd;
       const bf16x4 zh = to_bf4(z);
       *(bf16x4*)(DCAT + ioff(j, q)) = zh;
-      arena4(L[LD0].xT, j, Bp, b0, q, zh);
+      arena4(L[LD0].xT, L[LD0].Kp, j, b0, q, zh);
     }
   }
+#pragma unroll
+  for (int g = 2; g < G3; ++g)
+    if (wave + NW * g < NG3) wload(wD3[g], Wf(LD3), H, wave + NW * g);
   lbar();
   stamp();
-  bf16x8 wD2[4];
-  wload(wD2, Wf(LD2), H, wave);
-  {  // D0
+  {  // S5: D0
     uint32_t nib;
     const bf16x4 h = relu(mm(DCAT, wD0), bias(LD0, n), MD0, n, nib);
     *(bf16x4*)(A0 + ioff(n, q)) = h;
-    arena4(L[LD1].xT, n, Bp, b0, q, h);
+    arena4(L[LD1].xT, L[LD1].Kp, n, b0, q, h);
   }
+  wload_part<0, NKI / 2>(wD3b, Wb(LD3), Ip, wave);
   lbar();
   stamp();
-  bf16x8 wD3[G3][4];  // D3's n-tiles of this wave (clamped: waves with fewer reload their last)
-#pragma unroll
-  for (int g = 0; g < G3; ++g) wload(wD3[g], Wf(LD3), H, min(wave + NW * g, NG3 - 1));
-  {  // D1
+  {  // S6: D1
     uint32_t nib;
     const bf16x4 h = relu(mm(A0, wD1), bias(LD1, n), MD1, n, nib);
     *(bf16x4*)(A1 + ioff(n, q)) = h;
-    arena4(L[LD2].xT, n, Bp, b0, q, h);
+    arena4(L[LD2].xT, L[LD2].Kp, n, b0, q, h);
   }
+  wload_part<NKI / 2, NKI>(wD3b, Wb(LD3), Ip, wave);
   lbar();
   stamp();
-  {  // D2
+  {  // S7: D2
     uint32_t nib;
     const bf16x4 h = relu(mm(A1, wD2), bias(LD2, n), MD2, n, nib);
     *(bf16x4*)(A0 + ioff(n, q)) = h;
-    arena4(L[LD3].xT, n, Bp, b0, q, h);
+    arena4(L[LD3].xT, L[LD3].Kp, n, b0, q, h);
   }
   lbar();
   stamp();
-  bf16x8 wD3b[NKI];
-  wload(wD3b, Wb(LD3), Ip, wave);
-  {  // D3 + conditional_vae_loss (:229-268) + dL/drecon, written over x_rel in place
+  {  // S8: D3 + conditional_vae_loss (:229-268) + dL/drecon, over x_rel in place
     const float inv_D = 1.f / (float)D;
 #pragma unroll
     for (int g = 0; g < G3; ++g) {
@@ -415,79 +453,82 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
       }
     }
   }
+  wload(wD2b, Wb(LD2), H, wave);
+  wload(wD1b, Wb(LD1), H, wave);
+  stamp();
   lbar();
+  stamp();
   // time-monotonicity term relu(r_s − r_{s+1}) (:261-262, ReLU'(0) = 0) into the time channel of
-  // dL/drecon, then the feature-major arena copy gT(D3) of the whole tile
+  // dL/drecon (one task per (timestep, row quad): its GL image entry and its arena row), and the
+  // feature-major arena copy gT(D3) of every other feature (the time channel is the fix task's)
   {
     constexpr int UF = (Ip * 4 + NT - 1) / NT;
     const float inv_D = 1.f / (float)D, wt = a.w_time * inv_BS1;
     void* const gd3 = L[LD3].gT;
+    for (int e = tid; e < S * 4; e += NT) {
+      const int s = e >> 2, qq = e & 3, f = s * D;
+      f32x4 gv = *(const f32x4*)(GD0 + s * R + 4 * qq);  // fp32: dL/drecon is rounded once
+      if (use_time) {
+        const f32x4 rs = *(const f32x4*)(RCH0 + s * R + 4 * qq);
+        const f32x4 rn = *(const f32x4*)(RCH0 + min(s + 1, S - 1) * R + 4 * qq);
+        const f32x4 rp = *(const f32x4*)(RCH0 + max(s - 1, 0) * R + 4 * qq);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bool live = 4 * qq + i < nrows;
+          const float u1 = rs[i] - rn[i], u0 = rp[i] - rs[i];  // 0 at the sequence ends
+          if (live && u1 > 0.f) {
+            gv[i] += wt;
+            s_relu += u1;
+          }
+          if (live && u0 > 0.f) gv[i] -= wt;
+        }
+      }
+      const bf16x4 h = to_bf4(gv);
+      *(bf16x4*)(XIN + ioff(f, qq)) = h;
+      arena4(gd3, L[LD3].Np, f, b0, qq, h);
+    }
 #pragma unroll
     for (int u = 0; u < UF; ++u) {
       const int e = u * NT + tid;
-      if (e < Ip * 4) {
-        const int f = e >> 2, qq = e & 3;
-        bf16x4 h = *(const bf16x4*)(XIN + ioff(f, qq));
-        const int s = fdiv(f, inv_D);
-        if (use_time && f < I && f == s * D) {
-          f32x4 gv = *(const f32x4*)(GD0 + s * R + 4 * qq);  // fp32: dL/drecon is rounded once
-          const f32x4 rs = *(const f32x4*)(RCH0 + s * R + 4 * qq);
-          const f32x4 rn = s < S - 1 ? *(const f32x4*)(RCH0 + (s + 1) * R + 4 * qq) : rs;
-          const f32x4 rp = s > 0 ? *(const f32x4*)(RCH0 + (s - 1) * R + 4 * qq) : rs;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            if (4 * qq + i >= nrows) continue;
-            const float u1 = rs[i] - rn[i], u0 = rp[i] - rs[i];
-            if (u1 > 0.f) {
-              gv[i] += wt;
-              s_relu += u1;
-            }
-            if (u0 > 0.f) gv[i] -= wt;
-          }
-          h = to_bf4(gv);
-          *(bf16x4*)(XIN + ioff(f, qq)) = h;
-        }
-        arena4(gd3, f, Bp, b0, qq, h);
-      }
+      const int f = e >> 2, qq = e & 3;
+      if (e < Ip * 4 && (f >= I || f != fdiv(f, inv_D) * D))
+        arena4(gd3, L[LD3].Np, f, b0, qq, *(const bf16x4*)(XIN + ioff(f, qq)));
     }
   }
+  wload(wD0b[0], Wb(LD0), H, wave);
+  if (wave < 2) wload(wD0b[1], Wb(LD0), H, wave + NW);  // decoder layer 0 input: 160 (136 real) features
+  wload(wFCb[0], Wb(LFC), 32, wave);                    // fc input features 0..255: h_traj, h_c
+  wload(wFCb[1], Wb(LFC), 32, wave + NW);
   lbar();
   stamp();
 
   // ================================================================ backward
-  bf16x8 wD2b[4], wD1b[4];
-  wload(wD2b, Wb(LD2), H, wave);
-  wload(wD1b, Wb(LD1), H, wave);
-  {  // D3ᵀ: dL/d h_D2 = GL · W_D3, ReLU mask of D2
+  {  // S9: D3ᵀ: dL/d h_D2 = GL · W_D3, ReLU mask of D2
     const bf16x4 h = masked(mm(XIN, wD3b), MD2, n);
     *(bf16x4*)(A1 + ioff(n, q)) = h;
-    arena4(L[LD2].gT, n, Bp, b0, q, h);
+    arena4(L[LD2].gT, L[LD2].Np, n, b0, q, h);
   }
+  wload(wE3b, Wb(LE3), H, wave);
+  wload(wE2b, Wb(LE2), H, wave);
   lbar();
   stamp();
-  bf16x8 wD0b[2][4];  // decoder layer 0's input has 160 (136 real) features: n-tiles wave, wave + 8
-  wload(wD0b[0], Wb(LD0), H, wave);
-  wload(wD0b[1], Wb(LD0), H, min(wave + NW, 9));
-  {
+  {  // S10: D2ᵀ
     const bf16x4 h = masked(mm(A1, wD2b), MD1, n);
     *(bf16x4*)(A0 + ioff(n, q)) = h;
-    arena4(L[LD1].gT, n, Bp, b0, q, h);
+    arena4(L[LD1].gT, L[LD1].Np, n, b0, q, h);
   }
+  wload(wE1b, Wb(LE1), H, wave);
+  wload(wC1b, Wb(LC1), H, wave);
   lbar();
   stamp();
-  bf16x8 wFCb[2][1];  // fc input features 0..255: n-tiles wave (h_traj) and wave + 8 (h_c)
-  wload(wFCb[0], Wb(LFC), 32, wave);
-  wload(wFCb[1], Wb(LFC), 32, wave + NW);
-  {
+  {  // S11: D1ᵀ
     const bf16x4 h = masked(mm(A0, wD1b), MD0, n);
     *(bf16x4*)(A1 + ioff(n, q)) = h;
-    arena4(L[LD0].gT, n, Bp, b0, q, h);
+    arena4(L[LD0].gT, L[LD0].Np, n, b0, q, h);
   }
   lbar();
   stamp();
-  bf16x8 wE3b[4];
-  wload(wE3b, Wb(LE3), H, wave);
-  {  // D0ᵀ: [dz ‖ dh_c(decoder share)]; dz → KL/reparameterisation backward → G_fc
+  {  // S12: D0ᵀ: [dz ‖ dh_c(decoder share)]; dz → KL/reparameterisation backward → G_fc
 #pragma unroll
     for (int h2 = 0; h2 < 2; ++h2) {
       const int t = wave + NW * h2;
@@ -508,8 +549,8 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
           const bf16x4 hm = to_bf4(gm), hl = to_bf4(gl);
           *(bf16x4*)(GFC + ioff(j, q)) = hm;
           *(bf16x4*)(GFC + ioff(Z + j, q)) = hl;
-          arena4(L[LFC].gT, j, Bp, b0, q, hm);
-          arena4(L[LFC].gT, Z + j, Bp, b0, q, hl);
+          arena4(L[LFC].gT, L[LFC].Np, j, b0, q, hm);
+          arena4(L[LFC].gT, L[LFC].Np, Z + j, b0, q, hl);
         } else if (f < Z + H) {
           *(f32x4*)(DHC2 + (f - Z) * R + 4 * q) = acc;
         }
@@ -518,42 +559,37 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
   }
   lbar();
   stamp();
-  bf16x8 wE2b[4];
-  wload(wE2b, Wb(LE2), H, wave);
-  {  // fcᵀ: dh = G_fc · W_fc → h_traj gradient (mask E3) and h_c gradient (+ decoder share, mask C1)
+  {  // S13: fcᵀ: dh = G_fc · W_fc → h_traj gradient (mask E3) and h_c gradient (+ decoder share, mask C1)
     const bf16x4 ht = masked(mm(GFC, wFCb[0]), ME3, n);
     *(bf16x4*)(A0 + ioff(n, q)) = ht;
-    arena4(L[LE3].gT, n, Bp, b0, q, ht);
+    arena4(L[LE3].gT, L[LE3].Np, n, b0, q, ht);
     f32x4 acc = mm(GFC, wFCb[1]);
     const f32x4 d2 = *(const f32x4*)(DHC2 + n * R + 4 * q);
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i] += d2[i];
     const bf16x4 hc = masked(acc, MC1, n);
     *(bf16x4*)(CB + ioff(n, q)) = hc;
-    arena4(L[LC1].gT, n, Bp, b0, q, hc);
+    arena4(L[LC1].gT, L[LC1].Np, n, b0, q, hc);
   }
   lbar();
   stamp();
-  bf16x8 wE1b[4], wC1b[4];
-  wload(wE1b, Wb(LE1), H, wave);
-  wload(wC1b, Wb(LC1), H, wave);
-  {  // E3ᵀ
+  {  // S14: E3ᵀ
     const bf16x4 h = masked(mm(A0, wE3b), ME2, n);
     *(bf16x4*)(A1 + ioff(n, q)) = h;
-    arena4(L[LE2].gT, n, Bp, b0, q, h);
+    arena4(L[LE2].gT, L[LE2].Np, n, b0, q, h);
   }
   lbar();
   stamp();
-  {  // E2ᵀ
+  {  // S15: E2ᵀ
     const bf16x4 h = masked(mm(A1, wE2b), ME1, n);
     *(bf16x4*)(A0 + ioff(n, q)) = h;
-    arena4(L[LE1].gT, n, Bp, b0, q, h);
+    arena4(L[LE1].gT, L[LE1].Np, n, b0, q, h);
   }
   lbar();
   stamp();
-  {  // E1ᵀ ‖ C1ᵀ: the last two gradients only feed the dW kernel
-    arena4(L[LE0].gT, n, Bp, b0, q, masked(mm(A0, wE1b), ME0, n));
-    arena4(L[LC0].gT, n, Bp, b0, q, masked(mm(CB, wC1b), MC0, n));
+  {  // S16: E1ᵀ ‖ C1ᵀ: the last two gradients only feed the dW kernel
+    arena4(L[LE0].gT, L[LE0].Np, n, b0, q, masked(mm(A0, wE1b), ME0, n));
+    arena4(L[LC0].gT, L[LC0].Np, n, b0, q, masked(mm(CB, wC1b), MC0, n));
   }
 
   // ---- loss partial sums (deterministic order)

@@ -128,6 +128,7 @@ struct StepSpec {
   int goff1, goff2;  // arena row offsets of g1 / g2
   int concat;        // skip columns >= N (destination is part of a concatenation)
   int hc_out;        // inference: also write h_c (fp32) to RowArgs::hc_out
+  int kf1, kf2;      // feature rows of the g1 / g2 arena matrices (aoff)
 };
 
 // ... and as the kernel reads it: 64 B, copied into LDS by the prologue and read back every step
@@ -142,7 +143,7 @@ struct StepDesc {
   int code;          // xbuf | epi<<4 | (dst1+1)<<8 | (dst2+1)<<12 | concat<<16 | hc_out<<17 | (mask_out+1)<<20 | (mask_in+1)<<26
   int off1, off2;
   int goff;          // goff1 | goff2 << 16
-  int pad_[2];
+  int kf1, kf2;      // feature rows of the g1 / g2 arena matrices
 };
 static_assert(sizeof(StepDesc) == 64, "StepDesc is 4 x 16 B");
 
@@ -154,6 +155,7 @@ inline StepDesc encode_step(const StepSpec& s) {
            (s.hc_out << 17) | ((s.mask_out + 1) << 20) | ((s.mask_in + 1) << 26);
   d.off1 = s.off1; d.off2 = s.off2;
   d.goff = s.goff1 | (s.goff2 << 16);
+  d.kf1 = s.kf1; d.kf2 = s.kf2;
   return d;
 }
 
@@ -434,8 +436,9 @@ __device__ __forceinline__ uint32_t pack_bf16(float a, float b) {
   h[1] = (__bf16)b;
   return __builtin_bit_cast(uint32_t, h);
 }
-// base = arena row of feature f0 (+ b0); row = this lane's tile row (row & 3 == lane & 3)
-__device__ __forceinline__ void put4Tq(__bf16* base, int Bp, int row, f32x4 y) {
+// arena matrix mat (Kf feature rows), features f0..f0+3; brow = this lane's batch row
+// (brow & 3 == lane & 3)
+__device__ __forceinline__ void put4Tq(__bf16* mat, int Kf, int f0, int brow, f32x4 y) {
   if (CVAE_DIAG_NOSTORE) return;
   const int lane = threadIdx.x & 63;
   const bool b1 = lane & 1, b2 = lane & 2;
@@ -449,9 +452,9 @@ __device__ __forceinline__ void put4Tq(__bf16* base, int Bp, int row, f32x4 y) {
   const uint32_t Q0 = b1 ? __builtin_amdgcn_perm(D0, R2, 0x07060100u) : __builtin_amdgcn_perm(R2, D0, 0x05040100u);
   const uint32_t Q1 = b1 ? __builtin_amdgcn_perm(D1, R2, 0x07060302u) : __builtin_amdgcn_perm(R2, D1, 0x07060100u);
   typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-  gst<u32x2>(base + (size_t)(lane & 3) * Bp + (row & ~3), u32x2{Q0, Q1});
+  gst<u32x2>(mat + aoff(f0 + (lane & 3), brow & ~3, Kf), u32x2{Q0, Q1});
 }
-__device__ __forceinline__ void put4Tq(float* base, int Bp, int row, f32x4 y) {
+__device__ __forceinline__ void put4Tq(float* mat, int Kf, int f0, int brow, f32x4 y) {
   if (CVAE_DIAG_NOSTORE) return;
   const int lane = threadIdx.x & 63;
   const bool b1 = lane & 1, b2 = lane & 2;
@@ -464,7 +467,7 @@ __device__ __forceinline__ void put4Tq(float* base, int Bp, int row, f32x4 y) {
   // distance 1: even lanes send (A1, A3), odd lanes (A0, A2)
   const uint32_t Rc = dpp_xor1(u(b1 ? A0 : A1)), Rd = dpp_xor1(u(b1 ? A2 : A3));
   const f32x4 q = b1 ? f32x4{f(Rc), A1, f(Rd), A3} : f32x4{A0, f(Rc), A2, f(Rd)};
-  gst<f32x4>(base + (size_t)(lane & 3) * Bp + (row & ~3), q);
+  gst<f32x4>(mat + aoff(f0 + (lane & 3), brow & ~3, Kf), q);
 }
 
 // the 4 ReLU bits of features f0..f0+3 (f0 % 4 == 0) of one row: one byte per 4-feature group
@@ -557,15 +560,25 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
     const float inv_VPR = 1.f / (float)VPR, inv_Dd = 1.f / (float)D;
     const int last = max(a.batch - 1, 0);
     V xv[U], x0[U];
+    int64_t gr[U];  // source row per task; rows past the batch re-read a valid row (zeroed below)
+    int cc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int v = min(u * RC_THREADS + tid, NV - 1);
+      const int w = v >> 2, rq = fdiv(w, inv_VPR), c = w - rq * VPR, row = 4 * rq + (v & 3);
+      gr[u] = min(b0 + row, last);
+      cc[u] = c;
+    }
+    if (a.idx) {  // all idx loads in flight together, then the x loads
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (u * RC_THREADS < NV) gr[u] = gld<int64_t>(a.idx + gr[u]);
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (u * RC_THREADS < NV) {  // wave-uniform
-        const int v = min(u * RC_THREADS + tid, NV - 1);
-        const int w = v >> 2, rq = fdiv(w, inv_VPR), c = w - rq * VPR, row = 4 * rq + (v & 3);
-        const int rr = min(b0 + row, last);  // rows past the batch re-read a valid row (zeroed below)
-        const int64_t g = a.idx ? gld<int64_t>(a.idx + rr) : (int64_t)rr;
-        xv[u] = gld<V>(xg + g * I + c * EPL);
-        x0[u] = gld<V>(xg + g * I);
+        xv[u] = gld<V>(xg + gr[u] * I + cc[u] * EPL);
+        x0[u] = gld<V>(xg + gr[u] * I);
       }
     }
     setup_lds();  // overlaps the loads
@@ -599,7 +612,7 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
         if (TRAIN) {
 #pragma unroll
           for (int e = 0; e < EPL; e += 4)
-            put4Tq(xe0 + (size_t)(f0 + e) * Bp + b0, Bp, row, f32x4{q[e], q[e + 1], q[e + 2], q[e + 3]});
+            put4Tq(xe0, net.L[lE(net, 0)].Kp, f0 + e, b0 + row, f32x4{q[e], q[e + 1], q[e + 2], q[e + 3]});
         }
         if (c == 0) {  // quad-uniform: the condition input of this row (and its arena copy)
 #pragma unroll
@@ -609,7 +622,7 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
             for (int e = 0; e < EPL; ++e) cv[e] = to_t<T>(k + e == 0 ? s0 : k + e == 1 ? s1 : 0.f);
             *(V*)(Cin + row * P.scin + k) = cv;
           }
-          if (TRAIN) put4Tq(xc0 + b0, Bp, row, f32x4{to_f(to_t<T>(s0)), to_f(to_t<T>(s1)), 0.f, 0.f});
+          if (TRAIN) put4Tq(xc0, net.L[lC0(net)].Kp, 0, b0 + row, f32x4{to_f(to_t<T>(s0)), to_f(to_t<T>(s1)), 0.f, 0.f});
         }
       }
     }
@@ -672,18 +685,18 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
   // slow path only: feature-major copy of the input tiles for the weight-gradient kernel (one
   // 4-row × 1-column quad per task → one 8-B / 16-B store; the arena pads stay zero from creation)
   if (TRAIN && !fast && !CVAE_DIAG_NOSTORE) {
-    auto copy_T = [&](const T* src, int ld, int ncols, T* dst) {
+    auto copy_T = [&](const T* src, int ld, int ncols, T* dst, int Kf) {
       constexpr int RQ = R / 4;
       for (int t = tid; t < ncols * RQ; t += RC_THREADS) {
         const int c = t / RQ, q = t - c * RQ;
         f32x4 v;
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = to_f(src[(4 * q + i) * ld + c]);
-        gstore4(dst + (size_t)c * Bp + b0 + 4 * q, v);
+        gstore4(dst + aoff(c, b0 + 4 * q, Kf), v);
       }
     };
-    copy_T(Cin, P.scin, 2, (T*)net.L[lC0(net)].xT);
-    copy_T(Xin, P.sx, I, (T*)net.L[lE(net, 0)].xT);
+    copy_T(Cin, P.scin, 2, (T*)net.L[lC0(net)].xT, net.L[lC0(net)].Kp);
+    copy_T(Xin, P.sx, I, (T*)net.L[lE(net, 0)].xT, net.L[lE(net, 0)].Kp);
   }
 
   const float Bf = (float)a.batch;
@@ -717,6 +730,7 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
     const uint32_t code = sgpr(q2.z);
     const int off1 = (int)sgpr(q2.w), off2 = (int)sgpr(q3.x);
     const uint32_t goff = sgpr(q3.y);
+    const int kf1 = (int)sgpr(q3.z), kf2 = (int)sgpr(q3.w);
     const int goff1 = (int)(goff & 0xFFFF), goff2 = (int)(goff >> 16);
     const T* const nW = has_next ? (const T*)sptr(n0.x, n0.y) : (const T*)nullptr;
     const int nKp = (int)sgpr(n1.z), nNp = (int)sgpr(n1.w);
@@ -762,8 +776,8 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
       if (concat && f0 >= N) return;  // part of a concatenation: never write its pads
       if (!CVAE_DIAG_NOLDSW) put4(d1 + row * ld1 + off1 + f0, y);
       if (d2 && !CVAE_DIAG_NOLDSW) put4(d2 + row * ld2 + off2 + f0, y);
-      if (g1) put4Tq(g1 + (size_t)(goff1 + f0) * Bp + b0, Bp, row, y);
-      if (g2) put4Tq(g2 + (size_t)(goff2 + f0) * Bp + b0, Bp, row, y);
+      if (g1) put4Tq(g1, kf1, goff1 + f0, b0 + row, y);
+      if (g2) put4Tq(g2, kf2, goff2 + f0, b0 + row, y);
       if (!TRAIN && hc_o && a.hc_out && live && f0 < N) gst<f32x4>(a.hc_out + (size_t)(b0 + row) * H + f0, y);
     };
     // backward: mask with the producer's ReLU bits
@@ -774,7 +788,7 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
 #pragma unroll
       for (int i = 0; i < 4; ++i) y[i] = (nib >> i) & 1u ? v[i] : 0.f;
       if (d1) put4(d1 + row * ld1 + f0, y);
-      put4Tq(g1 + (size_t)f0 * Bp + b0, Bp, row, y);
+      put4Tq(g1, kf1, f0, b0 + row, y);
     };
     // mu ‖ logvar, fp32 in LDS
     auto epi_fc = [&](int row, int f0, f32x4 v, f32x4 b4) {
@@ -801,7 +815,7 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
       // (same lane, same elements), so no other reader is affected
       const f32x4 xr = get4(Xin + row * P.sx + f0);
       int s = fdiv(f0, inv_D), d = f0 - s * D;
-      T* gcol = g1 + (size_t)f0 * Bp + b0 + row;
+
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         float gi = 0.f;
@@ -825,7 +839,7 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
         }
         y[i] = gi;
         // the time channel (d == 0) is finished by the fix-up pass once its neighbours exist
-        if (!CVAE_DIAG_NOSTORE && (d != 0 || f0 + i >= I)) gst<T>(gcol + (size_t)i * Bp, to_t<T>(gi));
+        if (!CVAE_DIAG_NOSTORE && (d != 0 || f0 + i >= I)) gst<T>(g1 + aoff(f0 + i, b0 + row, kf1), to_t<T>(gi));
         if (++d == D) { d = 0; ++s; }
       }
       put4(GL + row * P.sx + f0, y);  // d == 0 entries are overwritten by the fix-up pass
@@ -852,7 +866,7 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
 #pragma unroll
         for (int i = 0; i < 4; ++i) y[i] = (nib >> i) & 1u ? v[i] : 0.f;
         put4(P1b + row * P.sp + f0, y);
-        put4Tq(g1 + (size_t)f0 * Bp + b0, Bp, row, y);
+        put4Tq(g1, kf1, f0, b0 + row, y);
       } else if (f0 < 2 * H) {
         const int c = f0 - H;
         const uint32_t nib = mask4(mkC1, mw, row, c);
@@ -860,7 +874,7 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
 #pragma unroll
         for (int i = 0; i < 4; ++i) y[i] = (nib >> i) & 1u ? v[i] + dh2[i] : 0.f;
         put4(Q + row * P.shc + c, y);
-        put4Tq(g2 + (size_t)c * Bp + b0, Bp, row, y);
+        put4Tq(g2, kf2, c, b0 + row, y);
       }
     };
     switch (kind) {
@@ -895,7 +909,7 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
         Eps[r * Z + j] = ep;
         Std[r * Z + j] = sd;
         Dec[r * P.sdec + j] = to_t<T>(z);
-        if (TRAIN && !CVAE_DIAG_NOSTORE) gst<T>(xd0 + (size_t)j * Bp + b0 + r, to_t<T>(z));
+        if (TRAIN && !CVAE_DIAG_NOSTORE) gst<T>(xd0 + aoff(j, b0 + r, net.L[lD(net, 0)].Kp), to_t<T>(z));
       }
       lds_barrier();
     } else if (kind == E_LOSS) {
@@ -921,7 +935,7 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
           }
         }
         GL[r * P.sx + s * D] = to_t<T>(g);
-        if (!CVAE_DIAG_NOSTORE) gst<T>(gl + (size_t)(s * D) * Bp + b0 + r, to_t<T>(g));
+        if (!CVAE_DIAG_NOSTORE) gst<T>(gl + aoff(s * D, b0 + r, kf1), to_t<T>(g));
       }
       lds_barrier();
     } else if (kind == E_D0B) {
@@ -941,7 +955,7 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
           }
         }
         P0b[r * P.sp + c] = to_t<T>(g);
-        if (!CVAE_DIAG_NOSTORE) gst<T>(gfc + (size_t)c * Bp + b0 + r, to_t<T>(g));
+        if (!CVAE_DIAG_NOSTORE) gst<T>(gfc + aoff(c, b0 + r, net.L[lFC(net)].Np), to_t<T>(g));
       }
       // pads of the two gradient targets of the fc backward must read as zero
       if (net.Hp > H) {

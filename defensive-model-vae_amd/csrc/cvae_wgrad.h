@@ -85,46 +85,62 @@ __device__ __forceinline__ float adam_math(float p, float g, float& m, float& v,
 // LDS image of one 32×32 tile: fp32 rows padded to 36 floats (16-B aligned rows)
 constexpr int WT_LD = 36;
 
-// Weights (o, i..i+3) of layer L (padded coordinates) with gradient g4: write the gradient
-// (GRAD), apply Adam (ADAM) or read (PACK) the fp32 master.  Returns the values for the operand
-// copies (0 in the padding).  All loads are issued before the first store.
+// The fp32 master state of weights (o, i..i+3) of layer L (padded coordinates), loaded before the
+// gradient exists (it does not depend on it) so the epilogue is arithmetic and stores only.
+struct Pre4 {
+  float p[4], m[4], v[4];
+  int64_t base;
+  int nv;  // valid elements (0: padding)
+};
 template <int MODE>
-__device__ __forceinline__ f32x4 update4(const LayerDev& L, int o, int i, f32x4 g4, const AdamArgs& a) {
-  f32x4 w = {0.f, 0.f, 0.f, 0.f};
-  if (o >= L.N || i >= L.K) return w;
+__device__ __forceinline__ Pre4 load4(const LayerDev& L, int o, int i, const AdamArgs& a) {
+  Pre4 s;
+  s.nv = 0;
+  s.base = 0;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) s.p[c] = s.m[c] = s.v[c] = 0.f;
+  if (o >= L.N || i >= L.K) return s;
   const int seg = (L.nseg == 2 && o >= L.seg_rows0) ? 1 : 0;
-  const int orow = seg ? o - L.seg_rows0 : o;
-  const int64_t base = L.pw[seg] + (int64_t)orow * L.K + i;
-  const int nv = min(4, L.K - i);
+  s.base = L.pw[seg] + (int64_t)(seg ? o - L.seg_rows0 : o) * L.K + i;
+  s.nv = min(4, L.K - i);
+  if (MODE == PM_GRAD) return s;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    if (c < s.nv) {
+      s.p[c] = a.params[s.base + c];
+      if (MODE == PM_ADAM) {
+        s.m[c] = a.m[s.base + c];
+        s.v[c] = a.v[s.base + c];
+      }
+    }
+  }
+  return s;
+}
+// write the gradient (GRAD), apply Adam (ADAM) or keep (PACK); returns the values for the operand
+// copies (0 in the padding)
+template <int MODE>
+__device__ __forceinline__ f32x4 apply4(Pre4 s, f32x4 g4, const AdamArgs& a) {
+  f32x4 w = {0.f, 0.f, 0.f, 0.f};
   if (MODE == PM_GRAD) {
 #pragma unroll
     for (int c = 0; c < 4; ++c)
-      if (c < nv) a.grads[base + c] = g4[c];
+      if (c < s.nv) a.grads[s.base + c] = g4[c];
     return w;
-  }
-  float p[4], m[4], v[4];
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    p[c] = c < nv ? a.params[base + c] : 0.f;
-    if (MODE == PM_ADAM) {
-      m[c] = c < nv ? a.m[base + c] : 0.f;
-      v[c] = c < nv ? a.v[base + c] : 0.f;
-    }
   }
   if (MODE == PM_ADAM) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) p[c] = adam_math(p[c], g4[c], m[c], v[c], a);
+    for (int c = 0; c < 4; ++c) s.p[c] = adam_math(s.p[c], g4[c], s.m[c], s.v[c], a);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      if (c < nv) {
-        a.params[base + c] = p[c];
-        a.m[base + c] = m[c];
-        a.v[base + c] = v[c];
+      if (c < s.nv) {
+        a.params[s.base + c] = s.p[c];
+        a.m[s.base + c] = s.m[c];
+        a.v[s.base + c] = s.v[c];
       }
     }
   }
 #pragma unroll
-  for (int c = 0; c < 4; ++c) w[c] = c < nv ? p[c] : 0.f;
+  for (int c = 0; c < 4; ++c) w[c] = c < s.nv ? s.p[c] : 0.f;
   return w;
 }
 
@@ -155,14 +171,15 @@ __device__ __forceinline__ void apply_bias(const LayerDev& L, int o, float g, co
 // (n-tile t, chunk kc) lane ln holds elements (16t + (ln & 15), KC·kc + frag_k(ln >> 4, e)) at
 // ((t·Kp/KC + kc)·64 + ln)·EPL (frag_off), so a tile is 2 n-tiles × 32/KC chunks of contiguous
 // 1-KB blocks per copy.
-template <typename T>
+template <typename T, int NTHR>
 __device__ __forceinline__ void store_operands(const LayerDev& L, int o0, int i0, const float* wt) {
   using V = typename Op<T>::V;
   constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC, CPT = 32 / KC;
   constexpr int PER_COPY = 2 * CPT * 64;
 #pragma unroll
-  for (int j0 = 0; j0 < 2 * PER_COPY; j0 += CVAE_THREADS) {
+  for (int j0 = 0; j0 < 2 * PER_COPY; j0 += NTHR) {
     const int j = j0 + (int)threadIdx.x;
+    if (NTHR > 2 * PER_COPY && j >= 2 * PER_COPY) break;
     const bool wb = j >= PER_COPY;  // wave-uniform: PER_COPY is a multiple of 64
     const int jj = wb ? j - PER_COPY : j;
     const int blk = jj >> 6, ln = jj & 63;
@@ -185,19 +202,21 @@ __device__ __forceinline__ void store_operands(const LayerDev& L, int o0, int i0
   }
 }
 
-// Shared by wgrad_kernel and param_kernel: thread (o = tid/8, i = 4·(tid%8)) of the tile owns the
-// gradient g4 of weights (o0+o, i0+i..+3); threads < 32 own bias o0+tid (tiles with i0 == 0).
-// wt: an LDS tile image (32 × WT_LD floats) the caller no longer needs.
-template <typename T, int MODE>
-__device__ __forceinline__ void tile_epilogue(const LayerDev& L, int o0, int i0, f32x4 g4, float db,
-                                              const AdamArgs& aa, float* wt) {
+// Shared by wgrad_kernel and param_kernel: thread (o = tid/8, i = 4·(tid%8)) < 256 of the tile
+// owns the gradient g4 of weights (o0+o, i0+i..+3) (state st from load4); threads < 32 own bias
+// o0+tid (tiles with i0 == 0).  wt: an LDS tile image (32 × WT_LD floats) the caller no longer
+// needs.  Every thread of the block calls it (barrier inside).
+template <typename T, int MODE, int NTHR>
+__device__ __forceinline__ void tile_epilogue(const LayerDev& L, int o0, int i0, const Pre4& st, f32x4 g4,
+                                              float db, const AdamArgs& aa, float* wt) {
   const int tid = threadIdx.x, o = tid >> 3, i4 = (tid & 7) * 4;
-  const f32x4 w = update4<MODE>(L, o0 + o, i0 + i4, g4, aa);
+  f32x4 w = {0.f, 0.f, 0.f, 0.f};
+  if (tid < 256) w = apply4<MODE>(st, g4, aa);
   if (i0 == 0 && tid < 32) apply_bias<MODE>(L, o0 + tid, db, aa);
   if (MODE == PM_GRAD || (CVAE_DIAG_NOWPACK && MODE == PM_ADAM)) return;
-  *(f32x4*)(wt + o * WT_LD + i4) = w;
+  if (tid < 256) *(f32x4*)(wt + o * WT_LD + i4) = w;
   __syncthreads();
-  store_operands<T>(L, o0, i0, wt);
+  store_operands<T, NTHR>(L, o0, i0, wt);
 }
 
 // called by one whole wave: lane-strided partial sums, then a fixed-order butterfly (deterministic)
@@ -221,13 +240,16 @@ __device__ void finish_loss(const LossArgs& l, int S, int D, int Z) {
   }
 }
 
+// 8 waves per tile: the batch (K) is cut into 8 wave slices whose loads are all in flight at once
+constexpr int WG_NW = 8, WG_THREADS = 64 * WG_NW;
+
 template <typename T, int MODE>
-__global__ __launch_bounds__(CVAE_THREADS) void wgrad_kernel(NetDev net, const TileDesc* __restrict__ tiles,
-                                                             int Bk, AdamArgs aa, LossArgs la) {
+__global__ __launch_bounds__(WG_THREADS) void wgrad_kernel(NetDev net, const TileDesc* __restrict__ tiles,
+                                                           int Bk, AdamArgs aa, LossArgs la) {
   using V = typename Op<T>::V;
   constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC;
-  __shared__ __attribute__((aligned(16))) float red[CVAE_NW * 32 * WT_LD];
-  __shared__ float dbp[CVAE_NW * 32];
+  __shared__ __attribute__((aligned(16))) float red[WG_NW * 32 * WT_LD];
+  __shared__ float dbp[WG_NW * 32];
   const TileDesc td = tiles[blockIdx.x];
   const LayerDev& L = net.L[td.layer];
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
@@ -236,36 +258,43 @@ __global__ __launch_bounds__(CVAE_THREADS) void wgrad_kernel(NetDev net, const T
   const T* G = (const T*)L.gT;
   const T* X = (const T*)L.xT;
   const bool bias_tile = td.i0 == 0;
+  const int o = tid >> 3, i4 = (tid & 7) * 4;
 
   WSTAMP(0);
-  if (blockIdx.x == 0 && tid < 64 && la.partials) finish_loss(la, net.S, net.D, net.Z);
-
   f32x4 acc[2][2];
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
     for (int n = 0; n < 2; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
   float gs[2] = {0.f, 0.f};  // bias partials: Σ of this lane's G fragment elements
+  // tile-major arena (aoff): this lane's 16-B pieces of rows o / i at batch offset kq of a chunk;
+  // one chunk of KC batch rows advances KC/16 row tiles = (KC/16)·Kf·16 elements
+  const int Kg = L.Np, Kx = L.Kp;
   const T* gp[2];
   const T* xp[2];
 #pragma unroll
-  for (int m = 0; m < 2; ++m) gp[m] = G + (size_t)(td.o0 + m * 16 + r16) * Bp + kq;
+  for (int m = 0; m < 2; ++m) gp[m] = G + aoff(td.o0 + m * 16 + r16, kq, Kg);
 #pragma unroll
-  for (int n = 0; n < 2; ++n) xp[n] = X + (size_t)(td.i0 + n * 16 + r16) * Bp + kq;
-  // this wave's chunks: c = wave + CVAE_NW*j; PF chunks of loads kept in flight
+  for (int n = 0; n < 2; ++n) xp[n] = X + aoff(td.i0 + n * 16 + r16, kq, Kx);
+  (void)Bp;
+  // this wave's chunks: c = wave + WG_NW*j; PF chunks of loads kept in flight
   const int nk = Bk / KC;
-  const int nmine = nk > wave ? (nk - wave + CVAE_NW - 1) / CVAE_NW : 0;
+  const int nmine = nk > wave ? (nk - wave + WG_NW - 1) / WG_NW : 0;
   constexpr int PF = 4;
   V ga[PF][2], xb[PF][2];
   auto load = [&](int u, int j) {  // unconditional, clamped to this wave's last chunk
-    const int c = (wave + CVAE_NW * min(j, nmine > 0 ? nmine - 1 : 0)) * KC;
+    const size_t ct = (size_t)(wave + WG_NW * min(j, nmine > 0 ? nmine - 1 : 0)) * (KC / 16) * 16;
 #pragma unroll
-    for (int m = 0; m < 2; ++m) ga[u][m] = gld<V>(gp[m] + c);
+    for (int m = 0; m < 2; ++m) ga[u][m] = gld<V>(gp[m] + ct * Kg);
 #pragma unroll
-    for (int n = 0; n < 2; ++n) xb[u][n] = gld<V>(xp[n] + c);
+    for (int n = 0; n < 2; ++n) xb[u][n] = gld<V>(xp[n] + ct * Kx);
   };
 #pragma unroll
   for (int u = 0; u < PF; ++u) load(u, u);
+  // the master state the epilogue updates (independent of the gradient) behind the operand loads
+  Pre4 st = {};
+  if (tid < 256) st = load4<MODE>(L, td.o0 + o, td.i0 + i4, aa);
+  if (blockIdx.x == 0 && wave == WG_NW - 1 && la.partials) finish_loss(la, net.S, net.D, net.Z);
   for (int j0 = 0; j0 < nmine; j0 += PF) {
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
@@ -282,7 +311,7 @@ __global__ __launch_bounds__(CVAE_THREADS) void wgrad_kernel(NetDev net, const T
             for (int e = 0; e < EPL; ++e) gs[m] += (float)ga[u][m][e];
         }
       }
-      load(u, j + PF);
+      if (j + PF < nmine) load(u, j + PF);
     }
   }
   WSTAMP(1);
@@ -303,17 +332,18 @@ __global__ __launch_bounds__(CVAE_THREADS) void wgrad_kernel(NetDev net, const T
   }
   __syncthreads();
   WSTAMP(2);
-  const int o = tid >> 3, i4 = (tid & 7) * 4;
   f32x4 g4 = {0.f, 0.f, 0.f, 0.f};
+  if (tid < 256) {
 #pragma unroll
-  for (int w = 0; w < CVAE_NW; ++w) g4 += *(const f32x4*)(red + w * 32 * WT_LD + o * WT_LD + i4);
+    for (int w = 0; w < WG_NW; ++w) g4 += *(const f32x4*)(red + w * 32 * WT_LD + o * WT_LD + i4);
+  }
   float db = 0.f;
   if (bias_tile && tid < 32) {
 #pragma unroll
-    for (int w = 0; w < CVAE_NW; ++w) db += dbp[w * 32 + tid];
+    for (int w = 0; w < WG_NW; ++w) db += dbp[w * 32 + tid];
   }
   __syncthreads();  // red becomes the image of the new weights
-  tile_epilogue<T, MODE>(L, td.o0, td.i0, g4, db, aa, red);
+  tile_epilogue<T, MODE, WG_THREADS>(L, td.o0, td.i0, st, g4, db, aa, red);
 #if CVAE_DIAG_STAMPS
   __syncthreads();
   WSTAMP(3);
@@ -328,22 +358,17 @@ __global__ __launch_bounds__(CVAE_THREADS) void param_kernel(NetDev net, const T
   const TileDesc td = tiles[blockIdx.x];
   const LayerDev& L = net.L[td.layer];
   const int tid = threadIdx.x;
-  const int o = td.o0 + (tid >> 3), i = td.i0 + (tid & 7) * 4;
+  const Pre4 st = load4<MODE>(L, td.o0 + (tid >> 3), td.i0 + (tid & 7) * 4, aa);
   f32x4 g4 = {0.f, 0.f, 0.f, 0.f};
   float db = 0.f;
   if (MODE == PM_ADAM) {
-    if (o < L.N && i < L.K) {
-      const int seg = (L.nseg == 2 && o >= L.seg_rows0) ? 1 : 0;
-      const int64_t base = L.pw[seg] + (int64_t)(seg ? o - L.seg_rows0 : o) * L.K + i;
-      const int nv = min(4, L.K - i);
 #pragma unroll
-      for (int c = 0; c < 4; ++c) g4[c] = c < nv ? aa.grads[base + c] * aa.grad_scale : 0.f;
-    }
+    for (int c = 0; c < 4; ++c) g4[c] = c < st.nv ? aa.grads[st.base + c] * aa.grad_scale : 0.f;
     const int ob = td.o0 + tid;
     if (td.i0 == 0 && tid < 32 && ob < L.N) {
       const int seg = (L.nseg == 2 && ob >= L.seg_rows0) ? 1 : 0;
       db = aa.grads[L.pb[seg] + (seg ? ob - L.seg_rows0 : ob)] * aa.grad_scale;
     }
   }
-  tile_epilogue<T, MODE>(L, td.o0, td.i0, g4, db, aa, wt);
+  tile_epilogue<T, MODE, CVAE_THREADS>(L, td.o0, td.i0, st, g4, db, aa, wt);
 }

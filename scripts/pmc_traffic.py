@@ -15,7 +15,7 @@ from collections import defaultdict
 
 
 def short(name):
-    if "rowchain_kernel" in name:
+    if "rowchain_kernel" in name or "fastchain_kernel" in name:
         return "rowchain"
     if "wgrad_kernel" in name:
         return "wgrad_adam"
