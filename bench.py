@@ -14,6 +14,10 @@ Prints ONE JSON line (rank 0).  `roofline` is the dominant kernel's algorithmic
 FLOP per launch ÷ its average HIP-event duration over the timed region;
 `cpu_baseline` times the repo's CPU oracle (a torch-CPU restatement of the
 reference step, oracle/cvae_oracle.py) on the host cores for ~10 s.
+
+Timing: the K timed steps run without events (value, ms_per_step); a second pass of the same K
+steps records HIP events between the kernels on the launch stream for the per-kernel durations
+(roofline), since events inside the timed pass perturb it.
 """
 import argparse
 import json
@@ -150,23 +154,31 @@ def main():
     dp = DataParallelStep(eng)  # N=1: fused train_step; N>1: fwd/bwd → RCCL all-reduce → Adam
     dp.broadcast_params()
 
-    def step():
-        dp.step(x, batch=B, global_batch=B * world)
+    def run(k):
+        """k training steps: on one GPU one cvae_train_steps call (no host work per step); under
+        data parallelism fwd/bwd → RCCL all-reduce → Adam per step."""
+        if world == 1:
+            eng.train_steps(x, k, batch=B)
+        else:
+            for _ in range(k):
+                dp.step(x, batch=B, global_batch=B * world)
 
-    for _ in range(args.warmup):
-        step()
+    run(args.warmup)
     torch.cuda.synchronize(dev)
-    eng.set_timing(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    run(args.steps)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     t = time.perf_counter() - t0
+    # kernel durations for the roofline: the same K steps again with HIP events recorded on the
+    # launch stream between kernels (events inside the timed pass would add ~10 us per step)
+    eng.set_timing(True)
+    run(args.steps)
+    torch.cuda.synchronize(dev)
     kt = eng.kernel_times()
     eng.set_timing(False)
     if world > 1:

@@ -680,6 +680,22 @@ int cvae_train_step(cvae_handle* h, const void* x, const int64_t* idx, int batch
   return tmark(h, s, "end");
 }
 
+int cvae_train_steps(cvae_handle* h, const void* x, const int64_t* idx, int batch, int n_steps, const float* eps,
+                     uint64_t seed, uint64_t offset, const cvae_loss_weights* w, float* params, float* m, float* v,
+                     int step0, float lr, float beta1, float beta2, float adam_eps, float* loss_out,
+                     float* loss_accum, void* stream) {
+  if (!h) return fail(CVAE_E_INVALID, "null handle");
+  if (n_steps < 0) return fail(CVAE_E_INVALID, "n_steps must be >= 0");
+  const int Z = h->cfg.latent_dim;
+  for (int i = 0; i < n_steps; ++i) {
+    const int rc = cvae_train_step(h, x, idx ? idx + (size_t)i * batch : nullptr, batch,
+                                   eps ? eps + (size_t)i * batch * Z : nullptr, seed, offset + (uint64_t)i, w, params,
+                                   m, v, step0 + i, lr, beta1, beta2, adam_eps, loss_out, loss_accum, stream);
+    if (rc) return rc;
+  }
+  return CVAE_OK;
+}
+
 int cvae_loss(const float* recon, const float* x, const float* mu, const float* logvar, int batch, int seq_len,
               int dim, int latent_dim, const cvae_loss_weights* w, float* loss_out, float* workspace,
               void* stream) {

@@ -113,8 +113,16 @@ __device__ __forceinline__ f32x4 from_bf4(bf16x4 h) {
 }
 // rows b0 + 4q .. +3 of feature f of an arena matrix with Kf feature rows (aoff; b0 % 16 == 0):
 // the 16 features × 4 row quads of one wave instruction are 512 contiguous bytes
+#ifndef CVAE_ARENA_SC1
+#define CVAE_ARENA_SC1 0
+#endif
 __device__ __forceinline__ void arena4(void* base, int Kf, int f, int b0, int q, bf16x4 h) {
-  if (!CVAE_DIAG_NOSTORE) gst<bf16x4>((__bf16*)base + aoff(f, b0 + 4 * q, Kf), h);
+  if (CVAE_DIAG_NOSTORE) return;
+  __bf16* p = (__bf16*)base + aoff(f, b0 + 4 * q, Kf);
+  if (CVAE_ARENA_SC1)  // write-through (sc1): the line leaves L2 now, not at the kernel-end release
+    __hip_atomic_store((uint64_t*)p, __builtin_bit_cast(uint64_t, h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    gst<bf16x4>(p, h);
 }
 
 // lane q (= lane & 3) of a quad holding row r0+q's values y[0..3] gets value q of rows r0..r0+3
@@ -190,6 +198,14 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
     return to_bf4(y);
   };
 
+  // one round (one (feature, row quad) task per thread) of the arena copy of the XIN image:
+  // the x_rel tile → xT(E0) during S1..S5 (before the loss overwrites it), dL/drecon → gT(D3)
+  // during S9..S13 — both only feed the dW kernel, so they stay off the critical phases
+  auto copy_round = [&](int k, void* mat, int Kf) {
+    const int e = k * NT + tid;
+    if (e < Ip * 4) arena4(mat, Kf, e >> 2, b0, e & 3, *(const bf16x4*)(XIN + ioff(e >> 2, e & 3)));
+  };
+  static_assert(Ip * 4 <= 5 * NT, "XIN arena copy: 5 rounds");
   const int n = 16 * wave + n16;  // this lane's feature in the 128-wide layers (n-tile = wave)
   // Weight registers of every step.  Issue schedule (loads per wave, after the step's own stores so
   // a burst never holds an epilogue store back; big sets spread over several steps, >= 2 steps
@@ -260,7 +276,6 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
     for (int k = 0; k < UB; ++k)
       if (k * NT + tid < net.nbias / 4) ((f32x4*)BIAS)[k * NT + tid] = bv[k];
     stamp();
-    void* const xe0 = L[LE0].xT;
     void* const xc0 = L[LC0].xT;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -283,8 +298,6 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
         const bf16x4 hi = to_bf4(quad_t(f32x4{val[4], val[5], val[6], val[7]}));
         *(bf16x4*)(XIN + ioff(f0 + qd, rq)) = lo;
         *(bf16x4*)(XIN + ioff(f0 + 4 + qd, rq)) = hi;
-        arena4(xe0, L[LE0].Kp, f0 + qd, b0, rq, lo);
-        arena4(xe0, L[LE0].Kp, f0 + 4 + qd, b0, rq, hi);
         if (c == 0) {  // quad-uniform: condition input features 0..3 (x, y, 0, 0) of these rows
           const bf16x4 cs = to_bf4(quad_t(f32x4{(float)(__bf16)s0, (float)(__bf16)s1, 0.f, 0.f}));
           *(bf16x4*)(CIN + ioff(qd, rq)) = cs;
@@ -329,6 +342,7 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
     *(bf16x4*)(A1 + ioff(n, q)) = he;
     arena4(L[LE2].xT, L[LE2].Kp, n, b0, q, he);
   }
+  copy_round(0, L[LE0].xT, L[LE0].Kp);
   wload(wE3, Wf(LE3), H, wave);
   if (wave == 0) wload(wFC, Wf(LFC), 2 * H, 0);  // fc_mu ‖ fc_logvar: one real n-tile
   lbar();
@@ -339,6 +353,7 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
     *(bf16x4*)(A0 + ioff(n, q)) = he;
     arena4(L[LE3].xT, L[LE3].Kp, n, b0, q, he);
   }
+  copy_round(1, L[LE0].xT, L[LE0].Kp);
   wload(wD0, Wf(LD0), 160, wave);
   wload(wD1, Wf(LD1), H, wave);
   lbar();
@@ -349,6 +364,7 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
     *(bf16x4*)(HCAT + ioff(n, q)) = he;
     arena4(L[LFC].xT, L[LFC].Kp, n, b0, q, he);
   }
+  copy_round(2, L[LE0].xT, L[LE0].Kp);
   wload(wD2, Wf(LD2), H, wave);
 #pragma unroll
   for (int g = 0; g < 2; ++g)
@@ -381,6 +397,7 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
       arena4(L[LD0].xT, L[LD0].Kp, j, b0, q, zh);
     }
   }
+  copy_round(3, L[LE0].xT, L[LE0].Kp);
 #pragma unroll
   for (int g = 2; g < G3; ++g)
     if (wave + NW * g < NG3) wload(wD3[g], Wf(LD3), H, wave + NW * g);
@@ -392,6 +409,7 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
     *(bf16x4*)(A0 + ioff(n, q)) = h;
     arena4(L[LD1].xT, L[LD1].Kp, n, b0, q, h);
   }
+  copy_round(4, L[LE0].xT, L[LE0].Kp);
   wload_part<0, NKI / 2>(wD3b, Wb(LD3), Ip, wave);
   lbar();
   stamp();
@@ -459,12 +477,10 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
   lbar();
   stamp();
   // time-monotonicity term relu(r_s − r_{s+1}) (:261-262, ReLU'(0) = 0) into the time channel of
-  // dL/drecon (one task per (timestep, row quad): its GL image entry and its arena row), and the
-  // feature-major arena copy gT(D3) of every other feature (the time channel is the fix task's)
+  // dL/drecon: one task per (timestep, row quad).  The arena copy gT(D3) of the finished image is
+  // spread over the backward steps (copy_round), off this critical phase.
   {
-    constexpr int UF = (Ip * 4 + NT - 1) / NT;
-    const float inv_D = 1.f / (float)D, wt = a.w_time * inv_BS1;
-    void* const gd3 = L[LD3].gT;
+    const float wt = a.w_time * inv_BS1;
     for (int e = tid; e < S * 4; e += NT) {
       const int s = e >> 2, qq = e & 3, f = s * D;
       f32x4 gv = *(const f32x4*)(GD0 + s * R + 4 * qq);  // fp32: dL/drecon is rounded once
@@ -483,16 +499,7 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
           if (live && u0 > 0.f) gv[i] -= wt;
         }
       }
-      const bf16x4 h = to_bf4(gv);
-      *(bf16x4*)(XIN + ioff(f, qq)) = h;
-      arena4(gd3, L[LD3].Np, f, b0, qq, h);
-    }
-#pragma unroll
-    for (int u = 0; u < UF; ++u) {
-      const int e = u * NT + tid;
-      const int f = e >> 2, qq = e & 3;
-      if (e < Ip * 4 && (f >= I || f != fdiv(f, inv_D) * D))
-        arena4(gd3, L[LD3].Np, f, b0, qq, *(const bf16x4*)(XIN + ioff(f, qq)));
+      *(bf16x4*)(XIN + ioff(f, qq)) = to_bf4(gv);
     }
   }
   wload(wD0b[0], Wb(LD0), H, wave);
@@ -508,6 +515,7 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
     *(bf16x4*)(A1 + ioff(n, q)) = h;
     arena4(L[LD2].gT, L[LD2].Np, n, b0, q, h);
   }
+  copy_round(0, L[LD3].gT, L[LD3].Np);
   wload(wE3b, Wb(LE3), H, wave);
   wload(wE2b, Wb(LE2), H, wave);
   lbar();
@@ -517,6 +525,7 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
     *(bf16x4*)(A0 + ioff(n, q)) = h;
     arena4(L[LD1].gT, L[LD1].Np, n, b0, q, h);
   }
+  copy_round(1, L[LD3].gT, L[LD3].Np);
   wload(wE1b, Wb(LE1), H, wave);
   wload(wC1b, Wb(LC1), H, wave);
   lbar();
@@ -526,6 +535,7 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
     *(bf16x4*)(A1 + ioff(n, q)) = h;
     arena4(L[LD0].gT, L[LD0].Np, n, b0, q, h);
   }
+  copy_round(2, L[LD3].gT, L[LD3].Np);
   lbar();
   stamp();
   {  // S12: D0ᵀ: [dz ‖ dh_c(decoder share)]; dz → KL/reparameterisation backward → G_fc
@@ -557,6 +567,7 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
       }
     }
   }
+  copy_round(3, L[LD3].gT, L[LD3].Np);
   lbar();
   stamp();
   {  // S13: fcᵀ: dh = G_fc · W_fc → h_traj gradient (mask E3) and h_c gradient (+ decoder share, mask C1)
@@ -571,6 +582,7 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
     *(bf16x4*)(CB + ioff(n, q)) = hc;
     arena4(L[LC1].gT, L[LC1].Np, n, b0, q, hc);
   }
+  copy_round(4, L[LD3].gT, L[LD3].Np);
   lbar();
   stamp();
   {  // S14: E3ᵀ

@@ -104,6 +104,20 @@ __device__ __forceinline__ Pre4 load4(const LayerDev& L, int o, int i, const Ada
   s.base = L.pw[seg] + (int64_t)(seg ? o - L.seg_rows0 : o) * L.K + i;
   s.nv = min(4, L.K - i);
   if (MODE == PM_GRAD) return s;
+  if (s.nv == 4 && (s.base & 3) == 0) {  // 16-B aligned run (every layer with K % 4 == 0)
+    const f32x4 p4 = *(const f32x4*)(a.params + s.base);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) s.p[c] = p4[c];
+    if (MODE == PM_ADAM) {
+      const f32x4 m4 = *(const f32x4*)(a.m + s.base), v4 = *(const f32x4*)(a.v + s.base);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        s.m[c] = m4[c];
+        s.v[c] = v4[c];
+      }
+    }
+    return s;
+  }
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     if (c < s.nv) {
@@ -130,12 +144,18 @@ __device__ __forceinline__ f32x4 apply4(Pre4 s, f32x4 g4, const AdamArgs& a) {
   if (MODE == PM_ADAM) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) s.p[c] = adam_math(s.p[c], g4[c], s.m[c], s.v[c], a);
+    if (s.nv == 4 && (s.base & 3) == 0) {
+      *(f32x4*)(a.params + s.base) = f32x4{s.p[0], s.p[1], s.p[2], s.p[3]};
+      *(f32x4*)(a.m + s.base) = f32x4{s.m[0], s.m[1], s.m[2], s.m[3]};
+      *(f32x4*)(a.v + s.base) = f32x4{s.v[0], s.v[1], s.v[2], s.v[3]};
+    } else {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      if (c < s.nv) {
-        a.params[s.base + c] = s.p[c];
-        a.m[s.base + c] = s.m[c];
-        a.v[s.base + c] = s.v[c];
+      for (int c = 0; c < 4; ++c) {
+        if (c < s.nv) {
+          a.params[s.base + c] = s.p[c];
+          a.m[s.base + c] = s.m[c];
+          a.v[s.base + c] = s.v[c];
+        }
       }
     }
   }

@@ -46,6 +46,10 @@ _SIGS = {
                                   C.POINTER(CvaeLossWeights), C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
                                   C.c_float, C.c_float, C.c_float, C.c_float, C.c_void_p, C.c_void_p,
                                   C.c_void_p]),
+    "cvae_train_steps": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_uint64,
+                                   C.c_uint64, C.POINTER(CvaeLossWeights), C.c_void_p, C.c_void_p, C.c_void_p,
+                                   C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, C.c_void_p, C.c_void_p,
+                                   C.c_void_p]),
     "cvae_loss": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
                             C.POINTER(CvaeLossWeights), C.c_void_p, C.c_void_p, C.c_void_p]),
     "cvae_set_timing": (C.c_int, [C.c_void_p, C.c_int]),

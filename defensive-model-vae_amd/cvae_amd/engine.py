@@ -184,6 +184,39 @@ class CVAEEngine:
             self._stream()), "cvae_train_step")
         return self.loss
 
+    def train_steps(self, x, n_steps, idx=None, eps=None, batch=None, weights=None, accumulate=True):
+        """``n_steps`` fused steps in one C call (cvae_train_steps): the loop body of
+        Training_VAE.py:340-370 over a run of equal-size batches, with no host work per step.
+
+        ``idx``: (n_steps·batch) rows of ``x`` (step i takes idx[i·batch:(i+1)·batch]); without it
+        every step uses rows 0..batch-1.  ``eps``: (n_steps·batch, Z) or None (Philox).
+        Returns the device loss tensor of the last step; no host sync.
+        """
+        x = self.as_input(x)
+        idx = self._idx(idx)
+        n_steps = int(n_steps)
+        if batch is None:
+            batch = idx.numel() // max(n_steps, 1) if idx is not None else x.shape[0]
+        B = int(batch)
+        self._check_rows(x, idx, B)
+        if idx is not None and idx.numel() < n_steps * B:
+            raise ValueError(f"idx holds {idx.numel()} rows, {n_steps} steps of {B} need {n_steps * B}")
+        e = None
+        if eps is not None:
+            e = torch.as_tensor(eps).to(device=self.device, dtype=torch.float32).contiguous()
+            if e.shape != (n_steps * B, self.shape[2]):
+                raise ValueError(f"eps must be ({n_steps * B},{self.shape[2]})")
+        w = self._weights(weights)
+        step0 = self.step_count + 1
+        offset = self.rng_offset
+        check(lib().cvae_train_steps(
+            self._h, ptr(x), ptr(idx), B, n_steps, ptr(e), C.c_uint64(self.seed), C.c_uint64(offset), C.byref(w),
+            ptr(self.params), ptr(self.m), ptr(self.v), step0, self.lr, self.betas[0], self.betas[1], self.eps,
+            ptr(self.loss), ptr(self.loss_accum) if accumulate else None, self._stream()), "cvae_train_steps")
+        self.step_count += n_steps
+        self.rng_offset += n_steps
+        return self.loss
+
     def forward_backward(self, x, idx=None, eps=None, batch=None, weights=None, accumulate=True):
         """fwd + loss + bwd into ``self.grads`` (means over this batch) — the DP half-step."""
         x = self.as_input(x)

@@ -145,6 +145,18 @@ int cvae_train_step(cvae_handle* h, const void* x, const int64_t* idx, int batch
                     float lr, float beta1, float beta2, float adam_eps,
                     float* loss_out, float* loss_accum, void* stream);
 
+/* n_steps consecutive fused steps (cvae_train_step) enqueued by one call: step i uses the rows
+ * idx[i*batch .. (i+1)*batch) of x (idx == NULL: rows 0..batch-1 every step), eps rows
+ * eps[i*batch ..] (NULL: Philox(seed, offset + i)) and Adam step step0 + i.  Replaces the inner
+ * `for batch in dataloader` loop of Training_VAE.py:340-370 for a run of equal-size batches
+ * (an epoch's permutation uploaded once); loss_out = the last step's losses, loss_accum += every
+ * step's loss * batch.  No host work per step beyond the two kernel launches. */
+int cvae_train_steps(cvae_handle* h, const void* x, const int64_t* idx, int batch, int n_steps,
+                     const float* eps, uint64_t seed, uint64_t offset, const cvae_loss_weights* w,
+                     float* params, float* m, float* v, int step0,
+                     float lr, float beta1, float beta2, float adam_eps,
+                     float* loss_out, float* loss_accum, void* stream);
+
 /* Standalone conditional_vae_loss (Training_VAE.py:229-268), forward only, for
  * callers holding (recon, x, mu, logvar) fp32 device tensors; x is the RELATIVE
  * batch as at the reference call site (:356-359).  loss_out fp32[5] =

@@ -314,3 +314,21 @@ def test_train_loop_end_to_end_traj20(cvae, golden, tmp_path):
     assert len(sd) == 24
     for k in cvae_np.param_keys():
         assert rel_l2(sd[k].numpy(), d["final/" + k]) < 1e-4, k
+
+
+def test_train_steps_equals_repeated_train_step(cvae):
+    """cvae_train_steps (one C call for n steps) == n train_step calls, bit for bit (bf16 fast
+    chain and fp32 generic chain), with per-step rows from idx and Philox eps offsets."""
+    for dtype, S, D in (("bf16", 100, 6), ("fp32", 10, 3)):
+        torch.manual_seed(0)
+        ref = OracleCVAE(S, D, 8)
+        m1, e1 = _model(cvae, S, D, 8, sd=ref.state_dict(), dtype=dtype, max_batch=64)
+        m2, e2 = _model(cvae, S, D, 8, sd=ref.state_dict(), dtype=dtype, max_batch=64)
+        data = torch.randn(300, S, D).cuda()
+        idx = torch.randint(0, 300, (3 * 64,)).cuda()
+        for i in range(3):
+            e1.train_step(data, idx=idx[i * 64:(i + 1) * 64])
+        e2.train_steps(data, 3, idx=idx, batch=64)
+        torch.cuda.synchronize()
+        assert torch.equal(e1.params, e2.params), dtype
+        assert torch.equal(e1.loss, e2.loss) and torch.equal(e1.loss_accum, e2.loss_accum), dtype
