@@ -696,6 +696,56 @@ int cvae_train_steps(cvae_handle* h, const void* x, const int64_t* idx, int batc
   return CVAE_OK;
 }
 
+int cvae_bench_kernels(cvae_handle* h, const void* x, const int64_t* idx, int batch, int reps, float* params,
+                       float* m, float* v, int step0, float* ms, void* stream) {
+  if (!h || !x || !params || !m || !v || !ms || reps < 1) return fail(CVAE_E_INVALID, "bad argument");
+  int rc = check_batch(h, batch);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const bool timing = h->timing;
+  h->timing = false;
+  hipEvent_t e0, e1;
+  HIPCK(hipEventCreate(&e0));
+  HIPCK(hipEventCreate(&e1));
+  const cvae_loss_weights w{0.1f, 0.1f, 1.0f, 1.0f};
+  const float lr = 1e-3f, b1 = 0.9f, b2 = 0.999f, ae = 1e-8f;
+  auto timed = [&](int which, float* out) -> int {
+    HIPCK(hipEventRecord(e0, s));
+    for (int r = 0; r < reps; ++r) {
+      int rc2 = CVAE_OK;
+      RowArgs ra;
+      if (which == 0) {
+        rc2 = h->cfg.dtype == CVAE_BF16 ? train_fwd_bwd_impl<__bf16>(h, x, idx, batch, nullptr, 1, r, &w, s, ra)
+                                        : train_fwd_bwd_impl<float>(h, x, idx, batch, nullptr, 1, r, &w, s, ra);
+      } else if (which == 1) {
+        AdamArgs aa = make_adam(params, nullptr, m, v, step0 + r, lr, b1, b2, ae, 1.f);
+        const int nt = (int)h->tiles.size();
+        if (h->cfg.dtype == CVAE_BF16)
+          hipLaunchKernelGGL((wgrad_kernel<__bf16, PM_ADAM>), dim3(nt), dim3(WG_THREADS), 0, s, h->net, h->d_tiles,
+                             bk_of(h, batch), aa, LossArgs{});
+        else
+          hipLaunchKernelGGL((wgrad_kernel<float, PM_ADAM>), dim3(nt), dim3(WG_THREADS), 0, s, h->net, h->d_tiles,
+                             bk_of(h, batch), aa, LossArgs{});
+        rc2 = hipGetLastError() == hipSuccess ? CVAE_OK : CVAE_E_HIP;
+      } else {
+        rc2 = cvae_train_step(h, x, idx, batch, nullptr, 1, r, &w, params, m, v, step0 + r, lr, b1, b2, ae, nullptr,
+                              nullptr, stream);
+      }
+      if (rc2) return rc2;
+    }
+    HIPCK(hipEventRecord(e1, s));
+    HIPCK(hipEventSynchronize(e1));
+    HIPCK(hipEventElapsedTime(out, e0, e1));
+    *out /= reps;
+    return CVAE_OK;
+  };
+  for (int k = 0; k < 3 && !rc; ++k) rc = timed(k, ms + k);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  h->timing = timing;
+  return rc;
+}
+
 int cvae_loss(const float* recon, const float* x, const float* mu, const float* logvar, int batch, int seq_len,
               int dim, int latent_dim, const cvae_loss_weights* w, float* loss_out, float* workspace,
               void* stream) {

@@ -35,7 +35,7 @@ enum { LC0 = 0, LC1, LE0, LE1, LE2, LE3, LFC, LD0, LD1, LD2, LD3 };
 enum { MC0 = 0, MC1, ME0, ME1, ME2, ME3, MD0, MD1, MD2 };
 
 struct Lds {  // byte offsets
-  int xin, cin, cb, a0, a1, hcat, dcat, gfc, mask, mulv, eps, stdv, rch0, gd0, dhc2, bias, part, total;
+  int xin, cin, cb, a0, a1, hcat, dcat, gfc, mask, mulv, eps, stdv, rch0, gd0, dhc2, bias, part, stamps, total;
 };
 __host__ __device__ inline Lds lds_layout(int Ip, int S, int nbias) {
   Lds p;
@@ -58,6 +58,7 @@ __host__ __device__ inline Lds lds_layout(int Ip, int S, int nbias) {
   p.dhc2 = take(H * R * 4);     // fp32 [c][row]: decoder share of dh_c
   p.bias = take(nbias * 4);
   p.part = take(NW * 8 * 4);
+  p.stamps = take(CVAE_DIAG_STAMPS ? 64 * 8 : 0);  // diagnostic builds: stamps kept in LDS
   p.total = o;
   return p;
 }
@@ -172,9 +173,11 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
   auto Wb = [&](int l) { return (const void*)L[l].Wb; };
   auto bias = [&](int l, int n) { return BIAS[net.bias_off[l] + n]; };
   int stamp_i = 0;
+  // diagnostic builds only: wave 0's step times, kept in LDS (a global store per stamp would queue
+  // behind the weight stream) and written out at the end
+  unsigned long long* const STAMPS = (unsigned long long*)(smem + P.stamps);
   auto stamp = [&]() {
-    if (CVAE_DIAG_STAMPS && a.stamps && tid == 0)
-      gst<unsigned long long>(a.stamps + blockIdx.x * 64 + (stamp_i < 63 ? stamp_i : 63), __builtin_amdgcn_s_memrealtime());
+    if (CVAE_DIAG_STAMPS && tid == 0 && stamp_i < 64) STAMPS[stamp_i] = __builtin_amdgcn_s_memrealtime();
     ++stamp_i;
   };
 
@@ -623,6 +626,10 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
     float s = 0.f;
     for (int w = 0; w < NW; ++w) s += PART[w * 8 + tid];
     gst<float>(a.partials + blockIdx.x * 8 + tid, s);
+  }
+  if (CVAE_DIAG_STAMPS && a.stamps && tid < 64) {
+    stamp();
+    gst<unsigned long long>(a.stamps + blockIdx.x * 64 + tid, tid < stamp_i ? STAMPS[tid] : 0ull);
   }
 }
 

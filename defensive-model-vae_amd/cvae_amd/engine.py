@@ -294,6 +294,19 @@ class CVAEEngine:
             out[k] = (ms[i], int(c))
         return out
 
+    def bench_kernels(self, x, reps, idx=None, batch=None):
+        """{'rowchain', 'wgrad_adam', 'step'}: average device ms of ``reps`` back-to-back launches
+        (cvae_bench_kernels; synchronises; updates params like training steps)."""
+        x = self.as_input(x)
+        idx = self._idx(idx)
+        B = int(batch if batch is not None else (idx.numel() if idx is not None else x.shape[0]))
+        self._check_rows(x, idx, B)
+        ms = (C.c_float * 3)()
+        check(lib().cvae_bench_kernels(self._h, ptr(x), ptr(idx), B, int(reps), ptr(self.params), ptr(self.m),
+                                       ptr(self.v), self.step_count + 1, ms, self._stream()), "cvae_bench_kernels")
+        self.step_count += 2 * int(reps)
+        return {"rowchain": ms[0], "wgrad_adam": ms[1], "step": ms[2]}
+
     def workspace_bytes(self):
         b = C.c_int64()
         check(lib().cvae_workspace_bytes(self._h, C.byref(b)))

@@ -176,6 +176,14 @@ int cvae_loss(const float* recon, const float* x, const float* mu, const float* 
 int cvae_set_timing(cvae_handle* h, int enabled);
 int cvae_kernel_times(cvae_handle* h, char* names, int names_len, float* ms, int max_n);
 
+/* Measurement: average device time (ms) of `reps` back-to-back launches of each kernel of the
+ * fused training step on the batch (x, idx, batch): ms[0] = the row chain (forward + loss + every
+ * dX), ms[1] = the dW + Adam kernel, ms[2] = the whole step.  Two HIP events per measurement on
+ * `stream`; SYNCHRONISES the stream (measurement only).  The row-chain and step runs update
+ * params/m/v like training steps (step numbers step0..). */
+int cvae_bench_kernels(cvae_handle* h, const void* x, const int64_t* idx, int batch, int reps,
+                       float* params, float* m, float* v, int step0, float* ms, void* stream);
+
 const char* cvae_last_error(void);
 int cvae_abi_version(void);
 
