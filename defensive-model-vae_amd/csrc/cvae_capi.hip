@@ -429,6 +429,26 @@ AdamArgs make_adam(float* params, float* grads, float* m, float* v, int step, fl
 // hidden 128, latent 8, 4+4 layers, S·D a multiple of 8 padding to one of the instantiated chunk
 // counts.  CVAE_GENERIC=1 in the environment forces the interpreter (A/B comparisons).
 constexpr int kFastNki[] = {19};
+// the compile-time arena layout the fast kernel addresses (fchain::Layout) is the handle's
+template <int NKI>
+bool fast_layout_matches(const cvae_handle* h) {
+  using LY = fchain::Layout<NKI>;
+  const NetDev& n = h->net;
+  if (n.n_layers != LY::NL || n.nbias != LY::nbias || n.Bp % 32 != 0 ||
+      (const char*)n.bias_all != h->arena + LY::bias_base)
+    return false;
+  const int64_t Bp2 = 2 * (int64_t)n.Bp;
+  for (int l = 0; l < LY::NL; ++l) {
+    const LayerDev& L = n.L[l];
+    if (L.Kp != LY::Kp(l) || L.Np != LY::Np(l) || n.bias_off[l] != LY::bias_off(l) ||
+        (char*)L.Wf != h->arena + LY::wf(l) || (char*)L.Wb != h->arena + LY::wb(l) ||
+        (char*)L.xT != h->arena + LY::act0 + Bp2 * LY::xrows(l) ||
+        (char*)L.gT != h->arena + LY::act0 + Bp2 * LY::grows(l))
+      return false;
+  }
+  return true;
+}
+
 int plan_fast(cvae_handle* h) {
   const cvae_config& c = h->cfg;
   const NetDev& n = h->net;
@@ -441,6 +461,7 @@ int plan_fast(cvae_handle* h) {
     if (n.Ip != 32 * nki) continue;
     const fchain::Lds lp = fchain::lds_layout(n.Ip, n.S, n.nbias);
     if (lp.total > 160 * 1024) return CVAE_OK;
+    if (nki == 19 && !fast_layout_matches<19>(h)) return CVAE_OK;
     h->fast_nki = nki;
     h->fast_lds = lp.total;
     if (nki == 19)
@@ -467,7 +488,8 @@ int train_fwd_bwd_impl(cvae_handle* h, const void* x, const int64_t* idx, int ba
     ra.stamps = h->d_stamps;
     const int grid = rup_i(batch, 32) / fchain::R;
     if (h->fast_nki == 19)
-      hipLaunchKernelGGL(fchain::fastchain_kernel<19>, dim3(grid), dim3(fchain::NT), h->fast_lds, s, h->net, ra);
+      hipLaunchKernelGGL(fchain::fastchain_kernel<19>, dim3(grid), dim3(fchain::NT), h->fast_lds, s,
+                         fchain::FastNet{h->arena, h->net.Bp, h->net.S, h->net.D, h->net.I}, ra);
     HIPCK(hipGetLastError());
     return CVAE_OK;
   }

@@ -34,6 +34,48 @@ typedef short i16x4 __attribute__((ext_vector_type(4)));
 enum { LC0 = 0, LC1, LE0, LE1, LE2, LE3, LFC, LD0, LD1, LD2, LD3 };
 enum { MC0 = 0, MC1, ME0, ME1, ME2, ME3, MD0, MD1, MD2 };
 
+// The arena of the fast configuration (alloc_arena in cvae_capi.hip) as compile-time byte offsets:
+// the kernel derives every weight-copy, bias and activation pointer from the arena base and Bp.
+// (Reading the ~50 pointers of NetDev instead, scalar-register pressure made the compiler re-load
+// them from the kernel arguments one serial s_load round trip at a time — ~2 us of the prologue.)
+// plan_fast checks every offset against the handle's NetDev before enabling the kernel.
+template <int NKI>
+struct Layout {
+  static constexpr int Ip = 32 * NKI, NL = 11;
+  __host__ __device__ static constexpr int Kp(int l) {
+    return l == LC0 ? 32 : l == LE0 ? Ip : l == LFC ? 2 * H : l == LD0 ? 160 : H;
+  }
+  __host__ __device__ static constexpr int Np(int l) { return l == LFC ? 32 : l == LD3 ? Ip : H; }
+  __host__ __device__ static constexpr int64_t r256(int64_t b) { return (b + 255) / 256 * 256; }
+  __host__ __device__ static constexpr int64_t wf(int l) {
+    int64_t o = 0;
+    for (int k = 0; k < l; ++k) o += 2 * r256(2LL * Np(k) * Kp(k));
+    return o;
+  }
+  __host__ __device__ static constexpr int64_t wb(int l) { return wf(l) + r256(2LL * Np(l) * Kp(l)); }
+  __host__ __device__ static constexpr int bias_off(int l) {
+    int o = 0;
+    for (int k = 0; k < l; ++k) o += Np(k);
+    return o;
+  }
+  static constexpr int nbias = bias_off(NL);
+  static constexpr int64_t bias_base = wf(NL);
+  static constexpr int64_t act0 = bias_base + r256(4LL * nbias);
+  // xT / gT of layer l start at act0 + Bp·2·(feature rows before them); every matrix is a
+  // multiple of 256 B when Bp % 32 == 0, so take()'s rounding adds nothing
+  __host__ __device__ static constexpr int64_t xrows(int l) {
+    int64_t o = 0;
+    for (int k = 0; k < l; ++k) o += Kp(k) + Np(k);
+    return o;
+  }
+  __host__ __device__ static constexpr int64_t grows(int l) { return xrows(l) + Kp(l); }
+};
+
+struct FastNet {  // kernel argument of fastchain_kernel (everything else is compile-time)
+  char* arena;
+  int Bp, S, D, I;
+};
+
 struct Lds {  // byte offsets
   int xin, cin, cb, a0, a1, hcat, dcat, gfc, mask, mulv, eps, stdv, rch0, gd0, dhc2, bias, part, stamps, total;
 };
@@ -142,7 +184,7 @@ __device__ __forceinline__ f32x4 quad_t(f32x4 y) {
 __device__ __forceinline__ void lbar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 template <int NKI>
-__global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
+__global__ __launch_bounds__(NT) void fastchain_kernel(FastNet net, RowArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int Ip = NKI * 32, NG3 = NKI * 2;                 // D3 output n-tiles
   constexpr int G3 = (NG3 + NW - 1) / NW;                     // D3 n-tiles per wave (max)
@@ -150,7 +192,8 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
   const int n16 = lane & 15, q = lane >> 4;
   const int b0 = blockIdx.x * R, nrows = max(0, min(R, a.batch - b0));
   const int Bp = net.Bp, S = net.S, D = net.D, I = net.I;
-  const Lds P = lds_layout(Ip, S, net.nbias);
+  using LY = Layout<NKI>;
+  const Lds P = lds_layout(Ip, S, LY::nbias);
   __bf16* const XIN = (__bf16*)(smem + P.xin);
   __bf16* const CIN = (__bf16*)(smem + P.cin);
   __bf16* const CB = (__bf16*)(smem + P.cb);
@@ -168,10 +211,13 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
   float* const DHC2 = (float*)(smem + P.dhc2);
   float* const BIAS = (float*)(smem + P.bias);
   float* const PART = (float*)(smem + P.part);
-  const LayerDev* const L = net.L;
-  auto Wf = [&](int l) { return (const void*)L[l].Wf; };
-  auto Wb = [&](int l) { return (const void*)L[l].Wb; };
-  auto bias = [&](int l, int n) { return BIAS[net.bias_off[l] + n]; };
+  char* const AR = net.arena;
+  const int64_t Bp2 = 2 * (int64_t)Bp;
+  auto Wf = [&](int l) { return (const void*)(AR + LY::wf(l)); };
+  auto Wb = [&](int l) { return (const void*)(AR + LY::wb(l)); };
+  auto XT = [&](int l) { return (void*)(AR + LY::act0 + Bp2 * LY::xrows(l)); };
+  auto GT = [&](int l) { return (void*)(AR + LY::act0 + Bp2 * LY::grows(l)); };
+  auto bias = [&](int l, int n) { return BIAS[LY::bias_off(l) + n]; };
   int stamp_i = 0;
   // diagnostic builds only: wave 0's step times, kept in LDS (a global store per stamp would queue
   // behind the weight stream) and written out at the end
@@ -251,11 +297,11 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
     f32x4 bv[UB];
 #pragma unroll
     for (int k = 0; k < UB; ++k) {
-      const int e = min(k * NT + tid, net.nbias / 4 - 1);
-      bv[k] = gld<f32x4>(net.bias_all + 4 * e);
+      const int e = min(k * NT + tid, LY::nbias / 4 - 1);
+      bv[k] = gld<f32x4>((const float*)(AR + LY::bias_base) + 4 * e);
     }
     // the weights of the first step queue behind the x tile and the biases (vmcnt retires in order)
-    wload(wC0, Wf(LC0), L[LC0].Kp, wave);
+    wload(wC0, Wf(LC0), LY::Kp(LC0), wave);
     wload_part<0, NKI / 2>(wE0, Wf(LE0), Ip, wave);
     stamp();
     // eps: 8 latents × 16 rows, 4 per thread (host-given, or Philox as philox_normal)
@@ -277,9 +323,9 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
     if (tid < 16 * 4) *(uint64_t*)(GFC + (16 + tid / 4) * 16 + 4 * (tid & 3)) = 0ull;
 #pragma unroll
     for (int k = 0; k < UB; ++k)
-      if (k * NT + tid < net.nbias / 4) ((f32x4*)BIAS)[k * NT + tid] = bv[k];
+      if (k * NT + tid < LY::nbias / 4) ((f32x4*)BIAS)[k * NT + tid] = bv[k];
     stamp();
-    void* const xc0 = L[LC0].xT;
+    void* const xc0 = XT(LC0);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int v = u * NT + tid;
@@ -304,7 +350,7 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
         if (c == 0) {  // quad-uniform: condition input features 0..3 (x, y, 0, 0) of these rows
           const bf16x4 cs = to_bf4(quad_t(f32x4{(float)(__bf16)s0, (float)(__bf16)s1, 0.f, 0.f}));
           *(bf16x4*)(CIN + ioff(qd, rq)) = cs;
-          arena4(xc0, L[LC0].Kp, qd, b0, rq, cs);
+          arena4(xc0, LY::Kp(LC0), qd, b0, rq, cs);
         }
       }
     }
@@ -325,10 +371,10 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
     uint32_t nib;
     const bf16x4 hc = relu(mm(CIN, wC0), bias(LC0, n), MC0, n, nib);
     *(bf16x4*)(CB + ioff(n, q)) = hc;
-    arena4(L[LC1].xT, L[LC1].Kp, n, b0, q, hc);
+    arena4(XT(LC1), LY::Kp(LC1), n, b0, q, hc);
     const bf16x4 he = relu(mm(XIN, wE0), bias(LE0, n), ME0, n, nib);
     *(bf16x4*)(A0 + ioff(n, q)) = he;
-    arena4(L[LE1].xT, L[LE1].Kp, n, b0, q, he);
+    arena4(XT(LE1), LY::Kp(LE1), n, b0, q, he);
   }
   wload(wE1, Wf(LE1), H, wave);
   wload(wE2, Wf(LE2), H, wave);
@@ -339,13 +385,13 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
     const bf16x4 hc = relu(mm(CB, wC1), bias(LC1, n), MC1, n, nib);
     *(bf16x4*)(HCAT + ioff(H + n, q)) = hc;
     *(bf16x4*)(DCAT + ioff(Z + n, q)) = hc;
-    arena4(L[LFC].xT, L[LFC].Kp, H + n, b0, q, hc);
-    arena4(L[LD0].xT, L[LD0].Kp, Z + n, b0, q, hc);
+    arena4(XT(LFC), LY::Kp(LFC), H + n, b0, q, hc);
+    arena4(XT(LD0), LY::Kp(LD0), Z + n, b0, q, hc);
     const bf16x4 he = relu(mm(A0, wE1), bias(LE1, n), ME1, n, nib);
     *(bf16x4*)(A1 + ioff(n, q)) = he;
-    arena4(L[LE2].xT, L[LE2].Kp, n, b0, q, he);
+    arena4(XT(LE2), LY::Kp(LE2), n, b0, q, he);
   }
-  copy_round(0, L[LE0].xT, L[LE0].Kp);
+  copy_round(0, XT(LE0), LY::Kp(LE0));
   wload(wE3, Wf(LE3), H, wave);
   if (wave == 0) wload(wFC, Wf(LFC), 2 * H, 0);  // fc_mu ‖ fc_logvar: one real n-tile
   lbar();
@@ -354,9 +400,9 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
     uint32_t nib;
     const bf16x4 he = relu(mm(A1, wE2), bias(LE2, n), ME2, n, nib);
     *(bf16x4*)(A0 + ioff(n, q)) = he;
-    arena4(L[LE3].xT, L[LE3].Kp, n, b0, q, he);
+    arena4(XT(LE3), LY::Kp(LE3), n, b0, q, he);
   }
-  copy_round(1, L[LE0].xT, L[LE0].Kp);
+  copy_round(1, XT(LE0), LY::Kp(LE0));
   wload(wD0, Wf(LD0), 160, wave);
   wload(wD1, Wf(LD1), H, wave);
   lbar();
@@ -365,9 +411,9 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
     uint32_t nib;
     const bf16x4 he = relu(mm(A0, wE3), bias(LE3, n), ME3, n, nib);
     *(bf16x4*)(HCAT + ioff(n, q)) = he;
-    arena4(L[LFC].xT, L[LFC].Kp, n, b0, q, he);
+    arena4(XT(LFC), LY::Kp(LFC), n, b0, q, he);
   }
-  copy_round(2, L[LE0].xT, L[LE0].Kp);
+  copy_round(2, XT(LE0), LY::Kp(LE0));
   wload(wD2, Wf(LD2), H, wave);
 #pragma unroll
   for (int g = 0; g < 2; ++g)
@@ -397,10 +443,10 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
       *(f32x4*)(STDV + j * R + 4 * q) = sd;
       const bf16x4 zh = to_bf4(z);
       *(bf16x4*)(DCAT + ioff(j, q)) = zh;
-      arena4(L[LD0].xT, L[LD0].Kp, j, b0, q, zh);
+      arena4(XT(LD0), LY::Kp(LD0), j, b0, q, zh);
     }
   }
-  copy_round(3, L[LE0].xT, L[LE0].Kp);
+  copy_round(3, XT(LE0), LY::Kp(LE0));
 #pragma unroll
   for (int g = 2; g < G3; ++g)
     if (wave + NW * g < NG3) wload(wD3[g], Wf(LD3), H, wave + NW * g);
@@ -410,9 +456,9 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
     uint32_t nib;
     const bf16x4 h = relu(mm(DCAT, wD0), bias(LD0, n), MD0, n, nib);
     *(bf16x4*)(A0 + ioff(n, q)) = h;
-    arena4(L[LD1].xT, L[LD1].Kp, n, b0, q, h);
+    arena4(XT(LD1), LY::Kp(LD1), n, b0, q, h);
   }
-  copy_round(4, L[LE0].xT, L[LE0].Kp);
+  copy_round(4, XT(LE0), LY::Kp(LE0));
   wload_part<0, NKI / 2>(wD3b, Wb(LD3), Ip, wave);
   lbar();
   stamp();
@@ -420,7 +466,7 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
     uint32_t nib;
     const bf16x4 h = relu(mm(A0, wD1), bias(LD1, n), MD1, n, nib);
     *(bf16x4*)(A1 + ioff(n, q)) = h;
-    arena4(L[LD2].xT, L[LD2].Kp, n, b0, q, h);
+    arena4(XT(LD2), LY::Kp(LD2), n, b0, q, h);
   }
   wload_part<NKI / 2, NKI>(wD3b, Wb(LD3), Ip, wave);
   lbar();
@@ -429,7 +475,7 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
     uint32_t nib;
     const bf16x4 h = relu(mm(A1, wD2), bias(LD2, n), MD2, n, nib);
     *(bf16x4*)(A0 + ioff(n, q)) = h;
-    arena4(L[LD3].xT, L[LD3].Kp, n, b0, q, h);
+    arena4(XT(LD3), LY::Kp(LD3), n, b0, q, h);
   }
   lbar();
   stamp();
@@ -516,9 +562,9 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
   {  // S9: D3ᵀ: dL/d h_D2 = GL · W_D3, ReLU mask of D2
     const bf16x4 h = masked(mm(XIN, wD3b), MD2, n);
     *(bf16x4*)(A1 + ioff(n, q)) = h;
-    arena4(L[LD2].gT, L[LD2].Np, n, b0, q, h);
+    arena4(GT(LD2), LY::Np(LD2), n, b0, q, h);
   }
-  copy_round(0, L[LD3].gT, L[LD3].Np);
+  copy_round(0, GT(LD3), LY::Np(LD3));
   wload(wE3b, Wb(LE3), H, wave);
   wload(wE2b, Wb(LE2), H, wave);
   lbar();
@@ -526,9 +572,9 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
   {  // S10: D2ᵀ
     const bf16x4 h = masked(mm(A1, wD2b), MD1, n);
     *(bf16x4*)(A0 + ioff(n, q)) = h;
-    arena4(L[LD1].gT, L[LD1].Np, n, b0, q, h);
+    arena4(GT(LD1), LY::Np(LD1), n, b0, q, h);
   }
-  copy_round(1, L[LD3].gT, L[LD3].Np);
+  copy_round(1, GT(LD3), LY::Np(LD3));
   wload(wE1b, Wb(LE1), H, wave);
   wload(wC1b, Wb(LC1), H, wave);
   lbar();
@@ -536,9 +582,9 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
   {  // S11: D1ᵀ
     const bf16x4 h = masked(mm(A0, wD1b), MD0, n);
     *(bf16x4*)(A1 + ioff(n, q)) = h;
-    arena4(L[LD0].gT, L[LD0].Np, n, b0, q, h);
+    arena4(GT(LD0), LY::Np(LD0), n, b0, q, h);
   }
-  copy_round(2, L[LD3].gT, L[LD3].Np);
+  copy_round(2, GT(LD3), LY::Np(LD3));
   lbar();
   stamp();
   {  // S12: D0ᵀ: [dz ‖ dh_c(decoder share)]; dz → KL/reparameterisation backward → G_fc
@@ -562,49 +608,49 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(NetDev net, RowArgs a) {
           const bf16x4 hm = to_bf4(gm), hl = to_bf4(gl);
           *(bf16x4*)(GFC + ioff(j, q)) = hm;
           *(bf16x4*)(GFC + ioff(Z + j, q)) = hl;
-          arena4(L[LFC].gT, L[LFC].Np, j, b0, q, hm);
-          arena4(L[LFC].gT, L[LFC].Np, Z + j, b0, q, hl);
+          arena4(GT(LFC), LY::Np(LFC), j, b0, q, hm);
+          arena4(GT(LFC), LY::Np(LFC), Z + j, b0, q, hl);
         } else if (f < Z + H) {
           *(f32x4*)(DHC2 + (f - Z) * R + 4 * q) = acc;
         }
       }
     }
   }
-  copy_round(3, L[LD3].gT, L[LD3].Np);
+  copy_round(3, GT(LD3), LY::Np(LD3));
   lbar();
   stamp();
   {  // S13: fcᵀ: dh = G_fc · W_fc → h_traj gradient (mask E3) and h_c gradient (+ decoder share, mask C1)
     const bf16x4 ht = masked(mm(GFC, wFCb[0]), ME3, n);
     *(bf16x4*)(A0 + ioff(n, q)) = ht;
-    arena4(L[LE3].gT, L[LE3].Np, n, b0, q, ht);
+    arena4(GT(LE3), LY::Np(LE3), n, b0, q, ht);
     f32x4 acc = mm(GFC, wFCb[1]);
     const f32x4 d2 = *(const f32x4*)(DHC2 + n * R + 4 * q);
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i] += d2[i];
     const bf16x4 hc = masked(acc, MC1, n);
     *(bf16x4*)(CB + ioff(n, q)) = hc;
-    arena4(L[LC1].gT, L[LC1].Np, n, b0, q, hc);
+    arena4(GT(LC1), LY::Np(LC1), n, b0, q, hc);
   }
-  copy_round(4, L[LD3].gT, L[LD3].Np);
+  copy_round(4, GT(LD3), LY::Np(LD3));
   lbar();
   stamp();
   {  // S14: E3ᵀ
     const bf16x4 h = masked(mm(A0, wE3b), ME2, n);
     *(bf16x4*)(A1 + ioff(n, q)) = h;
-    arena4(L[LE2].gT, L[LE2].Np, n, b0, q, h);
+    arena4(GT(LE2), LY::Np(LE2), n, b0, q, h);
   }
   lbar();
   stamp();
   {  // S15: E2ᵀ
     const bf16x4 h = masked(mm(A1, wE2b), ME1, n);
     *(bf16x4*)(A0 + ioff(n, q)) = h;
-    arena4(L[LE1].gT, L[LE1].Np, n, b0, q, h);
+    arena4(GT(LE1), LY::Np(LE1), n, b0, q, h);
   }
   lbar();
   stamp();
   {  // S16: E1ᵀ ‖ C1ᵀ: the last two gradients only feed the dW kernel
-    arena4(L[LE0].gT, L[LE0].Np, n, b0, q, masked(mm(A0, wE1b), ME0, n));
-    arena4(L[LC0].gT, L[LC0].Np, n, b0, q, masked(mm(CB, wC1b), MC0, n));
+    arena4(GT(LE0), LY::Np(LE0), n, b0, q, masked(mm(A0, wE1b), ME0, n));
+    arena4(GT(LC0), LY::Np(LC0), n, b0, q, masked(mm(CB, wC1b), MC0, n));
   }
 
   // ---- loss partial sums (deterministic order)
