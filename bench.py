@@ -199,6 +199,9 @@ def main():
         flop = {"rowchain": fl["rowchain"] * B, "wgrad": fl["wgrad"] * B, "wgrad_adam": fl["wgrad"] * B}
         nbytes = {"rowchain": bt["rowchain"] * B, "wgrad": bt["wgrad"] * B + 4 * n_par,
                   "wgrad_adam": bt["wgrad"] * B + ADAM_BYTES_PER_PARAM * n_par}
+        # the fused launch (one kernel per step: row chain + dW ⊕ Adam tiles)
+        flop["fused_step"] = flop["rowchain"] + flop["wgrad_adam"]
+        nbytes["fused_step"] = nbytes["rowchain"] + nbytes["wgrad_adam"]
         dom = max((k for k in kt if k in flop), key=lambda k: kt[k][0])
         traffic = measured_traffic(args.traffic_file, dom, B, args.dtype)
         roof = roofline(dom, kt[dom][0], flop[dom], nbytes[dom], args.dtype, traffic)

@@ -16,7 +16,7 @@
 #include "cvae_rowchain.h"
 #include "cvae_wgrad.h"
 #include "cvae_loss.h"
-#include "cvae_fastchain.h"
+#include "cvae_fastwgrad.h"
 
 namespace {
 
@@ -52,6 +52,8 @@ struct cvae_handle {
   std::vector<TileDesc> tiles;
   TileDesc* d_tiles = nullptr;
   char* arena = nullptr;    // weight copies + activations
+  unsigned* d_sync = nullptr;  // fused launch hand-off words (fchain::FusedArgs::sync), zero between launches
+  bool fused = false;          // training steps run as one fused_step_kernel launch
   int64_t arena_bytes = 0;
   float* d_partials = nullptr;
   int max_row_tiles = 0;
@@ -305,6 +307,7 @@ int alloc_arena(cvae_handle* h) {
   for (int l = 0; l < n.n_layers; ++l) maxnp = std::max(maxnp, std::max(n.L[l].Np, n.L[l].Kp));
   const int64_t zb_off = take((int64_t)maxnp * 4);
   const int64_t part_off = take((int64_t)h->max_row_tiles * 8 * 4);
+  const int64_t sync_off = take(256);
   const int64_t tile_off = take((int64_t)h->tiles.size() * sizeof(TileDesc));
   int64_t step_off[cvae_handle::ST_N];
   for (int m = 0; m < cvae_handle::ST_N; ++m) step_off[m] = take(64 * (int64_t)sizeof(StepDesc));
@@ -322,6 +325,7 @@ int alloc_arena(cvae_handle* h) {
   n.zbias = (const float*)(h->arena + zb_off);
   n.bias_all = (const float*)(h->arena + bias_base);
   h->d_partials = (float*)(h->arena + part_off);
+  h->d_sync = (unsigned*)(h->arena + sync_off);
   h->d_tiles = (TileDesc*)(h->arena + tile_off);
   HIPCK(hipMemcpy(h->d_tiles, h->tiles.data(), h->tiles.size() * sizeof(TileDesc), hipMemcpyHostToDevice));
   for (int m = 0; m < cvae_handle::ST_N; ++m) {
@@ -438,8 +442,21 @@ bool fast_layout_matches(const cvae_handle* h) {
       (const char*)n.bias_all != h->arena + LY::bias_base)
     return false;
   const int64_t Bp2 = 2 * (int64_t)n.Bp;
+  const int nt = (int)h->tiles.size();
+  if (nt != fchain::Tiles<NKI>::total()) return false;
+  for (int b = 0; b < nt; ++b) {
+    const TileDesc t = fchain::Tiles<NKI>::at(b);
+    if (t.layer != h->tiles[b].layer || t.o0 != h->tiles[b].o0 || t.i0 != h->tiles[b].i0) return false;
+  }
   for (int l = 0; l < LY::NL; ++l) {
     const LayerDev& L = n.L[l];
+    const LayerDev F = fchain::fast_layer<NKI>(l, h->arena, n.Bp, n.I);
+    if (F.K != L.K || F.N != L.N || F.Kp != L.Kp || F.Np != L.Np || F.relu != L.relu || F.nseg != L.nseg ||
+        F.seg_rows0 != L.seg_rows0 || F.Wf != L.Wf || F.Wb != L.Wb || F.bias != L.bias || F.xT != L.xT ||
+        F.gT != L.gT)
+      return false;
+    for (int g = 0; g < 2; ++g)
+      if (F.pw[g] != L.pw[g] || F.pb[g] != L.pb[g]) return false;
     if (L.Kp != LY::Kp(l) || L.Np != LY::Np(l) || n.bias_off[l] != LY::bias_off(l) ||
         (char*)L.Wf != h->arena + LY::wf(l) || (char*)L.Wb != h->arena + LY::wb(l) ||
         (char*)L.xT != h->arena + LY::act0 + Bp2 * LY::xrows(l) ||
@@ -464,9 +481,18 @@ int plan_fast(cvae_handle* h) {
     if (nki == 19 && !fast_layout_matches<19>(h)) return CVAE_OK;
     h->fast_nki = nki;
     h->fast_lds = lp.total;
-    if (nki == 19)
+    if (nki == 19) {
       HIPCK(hipFuncSetAttribute((const void*)fchain::fastchain_kernel<19>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lp.total));
+      HIPCK(hipFuncSetAttribute((const void*)fchain::fused_step_kernel<19>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lp.total));
+    }
+    // CVAE_FUSE=1: one fused_step_kernel launch per training step instead of two.  Correct, and
+    // measured slower at B = 1024 (32.1 vs 29.2 us per step): the chain's per-group drains and the
+    // waiting tiles' polls cost it ~3 us, and the encoder tiles (112 after the chain's last step)
+    // queue for CUs behind the decoder tiles — DESIGN.md §fused launch.
+    const char* fu = std::getenv("CVAE_FUSE");
+    h->fused = fu && fu[0] == '1';
   }
   return CVAE_OK;
 }
@@ -507,6 +533,53 @@ LossArgs make_loss(cvae_handle* h, const RowArgs& ra, float* loss_out, float* lo
 }
 
 int bk_of(cvae_handle*, int batch) { return rup_i(batch, 32); }
+
+// the dW (⊕ Adam) launch of a training step: the fast kernel for the fast configuration
+template <int MODE>
+int launch_wgrad(cvae_handle* h, int batch, const AdamArgs& aa, const LossArgs& la, hipStream_t s) {
+  const int nt = (int)h->tiles.size();
+  if (h->fast_nki == 19) {
+    hipLaunchKernelGGL((fchain::fastwgrad_kernel<19, MODE>), dim3(nt), dim3(WG_THREADS), 0, s,
+                       fchain::FastNet{h->arena, h->net.Bp, h->net.S, h->net.D, h->net.I}, bk_of(h, batch), aa, la);
+  } else if (h->cfg.dtype == CVAE_BF16) {
+    hipLaunchKernelGGL((wgrad_kernel<__bf16, MODE>), dim3(nt), dim3(WG_THREADS), 0, s, h->net, h->d_tiles,
+                       bk_of(h, batch), aa, la);
+  } else {
+    hipLaunchKernelGGL((wgrad_kernel<float, MODE>), dim3(nt), dim3(WG_THREADS), 0, s, h->net, h->d_tiles,
+                       bk_of(h, batch), aa, la);
+  }
+  HIPCK(hipGetLastError());
+  return CVAE_OK;
+}
+
+// one training step as a single fused_step_kernel launch (fast configuration, 16-B aligned x)
+int launch_fused(cvae_handle* h, const void* x, const int64_t* idx, int batch, const float* eps, uint64_t seed,
+                 uint64_t offset, const cvae_loss_weights* w, const AdamArgs& aa, float* loss_out,
+                 float* loss_accum, hipStream_t s) {
+  RowArgs ra{};
+  ra.x = x; ra.idx = idx; ra.batch = batch; ra.eps = eps; ra.seed = seed; ra.offset = offset;
+  ra.w_recon = w ? w->recon : 0.1f; ra.w_kld = w ? w->kld : 0.1f;
+  ra.w_start = w ? w->start : 1.0f; ra.w_time = w ? w->time : 1.0f;
+  ra.partials = h->d_partials;
+  ra.stamps = h->d_stamps;
+  fchain::FusedArgs f{};
+  f.aa = aa;
+  f.la = make_loss(h, ra, loss_out, loss_accum);
+  f.sync = h->d_sync;
+  f.Bk = bk_of(h, batch);
+  f.nchain = rup_i(batch, 32) / fchain::R;
+  const int nt = (int)h->tiles.size();
+  int rc = tmark(h, s, "fused_step");
+  if (rc) return rc;
+  hipLaunchKernelGGL(fchain::fused_step_kernel<19>, dim3(f.nchain + nt), dim3(fchain::NT), h->fast_lds, s,
+                     fchain::FastNet{h->arena, h->net.Bp, h->net.S, h->net.D, h->net.I}, ra, f);
+  HIPCK(hipGetLastError());
+  return tmark(h, s, "end");
+}
+
+bool use_fused(const cvae_handle* h, const void* x) {
+  return h->fused && h->fast_nki == 19 && (((uintptr_t)x) & 15) == 0;
+}
 
 }  // namespace
 
@@ -645,15 +718,8 @@ int cvae_train_fwd_bwd(cvae_handle* h, const void* x, const int64_t* idx, int ba
   AdamArgs aa{};
   aa.grads = grads;
   const LossArgs la = make_loss(h, ra, loss_out, loss_accum);
-  const int nt = (int)h->tiles.size();
   if ((rc = tmark(h, s, "wgrad"))) return rc;
-  if (h->cfg.dtype == CVAE_BF16)
-    hipLaunchKernelGGL((wgrad_kernel<__bf16, PM_GRAD>), dim3(nt), dim3(WG_THREADS), 0, s, h->net, h->d_tiles,
-                       bk_of(h, batch), aa, la);
-  else
-    hipLaunchKernelGGL((wgrad_kernel<float, PM_GRAD>), dim3(nt), dim3(WG_THREADS), 0, s, h->net, h->d_tiles,
-                       bk_of(h, batch), aa, la);
-  HIPCK(hipGetLastError());
+  if ((rc = launch_wgrad<PM_GRAD>(h, batch, aa, la, s))) return rc;
   return tmark(h, s, "end");
 }
 
@@ -684,21 +750,15 @@ int cvae_train_step(cvae_handle* h, const void* x, const int64_t* idx, int batch
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   tbegin(h);
+  AdamArgs aa = make_adam(params, nullptr, m, v, step, lr, beta1, beta2, adam_eps, 1.f);
+  if (use_fused(h, x)) return launch_fused(h, x, idx, batch, eps, seed, offset, w, aa, loss_out, loss_accum, s);
   RowArgs ra;
   rc = h->cfg.dtype == CVAE_BF16 ? train_fwd_bwd_impl<__bf16>(h, x, idx, batch, eps, seed, offset, w, s, ra)
                                  : train_fwd_bwd_impl<float>(h, x, idx, batch, eps, seed, offset, w, s, ra);
   if (rc) return rc;
-  AdamArgs aa = make_adam(params, nullptr, m, v, step, lr, beta1, beta2, adam_eps, 1.f);
   const LossArgs la = make_loss(h, ra, loss_out, loss_accum);
-  const int nt = (int)h->tiles.size();
   if ((rc = tmark(h, s, "wgrad_adam"))) return rc;
-  if (h->cfg.dtype == CVAE_BF16)
-    hipLaunchKernelGGL((wgrad_kernel<__bf16, PM_ADAM>), dim3(nt), dim3(WG_THREADS), 0, s, h->net, h->d_tiles,
-                       bk_of(h, batch), aa, la);
-  else
-    hipLaunchKernelGGL((wgrad_kernel<float, PM_ADAM>), dim3(nt), dim3(WG_THREADS), 0, s, h->net, h->d_tiles,
-                       bk_of(h, batch), aa, la);
-  HIPCK(hipGetLastError());
+  if ((rc = launch_wgrad<PM_ADAM>(h, batch, aa, la, s))) return rc;
   return tmark(h, s, "end");
 }
 
@@ -741,14 +801,7 @@ int cvae_bench_kernels(cvae_handle* h, const void* x, const int64_t* idx, int ba
                                         : train_fwd_bwd_impl<float>(h, x, idx, batch, nullptr, 1, r, &w, s, ra);
       } else if (which == 1) {
         AdamArgs aa = make_adam(params, nullptr, m, v, step0 + r, lr, b1, b2, ae, 1.f);
-        const int nt = (int)h->tiles.size();
-        if (h->cfg.dtype == CVAE_BF16)
-          hipLaunchKernelGGL((wgrad_kernel<__bf16, PM_ADAM>), dim3(nt), dim3(WG_THREADS), 0, s, h->net, h->d_tiles,
-                             bk_of(h, batch), aa, LossArgs{});
-        else
-          hipLaunchKernelGGL((wgrad_kernel<float, PM_ADAM>), dim3(nt), dim3(WG_THREADS), 0, s, h->net, h->d_tiles,
-                             bk_of(h, batch), aa, LossArgs{});
-        rc2 = hipGetLastError() == hipSuccess ? CVAE_OK : CVAE_E_HIP;
+        rc2 = launch_wgrad<PM_ADAM>(h, batch, aa, LossArgs{}, s);
       } else {
         rc2 = cvae_train_step(h, x, idx, batch, nullptr, 1, r, &w, params, m, v, step0 + r, lr, b1, b2, ae, nullptr,
                               nullptr, stream);
@@ -766,6 +819,13 @@ int cvae_bench_kernels(cvae_handle* h, const void* x, const int64_t* idx, int ba
   (void)hipEventDestroy(e1);
   h->timing = timing;
   return rc;
+}
+
+int cvae_sync_words(cvae_handle* h, unsigned* out) {
+  if (!h || !out) return fail(CVAE_E_INVALID, "null argument");
+  HIPCK(hipDeviceSynchronize());
+  HIPCK(hipMemcpy(out, h->d_sync, 5 * sizeof(unsigned), hipMemcpyDeviceToHost));
+  return CVAE_OK;
 }
 
 int cvae_loss(const float* recon, const float* x, const float* mu, const float* logvar, int batch, int seq_len,

@@ -157,7 +157,7 @@ __device__ __forceinline__ f32x4 from_bf4(bf16x4 h) {
 // rows b0 + 4q .. +3 of feature f of an arena matrix with Kf feature rows (aoff; b0 % 16 == 0):
 // the 16 features × 4 row quads of one wave instruction are 512 contiguous bytes
 #ifndef CVAE_ARENA_SC1
-#define CVAE_ARENA_SC1 0
+#define CVAE_ARENA_SC1 1
 #endif
 __device__ __forceinline__ void arena4(void* base, int Kf, int f, int b0, int q, bf16x4 h) {
   if (CVAE_DIAG_NOSTORE) return;
@@ -183,14 +183,21 @@ __device__ __forceinline__ f32x4 quad_t(f32x4 y) {
 
 __device__ __forceinline__ void lbar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// The row chain of batch tile `blk`.  pub (the fused launch, fused_step_kernel): after the steps
+// that finish a group of layers' arena rows, every wave drains its (sc1, write-through) stores,
+// the step barrier follows, and one lane adds 1 to pub[group] (agent scope) — the dW tiles of
+// those layers wait for all row tiles' adds.  Groups: 0 after S11 (D0 D1 D2), 1 after S13 (D3 FC
+// E3 C1), 2 at the end (E2 E1 E0 C0 and the loss partials).  Every weight load of the chain is
+// issued before S11, so the drain at group 0 also retires them: the tiles may then overwrite the
+// operand copies.
 template <int NKI>
-__global__ __launch_bounds__(NT) void fastchain_kernel(FastNet net, RowArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+__device__ __forceinline__ void chain_body(const FastNet& net, const RowArgs& a, char* smem, unsigned* pub,
+                                           int blk) {
   constexpr int Ip = NKI * 32, NG3 = NKI * 2;                 // D3 output n-tiles
   constexpr int G3 = (NG3 + NW - 1) / NW;                     // D3 n-tiles per wave (max)
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int n16 = lane & 15, q = lane >> 4;
-  const int b0 = blockIdx.x * R, nrows = max(0, min(R, a.batch - b0));
+  const int b0 = blk * R, nrows = max(0, min(R, a.batch - b0));
   const int Bp = net.Bp, S = net.S, D = net.D, I = net.I;
   using LY = Layout<NKI>;
   const Lds P = lds_layout(Ip, S, LY::nbias);
@@ -585,7 +592,9 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(FastNet net, RowArgs a) {
     arena4(GT(LD0), LY::Np(LD0), n, b0, q, h);
   }
   copy_round(2, GT(LD3), LY::Np(LD3));
+  if (pub) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   lbar();
+  if (pub && tid == 0) __hip_atomic_fetch_add(pub + 0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   stamp();
   {  // S12: D0ᵀ: [dz ‖ dh_c(decoder share)]; dz → KL/reparameterisation backward → G_fc
 #pragma unroll
@@ -632,7 +641,9 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(FastNet net, RowArgs a) {
     arena4(GT(LC1), LY::Np(LC1), n, b0, q, hc);
   }
   copy_round(4, GT(LD3), LY::Np(LD3));
+  if (pub) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   lbar();
+  if (pub && tid == 0) __hip_atomic_fetch_add(pub + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   stamp();
   {  // S14: E3ᵀ
     const bf16x4 h = masked(mm(A0, wE3b), ME2, n);
@@ -671,12 +682,24 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(FastNet net, RowArgs a) {
   if (tid < 5) {
     float s = 0.f;
     for (int w = 0; w < NW; ++w) s += PART[w * 8 + tid];
-    gst<float>(a.partials + blockIdx.x * 8 + tid, s);
+    __hip_atomic_store((unsigned*)(a.partials + blk * 8 + tid), __builtin_bit_cast(unsigned, s), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);  // sc1: read by a dW tile of the fused launch
+  }
+  if (pub) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lbar();
+    if (tid == 0) __hip_atomic_fetch_add(pub + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (CVAE_DIAG_STAMPS && a.stamps && tid < 64) {
     stamp();
-    gst<unsigned long long>(a.stamps + blockIdx.x * 64 + tid, tid < stamp_i ? STAMPS[tid] : 0ull);
+    gst<unsigned long long>(a.stamps + blk * 64 + tid, tid < stamp_i ? STAMPS[tid] : 0ull);
   }
+}
+
+template <int NKI>
+__global__ __launch_bounds__(NT) void fastchain_kernel(FastNet net, RowArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  chain_body<NKI>(net, a, smem, nullptr, blockIdx.x);
 }
 
 }  // namespace fchain

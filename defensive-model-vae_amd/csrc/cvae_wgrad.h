@@ -239,12 +239,17 @@ __device__ __forceinline__ void tile_epilogue(const LayerDev& L, int o0, int i0,
   store_operands<T, NTHR>(L, o0, i0, wt);
 }
 
-// called by one whole wave: lane-strided partial sums, then a fixed-order butterfly (deterministic)
+// called by one whole wave: lane-strided partial sums, then a fixed-order butterfly (deterministic).
+// SC1: the partials were handed over inside the launch (sc1 loads, fused_step_kernel).
+template <bool SC1 = false>
 __device__ void finish_loss(const LossArgs& l, int S, int D, int Z) {
   const int lane = threadIdx.x & 63;
   float s[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   for (int t = lane; t < l.ntiles; t += 64)
-    for (int k = 0; k < 5; ++k) s[k] += l.partials[t * 8 + k];
+    for (int k = 0; k < 5; ++k)
+      s[k] += SC1 ? __builtin_bit_cast(float, __hip_atomic_load((const unsigned*)(l.partials + t * 8 + k),
+                                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                  : l.partials[t * 8 + k];
   for (int k = 0; k < 5; ++k) s[k] = wave_sum(s[k]);
   if (lane != 0) return;
   const float B = (float)l.batch;
@@ -263,18 +268,18 @@ __device__ void finish_loss(const LossArgs& l, int S, int D, int Z) {
 // 8 waves per tile: the batch (K) is cut into 8 wave slices whose loads are all in flight at once
 constexpr int WG_NW = 8, WG_THREADS = 64 * WG_NW;
 
-template <typename T, int MODE>
-__global__ __launch_bounds__(WG_THREADS) void wgrad_kernel(NetDev net, const TileDesc* __restrict__ tiles,
-                                                           int Bk, AdamArgs aa, LossArgs la) {
+// One workgroup = tile td of layer L (loss_block: this workgroup also finishes the loss; S, D, Z:
+// its shape).  SC1: the arena rows were handed over inside the launch (fused_step_kernel): every
+// load of them is an sc1 buffer load.
+template <typename T, int MODE, bool SC1 = false>
+__device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td, int Bk, const AdamArgs& aa,
+                                           const LossArgs& la, bool loss_block, int S, int D, int Z) {
   using V = typename Op<T>::V;
   constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC;
   __shared__ __attribute__((aligned(16))) float red[WG_NW * 32 * WT_LD];
   __shared__ float dbp[WG_NW * 32];
-  const TileDesc td = tiles[blockIdx.x];
-  const LayerDev& L = net.L[td.layer];
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int r16 = lane & 15, kq = (lane >> 4) * EPL;
-  const int Bp = net.Bp;
   const T* G = (const T*)L.gT;
   const T* X = (const T*)L.xT;
   const bool bias_tile = td.i0 == 0;
@@ -296,25 +301,40 @@ __global__ __launch_bounds__(WG_THREADS) void wgrad_kernel(NetDev net, const Til
   for (int m = 0; m < 2; ++m) gp[m] = G + aoff(td.o0 + m * 16 + r16, kq, Kg);
 #pragma unroll
   for (int n = 0; n < 2; ++n) xp[n] = X + aoff(td.i0 + n * 16 + r16, kq, Kx);
-  (void)Bp;
   // this wave's chunks: c = wave + WG_NW*j; PF chunks of loads kept in flight
   const int nk = Bk / KC;
   const int nmine = nk > wave ? (nk - wave + WG_NW - 1) / WG_NW : 0;
   constexpr int PF = 4;
   V ga[PF][2], xb[PF][2];
+  __amdgpu_buffer_rsrc_t rg, rx;
+  if (SC1) {
+    rg = __builtin_amdgcn_make_buffer_rsrc((void*)G, (short)0, 0x7fffffff, 0x00020000);
+    rx = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, 0x7fffffff, 0x00020000);
+  }
   auto load = [&](int u, int j) {  // unconditional, clamped to this wave's last chunk
     const size_t ct = (size_t)(wave + WG_NW * min(j, nmine > 0 ? nmine - 1 : 0)) * (KC / 16) * 16;
+    if (SC1) {
 #pragma unroll
-    for (int m = 0; m < 2; ++m) ga[u][m] = gld<V>(gp[m] + ct * Kg);
+      for (int m = 0; m < 2; ++m)
+        ga[u][m] = __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(
+                                             rg, (int)((gp[m] + ct * Kg - G) * sizeof(T)), 0, 16));
 #pragma unroll
-    for (int n = 0; n < 2; ++n) xb[u][n] = gld<V>(xp[n] + ct * Kx);
+      for (int n = 0; n < 2; ++n)
+        xb[u][n] = __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(
+                                             rx, (int)((xp[n] + ct * Kx - X) * sizeof(T)), 0, 16));
+    } else {
+#pragma unroll
+      for (int m = 0; m < 2; ++m) ga[u][m] = gld<V>(gp[m] + ct * Kg);
+#pragma unroll
+      for (int n = 0; n < 2; ++n) xb[u][n] = gld<V>(xp[n] + ct * Kx);
+    }
   };
 #pragma unroll
   for (int u = 0; u < PF; ++u) load(u, u);
   // the master state the epilogue updates (independent of the gradient) behind the operand loads
   Pre4 st = {};
   if (tid < 256) st = load4<MODE>(L, td.o0 + o, td.i0 + i4, aa);
-  if (blockIdx.x == 0 && wave == WG_NW - 1 && la.partials) finish_loss(la, net.S, net.D, net.Z);
+  if (loss_block && wave == WG_NW - 1 && la.partials) finish_loss<SC1>(la, S, D, Z);
   for (int j0 = 0; j0 < nmine; j0 += PF) {
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
@@ -368,6 +388,14 @@ __global__ __launch_bounds__(WG_THREADS) void wgrad_kernel(NetDev net, const Til
   __syncthreads();
   WSTAMP(3);
 #endif
+}
+
+// generic configurations: tile descriptors and layer records from memory
+template <typename T, int MODE>
+__global__ __launch_bounds__(WG_THREADS) void wgrad_kernel(NetDev net, const TileDesc* __restrict__ tiles,
+                                                           int Bk, AdamArgs aa, LossArgs la) {
+  const TileDesc td = tiles[blockIdx.x];
+  wgrad_body<T, MODE>(net.L[td.layer], td, Bk, aa, la, blockIdx.x == 0, net.S, net.D, net.Z);
 }
 
 // Adam from a (reduced) gradient buffer, or repack of the operand copies.

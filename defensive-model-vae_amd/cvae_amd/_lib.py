@@ -52,6 +52,7 @@ _SIGS = {
                                    C.c_void_p]),
     "cvae_bench_kernels": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
                                      C.c_void_p, C.c_int, C.POINTER(C.c_float), C.c_void_p]),
+    "cvae_sync_words": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint)]),
     "cvae_loss": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
                             C.POINTER(CvaeLossWeights), C.c_void_p, C.c_void_p, C.c_void_p]),
     "cvae_set_timing": (C.c_int, [C.c_void_p, C.c_int]),

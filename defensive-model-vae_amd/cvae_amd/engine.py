@@ -307,6 +307,13 @@ class CVAEEngine:
         self.step_count += 2 * int(reps)
         return {"rowchain": ms[0], "wgrad_adam": ms[1], "step": ms[2]}
 
+    def sync_words(self):
+        """The fused launch's hand-off words (cvae_sync_words): [group0, group1, group2, finished
+        tiles, time-out flag], all 0 between launches."""
+        out = (C.c_uint * 5)()
+        check(lib().cvae_sync_words(self._h, out), "cvae_sync_words")
+        return list(out)
+
     def workspace_bytes(self):
         b = C.c_int64()
         check(lib().cvae_workspace_bytes(self._h, C.byref(b)))

@@ -184,6 +184,11 @@ int cvae_kernel_times(cvae_handle* h, char* names, int names_len, float* ms, int
 int cvae_bench_kernels(cvae_handle* h, const void* x, const int64_t* idx, int batch, int reps,
                        float* params, float* m, float* v, int step0, float* ms, void* stream);
 
+/* The five hand-off words of the fused training launch (three group counters, finished tiles, spin
+ * time-out flag), copied to `out` (host, 5 entries).  All zero between launches; a non-zero time-out
+ * flag means a tile gave up waiting (results of that step invalid).  Synchronises the device. */
+int cvae_sync_words(cvae_handle* h, unsigned* out);
+
 const char* cvae_last_error(void);
 int cvae_abi_version(void);
 

@@ -46,8 +46,21 @@ for i in range(k - 1):
     print(f"{names[i]:>14s} {i:2d}: median {np.median(d[:, i]) / 1000:7.3f} us   max {d[:, i].max() / 1000:7.3f} us")
 
 w = wbuf.view(NT, 4).cpu().numpy().astype(np.int64)
-nw = int((w[:, 0] > 0).sum())
-w = w[:nw]
+wid = np.nonzero(w[:, 0] > 0)[0]  # fused launch: tile blocks follow the row-chain blocks
+w = w[wid]
+nw = len(wid)
+if len(wid) and wid[0] > 0:
+    rel = lambda v: (v - t0) * 10 / 1000  # noqa: E731
+    print(f"fused: chain blocks end {rel(st[:, k - 1].min()):.2f}..{rel(st[:, k - 1].max()):.2f} us after the first"
+          f" chain stamp; tile work starts (pctl 0/25/50/75/100) "
+          f"{[round(rel(v), 2) for v in np.percentile(w[:, 0], [0, 25, 50, 75, 100])]}"
+          f", ends {[round(rel(v), 2) for v in np.percentile(w[:, 3], [0, 25, 50, 75, 100])]}")
+    for lo, hi, name in ((0, 52, "group0"), (52, 168, "group1"), (168, nw, "group2")):
+        g = w[lo:hi]
+        print(f"  {name} tiles {lo}..{hi - 1}: start {rel(g[:, 0].min()):.2f}..{rel(g[:, 0].max()):.2f}"
+              f"  end {rel(g[:, 3].min()):.2f}..{rel(g[:, 3].max()):.2f} us")
+if not nw:
+    sys.exit(0)
 rc_end = st[:, k - 1].max()
 print(f"wgrad: blocks={nw}; first entry {(w[:, 0].min() - rc_end) * 10 / 1000:.2f} us after the last row-chain stamp;"
       f" span {(w[:, 3].max() - w[:, 0].min()) * 10 / 1000:.2f} us")

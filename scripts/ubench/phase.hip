@@ -1,0 +1,215 @@
+// Microbenchmark (GPU box): one row-chain "step" structure in isolation, 64 workgroups, NSTEP steps
+// of a 16-row × 128 × 128 bf16 layer per workgroup, every step reading a fresh 32-KB weight block
+// (the same lines in every workgroup, 1 MB of distinct weights in all) and writing a 4-KB
+// activation block to global memory.
+//   A  (current design): 8 waves; each wave loads its own weight fragments into registers two
+//      steps ahead and stores its 8-B-per-lane results itself.
+//   B<L> (loader waves): 8 compute waves read weights from a 2-slot LDS ring; L extra loader waves
+//      stage the weights global→registers→LDS (LA steps ahead in registers) and copy each finished
+//      activation image LDS→global with 16-B stores.  Everyone meets at one s_barrier per step.
+// Prints ns per step (difference of two step counts: launch overhead cancels).
+#include <hip/hip_runtime.h>
+#include <cstdio>
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef short i16x8 __attribute__((ext_vector_type(8)));
+#define G __attribute__((address_space(1)))
+#define LDSP __attribute__((address_space(3)))
+
+constexpr int WSTEP = 32 * 1024;  // weight bytes per step per workgroup
+constexpr int NWSTEPS = 96;       // distinct weight blocks (3 MB: every step of a launch reads fresh lines)
+
+__device__ __forceinline__ void lbar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ __forceinline__ bf16x8 xfrag(const __bf16* img, int kc) {
+  const int lane = threadIdx.x & 63;
+  const int f = kc * 32 + 4 * (lane >> 4) + ((lane & 15) >> 2);
+  const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDSP i16x4*)(img + f * 16 + 4 * (lane & 3)));
+  const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDSP i16x4*)(img + (f + 16) * 16 + 4 * (lane & 3)));
+  const i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// ---- A: current design.  MODE bit0: no weight loads, bit1: no global stores; NB register sets
+// (weights loaded NB-1 steps ahead)
+template <int MODE, int NB>
+__global__ __launch_bounds__(512) void kA(const __bf16* W, __bf16* out, int nstep) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  auto img = [&](int i) { return (__bf16*)(smem + (i & 1) * 4096); };
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, n16 = lane & 15, q = lane >> 4;
+  const int n = wave * 16 + n16;
+  if (tid < 512) ((u32x4*)smem)[tid] = u32x4{0, 0, 0, 0};
+  bf16x8 w[NB][4];
+  auto wl = [&](bf16x8* wr, int s) {
+    const __bf16* p = W + (size_t)(s % NWSTEPS) * (WSTEP / 2) + ((size_t)wave * 4 * 64 + lane) * 8;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) wr[c] = (MODE & 1) ? bf16x8{} : *(const G bf16x8*)(p + c * 512);
+  };
+#pragma unroll
+  for (int b = 0; b < NB - 1; ++b) wl(w[b], b);
+  lbar();
+  for (int s0 = 0; s0 < nstep; s0 += NB) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int s = s0 + b;
+      const __bf16* in = img(s);
+      __bf16* o = img(s + 1);
+      if (MODE & 4) wl(w[(b + NB - 1) % NB], s + NB - 1);  // issue first: overlaps this step's compute?
+      bf16x8 x[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) x[c] = xfrag(in, c);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[c], w[b][c], acc, 0, 0, 0);
+      bf16x4 h;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) h[i] = (__bf16)fmaxf(acc[i] * 0.01f, 0.f);
+      *(bf16x4*)(o + n * 16 + 4 * q) = h;
+      if (!(MODE & 2)) *(G bf16x4*)(out + ((size_t)blockIdx.x * nstep + s) * 2048 + n * 16 + 4 * q) = h;
+      if (!(MODE & 4)) wl(w[(b + NB - 1) % NB], s + NB - 1);
+      lbar();
+    }
+  }
+}
+
+// ---- B: loader waves
+template <int L, int LA>
+__global__ __launch_bounds__(64 * (8 + L)) void kB(const __bf16* W, __bf16* out, int nstep) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* ring = smem + 8192;  // 2 × 32 KB
+  auto img = [&](int i) { return (__bf16*)(smem + (i & 1) * 4096); };
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid < 512) ((u32x4*)smem)[tid] = u32x4{0, 0, 0, 0};
+  constexpr int FPW = WSTEP / 1024 / L;  // fragments per loader wave per step
+  if (wave >= 8) {
+    const int lw = wave - 8;
+    u32x4 r[LA][FPW];
+    auto gl = [&](u32x4* d, int s) {
+      const char* p = (const char*)W + (size_t)(s % NWSTEPS) * WSTEP + (size_t)lw * FPW * 1024 + lane * 16;
+#pragma unroll
+      for (int f = 0; f < FPW; ++f) d[f] = *(const G u32x4*)(p + f * 1024);
+    };
+    auto dw = [&](const u32x4* d, int s) {
+      char* p = ring + (s & 1) * WSTEP + lw * FPW * 1024 + lane * 16;
+#pragma unroll
+      for (int f = 0; f < FPW; ++f) *(u32x4*)(p + f * 1024) = d[f];
+    };
+    // prologue: slot 0 filled, steps 1..LA in registers
+    gl(r[0], 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    dw(r[0], 0);
+#pragma unroll
+    for (int a = 0; a < LA; ++a) gl(r[a], 1 + a);
+    lbar();
+    for (int s0 = 0; s0 < nstep; s0 += LA) {
+#pragma unroll
+      for (int a = 0; a < LA; ++a) {
+        const int s = s0 + a;
+        // step s: write weights of step s+1 (oldest registers) into the free slot, reload them
+        // with step s+1+LA, copy the image finished in step s-1 (img(s)) to global
+        if (LA == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else if (LA == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(FPW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * FPW) : "memory");
+        dw(r[a], s + 1);
+        gl(r[a], s + 1 + LA);
+        if (s > 0) {
+          const int e = lw * 64 + lane;  // 16-B pieces of the 4-KB image: 256
+          if (e < 256) {
+            const u32x4 v = *(const u32x4*)((const char*)img(s) + e * 16);
+            *(G u32x4*)((char*)out + (((size_t)blockIdx.x * nstep + s - 1) * 2048) * 2 + e * 16) = v;
+          }
+        }
+        lbar();
+      }
+    }
+    return;
+  }
+  const int n16 = lane & 15, q = lane >> 4, n = wave * 16 + n16;
+  lbar();
+  for (int s = 0; s < nstep; ++s) {
+    const __bf16* in = img(s);
+    __bf16* o = img(s + 1);
+    const char* slot = ring + (s & 1) * WSTEP + wave * 4 * 1024 + lane * 16;
+    bf16x8 x[4], w[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) w[c] = *(const bf16x8*)(slot + c * 1024);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) x[c] = xfrag(in, c);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[c], w[c], acc, 0, 0, 0);
+    bf16x4 h;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h[i] = (__bf16)fmaxf(acc[i] * 0.01f, 0.f);
+    *(bf16x4*)(o + n * 16 + 4 * q) = h;
+    lbar();
+  }
+}
+
+// rewrites the weights from 256 workgroups (as the dW/Adam kernel does between row-chain launches):
+// the next launch finds them in no L2
+__global__ void rewrite(u32x4* W, int n16, unsigned v) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += gridDim.x * blockDim.x) W[i] = u32x4{v, v, v, v};
+}
+
+template <typename F>
+float timeit(F launch) {
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  for (int w = 0; w < 3; ++w) launch();
+  const int reps = 30;
+  hipEventRecord(a);
+  for (int r = 0; r < reps; ++r) launch();
+  hipEventRecord(b);
+  hipEventSynchronize(b);
+  float ms;
+  hipEventElapsedTime(&ms, a, b);
+  return ms * 1e6f / reps;  // ns per launch
+}
+
+int main() {
+  __bf16 *W, *out;
+  hipMalloc(&W, (size_t)WSTEP * NWSTEPS);
+  hipMalloc(&out, (size_t)64 * 96 * 4096);
+  hipMemset(W, 0, (size_t)WSTEP * NWSTEPS);
+  bool cold = false;
+  auto per_step = [&](const char* name, auto launch) {
+    auto l2 = [&](int s) {
+      if (cold) hipLaunchKernelGGL(rewrite, dim3(256), dim3(256), 0, 0, (u32x4*)W, WSTEP * NWSTEPS / 16, 0u);
+      launch(s);
+    };
+    const float t24 = timeit([&] { l2(24); }), t96 = timeit([&] { l2(96); });
+    printf("%-24s %s %7.1f ns/step   (24-step launch %8.1f ns)\n", name, cold ? "cold" : "warm", (t96 - t24) / 72.f, t24);
+  };
+  hipFuncSetAttribute((const void*)kB<2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 8192 + 2 * WSTEP);
+  hipFuncSetAttribute((const void*)kB<4, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 8192 + 2 * WSTEP);
+  hipFuncSetAttribute((const void*)kB<4, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 8192 + 2 * WSTEP);
+  hipFuncSetAttribute((const void*)kB<4, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, 8192 + 2 * WSTEP);
+  hipFuncSetAttribute((const void*)kB<8, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 8192 + 2 * WSTEP);
+  const int sh = 8192 + 2 * WSTEP;
+  for (int c = 0; c < 2; ++c) {
+    cold = c == 1;
+    per_step("A LA=1", [&](int s) { hipLaunchKernelGGL((kA<0, 2>), dim3(64), dim3(512), 8192, 0, W, out, s); });
+    per_step("A LA=2", [&](int s) { hipLaunchKernelGGL((kA<0, 3>), dim3(64), dim3(512), 8192, 0, W, out, s); });
+    per_step("A LA=3", [&](int s) { hipLaunchKernelGGL((kA<0, 4>), dim3(64), dim3(512), 8192, 0, W, out, s); });
+    per_step("A LA=5", [&](int s) { hipLaunchKernelGGL((kA<0, 6>), dim3(64), dim3(512), 8192, 0, W, out, s); });
+    per_step("A LA=2 issue first", [&](int s) { hipLaunchKernelGGL((kA<4, 3>), dim3(64), dim3(512), 8192, 0, W, out, s); });
+    per_step("A LA=3 issue first", [&](int s) { hipLaunchKernelGGL((kA<4, 4>), dim3(64), dim3(512), 8192, 0, W, out, s); });
+    per_step("A LA=2 issue first no st", [&](int s) { hipLaunchKernelGGL((kA<6, 3>), dim3(64), dim3(512), 8192, 0, W, out, s); });
+    per_step("A LA=2 no stores", [&](int s) { hipLaunchKernelGGL((kA<2, 3>), dim3(64), dim3(512), 8192, 0, W, out, s); });
+    per_step("A LA=2 no loads", [&](int s) { hipLaunchKernelGGL((kA<1, 3>), dim3(64), dim3(512), 8192, 0, W, out, s); });
+    per_step("A no loads no stores", [&](int s) { hipLaunchKernelGGL((kA<3, 3>), dim3(64), dim3(512), 8192, 0, W, out, s); });
+    if (c == 1 || c == 0) continue;
+    per_step("B L=2 LA=1", [&](int s) { hipLaunchKernelGGL((kB<2, 1>), dim3(64), dim3(640), sh, 0, W, out, s); });
+    per_step("B L=4 LA=1", [&](int s) { hipLaunchKernelGGL((kB<4, 1>), dim3(64), dim3(768), sh, 0, W, out, s); });
+    per_step("B L=4 LA=2", [&](int s) { hipLaunchKernelGGL((kB<4, 2>), dim3(64), dim3(768), sh, 0, W, out, s); });
+    per_step("B L=4 LA=3", [&](int s) { hipLaunchKernelGGL((kB<4, 3>), dim3(64), dim3(768), sh, 0, W, out, s); });
+    per_step("B L=8 LA=2", [&](int s) { hipLaunchKernelGGL((kB<8, 2>), dim3(64), dim3(1024), sh, 0, W, out, s); });
+  }
+  return 0;
+}

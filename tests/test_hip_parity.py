@@ -332,3 +332,27 @@ def test_train_steps_equals_repeated_train_step(cvae):
         torch.cuda.synchronize()
         assert torch.equal(e1.params, e2.params), dtype
         assert torch.equal(e1.loss, e2.loss) and torch.equal(e1.loss_accum, e2.loss_accum), dtype
+
+
+def test_fused_step_equals_two_launch_step(cvae, monkeypatch):
+    """The fused training launch (row chain and dW ⊕ Adam tiles in one kernel, hand-off through
+    counters; CVAE_FUSE=1 at handle creation) == the two-launch step, bit for bit over several
+    steps, ragged batch included; the hand-off counters come back to zero after every launch."""
+    S, D = 100, 6
+    torch.manual_seed(0)
+    ref = OracleCVAE(S, D, 8)
+    monkeypatch.delenv("CVAE_FUSE", raising=False)
+    m1, e1 = _model(cvae, S, D, 8, sd=ref.state_dict(), dtype="bf16", max_batch=200)
+    monkeypatch.setenv("CVAE_FUSE", "1")
+    m2, e2 = _model(cvae, S, D, 8, sd=ref.state_dict(), dtype="bf16", max_batch=200)
+    monkeypatch.delenv("CVAE_FUSE")
+    data = torch.randn(400, S, D).cuda()
+    for i, B in enumerate((200, 200, 77, 160)):
+        idx = torch.randint(0, 400, (B,), generator=torch.Generator().manual_seed(i)).cuda()
+        e1.train_step(data, idx=idx)
+        e2.train_step(data, idx=idx)
+        torch.cuda.synchronize()
+        assert torch.equal(e1.params, e2.params), B
+        assert torch.equal(e1.m, e2.m) and torch.equal(e1.v, e2.v), B
+        assert torch.equal(e1.loss, e2.loss) and torch.equal(e1.loss_accum, e2.loss_accum), B
+    assert e2.sync_words() == [0, 0, 0, 0, 0]
