@@ -128,6 +128,8 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-b2b", action="store_true",
+                    help="skip the back-to-back single-kernel pass (profiling runs: rocprof then sees step launches only)")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="per-launch HBM traffic from rocprofv3 --pmc passes (scripts/pmc_traffic.py)")
     args = ap.parse_args()
@@ -183,7 +185,7 @@ def main():
     eng.set_timing(False)
     # each kernel alone, launched back-to-back (cvae_bench_kernels): the step's kernels without
     # their neighbours' cache/instruction-cache effects
-    b2b = eng.bench_kernels(x, max(args.steps, 20), batch=B)
+    b2b = None if args.no_b2b else eng.bench_kernels(x, max(args.steps, 20), batch=B)
     if world > 1:
         tt = torch.tensor([t], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -206,7 +208,8 @@ def main():
         traffic = measured_traffic(args.traffic_file, dom, B, args.dtype)
         roof = roofline(dom, kt[dom][0], flop[dom], nbytes[dom], args.dtype, traffic)
         roof["kernels_ms"] = {k: round(v[0], 5) for k, v in kt.items()}
-        roof["kernels_back_to_back_ms"] = {k: round(v, 5) for k, v in b2b.items()}
+        if b2b:
+            roof["kernels_back_to_back_ms"] = {k: round(v, 5) for k, v in b2b.items()}
         value = world * B * args.steps / t
         res = {"metric": "trajectories/sec per ELBO step, batch=1024 seq_len=100; 1/2/4/8 MI355X",
                "value": round(value, 1), "unit": "trajectories/s", "n_gpus": world, "steps": args.steps,

@@ -1,6 +1,7 @@
 // cvae_capi.hip — host side of the C-ABI (include/cvae.h): planning, workspace,
 // launches.  All launches go to the caller's stream; nothing here synchronises.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cmath>
 #include <cstdio>
@@ -72,7 +73,7 @@ struct cvae_handle {
   int n_used = 0;
   struct Seg { int e0, e1; std::string name; };
   std::vector<Seg> segs;
-  int call_last = -1;
+  const char* pending = nullptr;  // name of the next timed launch (tmark)
 };
 
 namespace {
@@ -367,24 +368,36 @@ int set_lds_attrs(cvae_handle* h) {
   return CVAE_OK;
 }
 
-// ---- timing helpers (events on the caller's stream; no syncs)
-void tbegin(cvae_handle* h) { h->call_last = -1; }
-int tmark(cvae_handle* h, hipStream_t s, const char* name) {
-  if (!h->timing) return CVAE_OK;
+// ---- timing helpers (no syncs).  With timing on, tmark(name) names the next kernel launch and
+// klaunch records that launch's own start/end timestamps (hipExtLaunchKernelGGL's event pair: the
+// dispatch packet's begin/end, the interval rocprofv3's kernel trace reports) — events recorded
+// between kernels would add the dispatch gap and their own overhead to every duration.
+void tbegin(cvae_handle* h) { h->pending = nullptr; }
+int tmark(cvae_handle* h, hipStream_t, const char* name) {
+  h->pending = (h->timing && std::strcmp(name, "end") != 0) ? name : nullptr;
+  return CVAE_OK;
+}
+int tevent(cvae_handle* h) {
   if (h->n_used >= (int)h->pool.size()) {
     hipEvent_t e;
-    HIPCK(hipEventCreate(&e));
+    if (hipEventCreate(&e) != hipSuccess) return -1;
     h->pool.push_back(e);
   }
-  const int id = h->n_used++;
-  HIPCK(hipEventRecord(h->pool[id], s));
-  if (h->call_last >= 0) h->segs.back().e1 = id;
-  if (std::strcmp(name, "end") != 0) {
-    h->segs.push_back({id, -1, name});
-    h->call_last = id;
+  return h->n_used++;
+}
+template <typename... KArgs, typename... Args>
+int klaunch(cvae_handle* h, void (*kernel)(KArgs...), dim3 grid, dim3 block, size_t shm, hipStream_t s,
+            Args... args) {
+  if (h->timing && h->pending) {
+    const int e0 = tevent(h), e1 = tevent(h);
+    if (e0 < 0 || e1 < 0) return fail(CVAE_E_HIP, "hipEventCreate failed");
+    hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)shm, s, h->pool[e0], h->pool[e1], 0, args...);
+    h->segs.push_back({e0, e1, h->pending});
+    h->pending = nullptr;
   } else {
-    h->call_last = -1;
+    hipLaunchKernelGGL(kernel, grid, block, shm, s, args...);
   }
+  HIPCK(hipGetLastError());
   return CVAE_OK;
 }
 
@@ -400,9 +413,7 @@ int launch_rowchain(cvae_handle* h, RowArgs a, hipStream_t s) {
   a.steps = h->d_steps[st];
   a.nsteps = h->n_steps[st];
   a.stamps = h->d_stamps;
-  hipLaunchKernelGGL((rowchain_kernel<T, R, MODE>), dim3(grid), dim3(RC_THREADS), h->lds_bytes, s, h->net, a);
-  HIPCK(hipGetLastError());
-  return CVAE_OK;
+  return klaunch(h, rowchain_kernel<T, R, MODE>, dim3(grid), dim3(RC_THREADS), h->lds_bytes, s, h->net, a);
 }
 
 int check_batch(cvae_handle* h, int batch) {
@@ -513,11 +524,8 @@ int train_fwd_bwd_impl(cvae_handle* h, const void* x, const int64_t* idx, int ba
     ra.nsteps = h->n_steps[cvae_handle::ST_TRAIN];
     ra.stamps = h->d_stamps;
     const int grid = rup_i(batch, 32) / fchain::R;
-    if (h->fast_nki == 19)
-      hipLaunchKernelGGL(fchain::fastchain_kernel<19>, dim3(grid), dim3(fchain::NT), h->fast_lds, s,
-                         fchain::FastNet{h->arena, h->net.Bp, h->net.S, h->net.D, h->net.I}, ra);
-    HIPCK(hipGetLastError());
-    return CVAE_OK;
+    return klaunch(h, fchain::fastchain_kernel<19>, dim3(grid), dim3(fchain::NT), h->fast_lds, s,
+                   fchain::FastNet{h->arena, h->net.Bp, h->net.S, h->net.D, h->net.I}, ra);
   }
   return launch_rowchain<T, RC_TRAIN>(h, ra, s);
 }
@@ -538,18 +546,14 @@ int bk_of(cvae_handle*, int batch) { return rup_i(batch, 32); }
 template <int MODE>
 int launch_wgrad(cvae_handle* h, int batch, const AdamArgs& aa, const LossArgs& la, hipStream_t s) {
   const int nt = (int)h->tiles.size();
-  if (h->fast_nki == 19) {
-    hipLaunchKernelGGL((fchain::fastwgrad_kernel<19, MODE>), dim3(nt), dim3(WG_THREADS), 0, s,
-                       fchain::FastNet{h->arena, h->net.Bp, h->net.S, h->net.D, h->net.I}, bk_of(h, batch), aa, la);
-  } else if (h->cfg.dtype == CVAE_BF16) {
-    hipLaunchKernelGGL((wgrad_kernel<__bf16, MODE>), dim3(nt), dim3(WG_THREADS), 0, s, h->net, h->d_tiles,
-                       bk_of(h, batch), aa, la);
-  } else {
-    hipLaunchKernelGGL((wgrad_kernel<float, MODE>), dim3(nt), dim3(WG_THREADS), 0, s, h->net, h->d_tiles,
-                       bk_of(h, batch), aa, la);
-  }
-  HIPCK(hipGetLastError());
-  return CVAE_OK;
+  if (h->fast_nki == 19)
+    return klaunch(h, fchain::fastwgrad_kernel<19, MODE>, dim3(nt), dim3(WG_THREADS), 0, s,
+                   fchain::FastNet{h->arena, h->net.Bp, h->net.S, h->net.D, h->net.I}, bk_of(h, batch), aa, la);
+  if (h->cfg.dtype == CVAE_BF16)
+    return klaunch(h, wgrad_kernel<__bf16, MODE>, dim3(nt), dim3(WG_THREADS), 0, s, h->net,
+                   (const TileDesc*)h->d_tiles, bk_of(h, batch), aa, la);
+  return klaunch(h, wgrad_kernel<float, MODE>, dim3(nt), dim3(WG_THREADS), 0, s, h->net,
+                 (const TileDesc*)h->d_tiles, bk_of(h, batch), aa, la);
 }
 
 // one training step as a single fused_step_kernel launch (fast configuration, 16-B aligned x)
@@ -571,10 +575,8 @@ int launch_fused(cvae_handle* h, const void* x, const int64_t* idx, int batch, c
   const int nt = (int)h->tiles.size();
   int rc = tmark(h, s, "fused_step");
   if (rc) return rc;
-  hipLaunchKernelGGL(fchain::fused_step_kernel<19>, dim3(f.nchain + nt), dim3(fchain::NT), h->fast_lds, s,
-                     fchain::FastNet{h->arena, h->net.Bp, h->net.S, h->net.D, h->net.I}, ra, f);
-  HIPCK(hipGetLastError());
-  return tmark(h, s, "end");
+  return klaunch(h, fchain::fused_step_kernel<19>, dim3(f.nchain + nt), dim3(fchain::NT), h->fast_lds, s,
+                 fchain::FastNet{h->arena, h->net.Bp, h->net.S, h->net.D, h->net.I}, ra, f);
 }
 
 bool use_fused(const cvae_handle* h, const void* x) {
@@ -719,8 +721,7 @@ int cvae_train_fwd_bwd(cvae_handle* h, const void* x, const int64_t* idx, int ba
   aa.grads = grads;
   const LossArgs la = make_loss(h, ra, loss_out, loss_accum);
   if ((rc = tmark(h, s, "wgrad"))) return rc;
-  if ((rc = launch_wgrad<PM_GRAD>(h, batch, aa, la, s))) return rc;
-  return tmark(h, s, "end");
+  return launch_wgrad<PM_GRAD>(h, batch, aa, la, s);
 }
 
 int cvae_adam(cvae_handle* h, float* params, const float* grads, float* m, float* v, int step, float lr,
@@ -733,11 +734,10 @@ int cvae_adam(cvae_handle* h, float* params, const float* grads, float* m, float
   int rc = tmark(h, s, "adam");
   if (rc) return rc;
   if (h->cfg.dtype == CVAE_BF16)
-    hipLaunchKernelGGL((param_kernel<__bf16, PM_ADAM>), dim3(nt), dim3(CVAE_THREADS), 0, s, h->net, h->d_tiles, aa);
-  else
-    hipLaunchKernelGGL((param_kernel<float, PM_ADAM>), dim3(nt), dim3(CVAE_THREADS), 0, s, h->net, h->d_tiles, aa);
-  HIPCK(hipGetLastError());
-  return tmark(h, s, "end");
+    return klaunch(h, param_kernel<__bf16, PM_ADAM>, dim3(nt), dim3(CVAE_THREADS), 0, s, h->net,
+                   (const TileDesc*)h->d_tiles, aa);
+  return klaunch(h, param_kernel<float, PM_ADAM>, dim3(nt), dim3(CVAE_THREADS), 0, s, h->net,
+                 (const TileDesc*)h->d_tiles, aa);
 }
 
 int cvae_train_step(cvae_handle* h, const void* x, const int64_t* idx, int batch, const float* eps, uint64_t seed,
@@ -758,8 +758,7 @@ int cvae_train_step(cvae_handle* h, const void* x, const int64_t* idx, int batch
   if (rc) return rc;
   const LossArgs la = make_loss(h, ra, loss_out, loss_accum);
   if ((rc = tmark(h, s, "wgrad_adam"))) return rc;
-  if ((rc = launch_wgrad<PM_ADAM>(h, batch, aa, la, s))) return rc;
-  return tmark(h, s, "end");
+  return launch_wgrad<PM_ADAM>(h, batch, aa, la, s);
 }
 
 int cvae_train_steps(cvae_handle* h, const void* x, const int64_t* idx, int batch, int n_steps, const float* eps,
@@ -872,7 +871,7 @@ int cvae_set_timing(cvae_handle* h, int enabled) {
   h->timing = enabled != 0;
   h->segs.clear();
   h->n_used = 0;
-  h->call_last = -1;
+  h->pending = nullptr;
   return CVAE_OK;
 }
 
