@@ -547,7 +547,7 @@ template <int MODE>
 int launch_wgrad(cvae_handle* h, int batch, const AdamArgs& aa, const LossArgs& la, hipStream_t s) {
   const int nt = (int)h->tiles.size();
   if (h->fast_nki == 19)
-    return klaunch(h, fchain::fastwgrad_kernel<19, MODE>, dim3(nt), dim3(WG_THREADS), 0, s,
+    return klaunch(h, fchain::fastwgrad_kernel<19, MODE>, dim3(nt + 1), dim3(WG_THREADS), 0, s,
                    fchain::FastNet{h->arena, h->net.Bp, h->net.S, h->net.D, h->net.I}, bk_of(h, batch), aa, la);
   if (h->cfg.dtype == CVAE_BF16)
     return klaunch(h, wgrad_kernel<__bf16, MODE>, dim3(nt), dim3(WG_THREADS), 0, s, h->net,

@@ -487,45 +487,70 @@ __device__ __forceinline__ void chain_body(const FastNet& net, const RowArgs& a,
   lbar();
   stamp();
   {  // S8: D3 + conditional_vae_loss (:229-268) + dL/drecon, over x_rel in place
-    const float inv_D = 1.f / (float)D;
+    // the A operand is read once for all of this wave's n-tiles, whose MFMA chains interleave;
+    // n-tile g exists for every wave while NW·(g+1) <= NG3 (compile-time), else for waves < NG3 − NW·g
+    auto has = [&](int g) { return NW * (g + 1) <= NG3 || wave + NW * g < NG3; };
+    bf16x8 xa[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) xa[c] = xfrag(A0, c);
+    f32x4 accs[G3];
+#pragma unroll
+    for (int g = 0; g < G3; ++g) accs[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int g = 0; g < G3; ++g)
+        if (has(g)) accs[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[c], wD3[g][c], accs[g], 0, 0, 0);
+    typedef float f32x2 __attribute__((ext_vector_type(2)));  // packed fp32 (v_pk_*) epilogue
+    const float inv_D = 1.f / (float)D, cr = a.w_recon * 2.f;
+    f32x2 sr2 = {0.f, 0.f};
 #pragma unroll
     for (int g = 0; g < G3; ++g) {
+      if (!has(g)) continue;
       const int t = wave + NW * g;
-      if (t < NG3) {
-        const f32x4 acc = mm(A0, wD3[g]);
-        const int f = 16 * t + n16;
-        f32x4 gi = {0.f, 0.f, 0.f, 0.f};
-        if (f < I) {
-          const float b = bias(LD3, f);
-          const f32x4 xr = from_bf4(*(const bf16x4*)(XIN + ioff(f, q)));
-          const int s = fdiv(f, inv_D), d = f - s * D;
-          f32x4 r;
+      const f32x4 acc = accs[g];
+      const int f = 16 * t + n16;
+      f32x4 gi = {0.f, 0.f, 0.f, 0.f};
+      if (f < I) {
+        const float b = bias(LD3, f);
+        const f32x4 xr = from_bf4(*(const bf16x4*)(XIN + ioff(f, q)));
+        const int s = fdiv(f, inv_D), d = f - s * D;
+        const f32x2 r01 = f32x2{acc[0], acc[1]} + b, r23 = f32x2{acc[2], acc[3]} + b;
+        f32x2 d01 = r01 - f32x2{xr[0], xr[1]}, d23 = r23 - f32x2{xr[2], xr[3]};
+        if (nrows < R) {  // wave-uniform: the batch's last tile; rows past it add nothing
+          d01[0] = 4 * q + 0 < nrows ? d01[0] : 0.f;
+          d01[1] = 4 * q + 1 < nrows ? d01[1] : 0.f;
+          d23[0] = 4 * q + 2 < nrows ? d23[0] : 0.f;
+          d23[1] = 4 * q + 3 < nrows ? d23[1] : 0.f;
+        }
+        sr2 += d01 * d01;
+        sr2 += d23 * d23;
+        const f32x2 g01 = d01 * cr * inv_BSD, g23 = d23 * cr * inv_BSD;  // w_recon·2·diff / (B·S·D)
+        gi = f32x4{g01[0], g01[1], g23[0], g23[1]};
+        const f32x4 r = {r01[0], r01[1], r23[0], r23[1]};
+        if (16 * t < D) {  // wave-uniform: only these n-tiles hold timestep-0 features
+          const f32x4 df = {d01[0], d01[1], d23[0], d23[1]};
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const bool live = 4 * q + i < nrows;
-            r[i] = acc[i] + b;
-            const float diff = r[i] - xr[i];
-            if (!live) continue;
-            s_recon += diff * diff;
-            float gg = a.w_recon * 2.f * diff * inv_BSD;
+            if (4 * q + i >= nrows) continue;
             if (s == 0 && (d == 1 || d == 2) && use_start) {
-              s_start += diff * diff;
-              gg += a.w_start * 2.f * diff * inv_2B;
+              s_start += df[i] * df[i];
+              gi[i] += a.w_start * 2.f * df[i] * inv_2B;
             }
             if (d == 0 && s == 0 && use_time) {
               s_t0 += r[i] * r[i];
-              gg += a.w_time * 2.f * r[i] * inv_B;
+              gi[i] += a.w_time * 2.f * r[i] * inv_B;
             }
-            gi[i] = gg;
-          }
-          if (d == 0) {
-            *(f32x4*)(RCH0 + s * R + 4 * q) = r;
-            *(f32x4*)(GD0 + s * R + 4 * q) = gi;
           }
         }
-        *(bf16x4*)(XIN + ioff(f, q)) = to_bf4(gi);  // pad features f >= I: 0
+        if (d == 0) {
+          *(f32x4*)(RCH0 + s * R + 4 * q) = r;
+          *(f32x4*)(GD0 + s * R + 4 * q) = gi;
+        }
       }
+      *(bf16x4*)(XIN + ioff(f, q)) = to_bf4(gi);  // pad features f >= I: 0
     }
+    s_recon += sr2[0] + sr2[1];
   }
   wload(wD2b, Wb(LD2), H, wave);
   wload(wD1b, Wb(LD1), H, wave);

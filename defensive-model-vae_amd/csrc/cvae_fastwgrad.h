@@ -119,9 +119,13 @@ __host__ __device__ inline LayerDev fast_layer(int l, char* arena, int Bp, int I
 
 template <int NKI, int MODE>
 __global__ __launch_bounds__(WG_THREADS) void fastwgrad_kernel(FastNet fn, int Bk, AdamArgs aa, LossArgs la) {
+  if ((int)blockIdx.x == Tiles<NKI>::total()) {  // one extra block finishes the loss beside the tiles
+    if (threadIdx.x < 64 && la.partials) finish_loss(la, fn.S, fn.D, Z);
+    return;
+  }
   const TileDesc td = Tiles<NKI>::at(blockIdx.x);
   const LayerDev L = fast_layer<NKI>(td.layer, fn.arena, fn.Bp, fn.I);
-  wgrad_body<__bf16, MODE>(L, td, Bk, aa, la, blockIdx.x == 0, fn.S, fn.D, Z);
+  wgrad_body<__bf16, MODE>(L, td, Bk, aa, la, false, fn.S, fn.D, Z);
 }
 
 // ---------------------------------------------------------------- the fused training step

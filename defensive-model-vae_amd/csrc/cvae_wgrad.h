@@ -40,7 +40,7 @@ enum { PM_GRAD = 0, PM_ADAM = 1, PM_PACK = 2 };
 __device__ unsigned long long* g_wstamps;
 #define WSTAMP(k)                                                                         \
   do {                                                                                    \
-    if (threadIdx.x == 0 && g_wstamps) g_wstamps[blockIdx.x * 4 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    if (threadIdx.x == 0 && g_wstamps) g_wstamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #else
 #define WSTAMP(k) do { } while (0)
@@ -99,12 +99,17 @@ __device__ __forceinline__ Pre4 load4(const LayerDev& L, int o, int i, const Ada
   s.base = 0;
 #pragma unroll
   for (int c = 0; c < 4; ++c) s.p[c] = s.m[c] = s.v[c] = 0.f;
+  // wave-uniform: every run of the layer is a 16-B aligned float4 (K % 4 == 0, segment offsets % 4
+  // == 0).  The choice must not be per lane: divergent scalar and vector paths share destination
+  // registers, and the vector path then waits (vmcnt(0)) for every load in flight — the tile's
+  // operand loads included — before it can issue
+  const bool vec = (L.K & 3) == 0 && ((L.pw[0] | L.pw[1]) & 3) == 0;
   if (o >= L.N || i >= L.K) return s;
   const int seg = (L.nseg == 2 && o >= L.seg_rows0) ? 1 : 0;
   s.base = L.pw[seg] + (int64_t)(seg ? o - L.seg_rows0 : o) * L.K + i;
   s.nv = min(4, L.K - i);
   if (MODE == PM_GRAD) return s;
-  if (s.nv == 4 && (s.base & 3) == 0) {  // 16-B aligned run (every layer with K % 4 == 0)
+  if (vec) {
     const f32x4 p4 = *(const f32x4*)(a.params + s.base);
 #pragma unroll
     for (int c = 0; c < 4; ++c) s.p[c] = p4[c];
@@ -164,21 +169,37 @@ __device__ __forceinline__ f32x4 apply4(Pre4 s, f32x4 g4, const AdamArgs& a) {
   return w;
 }
 
+// the master state of bias o (padded coordinate) of layer L, loaded early like Pre4
+struct PreB {
+  float p, m, v;
+  int64_t idx;  // -1: padding
+};
 template <int MODE>
-__device__ __forceinline__ void apply_bias(const LayerDev& L, int o, float g, const AdamArgs& a) {
+__device__ __forceinline__ PreB loadb(const LayerDev& L, int o, const AdamArgs& a) {
+  PreB b{0.f, 0.f, 0.f, -1};
+  if (o >= L.N) return b;
+  const int seg = (L.nseg == 2 && o >= L.seg_rows0) ? 1 : 0;
+  b.idx = L.pb[seg] + (seg ? o - L.seg_rows0 : o);
+  if (MODE == PM_GRAD) return b;
+  b.p = a.params[b.idx];
+  if (MODE == PM_ADAM) {
+    b.m = a.m[b.idx];
+    b.v = a.v[b.idx];
+  }
+  return b;
+}
+template <int MODE>
+__device__ __forceinline__ void apply_bias(const LayerDev& L, int o, PreB b, float g, const AdamArgs& a) {
   if (o >= L.Np) return;
   float w = 0.f;
-  if (o < L.N) {
-    const int seg = (L.nseg == 2 && o >= L.seg_rows0) ? 1 : 0;
-    const int64_t idx = L.pb[seg] + (seg ? o - L.seg_rows0 : o);
-    if (MODE == PM_GRAD) { a.grads[idx] = g; return; }
-    w = a.params[idx];
+  if (b.idx >= 0) {
+    if (MODE == PM_GRAD) { a.grads[b.idx] = g; return; }
+    w = b.p;
     if (MODE == PM_ADAM) {
-      float m = a.m[idx], v = a.v[idx];
-      w = adam_math(w, g, m, v, a);
-      a.params[idx] = w;
-      a.m[idx] = m;
-      a.v[idx] = v;
+      w = adam_math(w, g, b.m, b.v, a);
+      a.params[b.idx] = w;
+      a.m[b.idx] = b.m;
+      a.v[b.idx] = b.v;
     }
   } else if (MODE == PM_GRAD) {
     return;
@@ -227,16 +248,19 @@ __device__ __forceinline__ void store_operands(const LayerDev& L, int o0, int i0
 // o0+tid (tiles with i0 == 0).  wt: an LDS tile image (32 × WT_LD floats) the caller no longer
 // needs.  Every thread of the block calls it (barrier inside).
 template <typename T, int MODE, int NTHR>
-__device__ __forceinline__ void tile_epilogue(const LayerDev& L, int o0, int i0, const Pre4& st, f32x4 g4,
-                                              float db, const AdamArgs& aa, float* wt) {
+__device__ __forceinline__ void tile_epilogue(const LayerDev& L, int o0, int i0, const Pre4& st, const PreB& sb,
+                                              f32x4 g4, float db, const AdamArgs& aa, float* wt) {
   const int tid = threadIdx.x, o = tid >> 3, i4 = (tid & 7) * 4;
   f32x4 w = {0.f, 0.f, 0.f, 0.f};
   if (tid < 256) w = apply4<MODE>(st, g4, aa);
-  if (i0 == 0 && tid < 32) apply_bias<MODE>(L, o0 + tid, db, aa);
+  WSTAMP(4);
+  if (i0 == 0 && tid < 32) apply_bias<MODE>(L, o0 + tid, sb, db, aa);
   if (MODE == PM_GRAD || (CVAE_DIAG_NOWPACK && MODE == PM_ADAM)) return;
   if (tid < 256) *(f32x4*)(wt + o * WT_LD + i4) = w;
   __syncthreads();
+  WSTAMP(5);
   store_operands<T, NTHR>(L, o0, i0, wt);
+  WSTAMP(6);
 }
 
 // called by one whole wave: lane-strided partial sums, then a fixed-order butterfly (deterministic).
@@ -329,11 +353,14 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
       for (int n = 0; n < 2; ++n) xb[u][n] = gld<V>(xp[n] + ct * Kx);
     }
   };
-#pragma unroll
-  for (int u = 0; u < PF; ++u) load(u, u);
-  // the master state the epilogue updates (independent of the gradient) behind the operand loads
+  // the master state the epilogue updates (independent of the gradient), issued FIRST: the
+  // compiler's waits inside load4's paths then cover nothing but these loads, never the operands
   Pre4 st = {};
   if (tid < 256) st = load4<MODE>(L, td.o0 + o, td.i0 + i4, aa);
+  PreB sb = {0.f, 0.f, 0.f, -1};
+  if (bias_tile && tid < 32) sb = loadb<MODE>(L, td.o0 + tid, aa);
+#pragma unroll
+  for (int u = 0; u < PF; ++u) load(u, u);
   if (loss_block && wave == WG_NW - 1 && la.partials) finish_loss<SC1>(la, S, D, Z);
   for (int j0 = 0; j0 < nmine; j0 += PF) {
 #pragma unroll
@@ -350,6 +377,7 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
 #pragma unroll
             for (int e = 0; e < EPL; ++e) gs[m] += (float)ga[u][m][e];
         }
+        if (j == 0) WSTAMP(7);
       }
       if (j + PF < nmine) load(u, j + PF);
     }
@@ -383,7 +411,7 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
     for (int w = 0; w < WG_NW; ++w) db += dbp[w * 32 + tid];
   }
   __syncthreads();  // red becomes the image of the new weights
-  tile_epilogue<T, MODE, WG_THREADS>(L, td.o0, td.i0, st, g4, db, aa, red);
+  tile_epilogue<T, MODE, WG_THREADS>(L, td.o0, td.i0, st, sb, g4, db, aa, red);
 #if CVAE_DIAG_STAMPS
   __syncthreads();
   WSTAMP(3);
@@ -407,6 +435,8 @@ __global__ __launch_bounds__(CVAE_THREADS) void param_kernel(NetDev net, const T
   const LayerDev& L = net.L[td.layer];
   const int tid = threadIdx.x;
   const Pre4 st = load4<MODE>(L, td.o0 + (tid >> 3), td.i0 + (tid & 7) * 4, aa);
+  PreB sb = {0.f, 0.f, 0.f, -1};
+  if (td.i0 == 0 && tid < 32) sb = loadb<MODE>(L, td.o0 + tid, aa);
   f32x4 g4 = {0.f, 0.f, 0.f, 0.f};
   float db = 0.f;
   if (MODE == PM_ADAM) {
@@ -418,5 +448,5 @@ __global__ __launch_bounds__(CVAE_THREADS) void param_kernel(NetDev net, const T
       db = aa.grads[L.pb[seg] + (seg ? ob - L.seg_rows0 : ob)] * aa.grad_scale;
     }
   }
-  tile_epilogue<T, MODE, CVAE_THREADS>(L, td.o0, td.i0, st, g4, db, aa, wt);
+  tile_epilogue<T, MODE, CVAE_THREADS>(L, td.o0, td.i0, st, sb, g4, db, aa, wt);
 }

@@ -27,7 +27,7 @@ R = 16
 nb = ((B + 31) // 32 * 32) // R
 dbuf = torch.zeros(nb * 64, dtype=torch.int64, device="cuda")
 NT = 4096
-wbuf = torch.zeros(NT * 4, dtype=torch.int64, device="cuda")
+wbuf = torch.zeros(NT * 8, dtype=torch.int64, device="cuda")
 for _ in range(30):
     eng.train_step(x)
 torch.cuda.synchronize()
@@ -45,7 +45,7 @@ names = ["prologue", "xT copies+C0"] + [f"step{i}" for i in range(1, 64)]
 for i in range(k - 1):
     print(f"{names[i]:>14s} {i:2d}: median {np.median(d[:, i]) / 1000:7.3f} us   max {d[:, i].max() / 1000:7.3f} us")
 
-w = wbuf.view(NT, 4).cpu().numpy().astype(np.int64)
+w = wbuf.view(NT, 8).cpu().numpy().astype(np.int64)
 wid = np.nonzero(w[:, 0] > 0)[0]  # fused launch: tile blocks follow the row-chain blocks
 w = w[wid]
 nw = len(wid)
@@ -68,6 +68,10 @@ print(f"  entry spread {(w[:, 0].max() - w[:, 0].min()) * 10 / 1000:.2f} us;"
       f" phases median/max us: mfma {np.median(w[:, 1] - w[:, 0]) / 100:.2f}/{(w[:, 1] - w[:, 0]).max() / 100:.2f}"
       f"  reduce {np.median(w[:, 2] - w[:, 1]) / 100:.2f}/{(w[:, 2] - w[:, 1]).max() / 100:.2f}"
       f"  adam {np.median(w[:, 3] - w[:, 2]) / 100:.2f}/{(w[:, 3] - w[:, 2]).max() / 100:.2f}")
+if (w[:, 6] > 0).all():
+    ph = lambda a, b: f"{np.median(w[:, b] - w[:, a]) / 100:.2f}/{(w[:, b] - w[:, a]).max() / 100:.2f}"  # noqa: E731
+    print(f"  detail median/max us: first chunk {ph(0, 7)}  rest of loop {ph(7, 1)}  apply4 {ph(2, 4)}"
+          f"  bias+image {ph(4, 5)}  operand stores {ph(5, 6)}  final barrier {ph(6, 3)}")
 late = np.argsort(w[:, 3])[-8:]
 print("  last blocks to finish (block: entry, exit us rel. first entry):",
       [(int(b), round((w[b, 0] - w[:, 0].min()) / 100, 2), round((w[b, 3] - w[:, 0].min()) / 100, 2)) for b in late])
