@@ -181,6 +181,15 @@ __device__ __forceinline__ f32x4 quad_t(f32x4 y) {
   return b1 ? f32x4{f(Rc), A1, f(Rd), A3} : f32x4{A0, f(Rc), A2, f(Rd)};
 }
 
+// value v of each lane of this lane's quad, in lane order (four DPP quad broadcasts)
+__device__ __forceinline__ f32x4 quad_all(float v) {
+  const int x = __builtin_bit_cast(int, v);
+  return f32x4{__builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, x, 0x00, 0xF, 0xF, false)),
+               __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, x, 0x55, 0xF, 0xF, false)),
+               __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, x, 0xAA, 0xF, 0xF, false)),
+               __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, x, 0xFF, 0xF, 0xF, false))};
+}
+
 __device__ __forceinline__ void lbar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // The row chain of batch tile `blk`.  pub (the fused launch, fused_step_kernel): after the steps
@@ -337,25 +346,34 @@ __device__ __forceinline__ void chain_body(const FastNet& net, const RowArgs& a,
     for (int u = 0; u < U; ++u) {
       const int v = u * NT + tid;
       if (v < NV) {  // NV % 4 == 0: quads are whole
-        const int w = v >> 2, rq = fdiv(w, inv_VPR), c = w - rq * VPR, row = 4 * rq + (v & 3);
-        const bool live = row < nrows;
-        const float s0 = live ? (float)x0[u][1] : 0.f, s1 = live ? (float)x0[u][2] : 0.f;
-        const int f0 = c * 8;
-        int d = f0 - fdiv(f0, inv_D) * D;
-        float val[8];
+        const int w = v >> 2, rq = fdiv(w, inv_VPR), c = w - rq * VPR;
+        // transpose the raw tile first (exact): this lane then holds features f0+qd and f0+4+qd of
+        // rows 4rq..4rq+3, so each of its two feature vectors has ONE channel d and the relative
+        // transform is one vector select and subtract per feature (one rounding, as before)
+        const int qd = lane & 3, f0 = c * 8;
+        const f32x4 xlo = quad_t(f32x4{(float)xv[u][0], (float)xv[u][1], (float)xv[u][2], (float)xv[u][3]});
+        const f32x4 xhi = quad_t(f32x4{(float)xv[u][4], (float)xv[u][5], (float)xv[u][6], (float)xv[u][7]});
+        const float s0 = (float)x0[u][1], s1 = (float)x0[u][2];
+        const f32x4 S0 = quad_all(s0), S1 = quad_all(s1);  // start points of rows 4rq..4rq+3
+        const int fl = f0 + qd, fh = fl + 4;
+        const int dl = fl - fdiv(fl, inv_D) * D, dh = fh - fdiv(fh, inv_D) * D;
+        const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+        f32x4 rl = xlo - (dl == 1 ? S0 : dl == 2 ? S1 : zero);
+        f32x4 rh = xhi - (dh == 1 ? S0 : dh == 2 ? S1 : zero);
+        f32x4 cv = qd == 0 ? S0 : qd == 1 ? S1 : zero;  // condition input (x, y, 0, 0) of the rows
+        if (nrows < R) {  // wave-uniform: the batch's last tile; rows past it are zero
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float xr = (float)xv[u][e] - (d == 1 ? s0 : 0.f) - (d == 2 ? s1 : 0.f);
-          val[e] = live ? (float)(__bf16)xr : 0.f;
-          d = d + 1 == D ? 0 : d + 1;
+          for (int i = 0; i < 4; ++i) {
+            const bool live = 4 * rq + i < nrows;
+            rl[i] = live ? rl[i] : 0.f;
+            rh[i] = live ? rh[i] : 0.f;
+            cv[i] = live ? cv[i] : 0.f;
+          }
         }
-        const int qd = lane & 3;  // this lane ends with features f0+qd, f0+4+qd of rows 4rq..4rq+3
-        const bf16x4 lo = to_bf4(quad_t(f32x4{val[0], val[1], val[2], val[3]}));
-        const bf16x4 hi = to_bf4(quad_t(f32x4{val[4], val[5], val[6], val[7]}));
-        *(bf16x4*)(XIN + ioff(f0 + qd, rq)) = lo;
-        *(bf16x4*)(XIN + ioff(f0 + 4 + qd, rq)) = hi;
-        if (c == 0) {  // quad-uniform: condition input features 0..3 (x, y, 0, 0) of these rows
-          const bf16x4 cs = to_bf4(quad_t(f32x4{(float)(__bf16)s0, (float)(__bf16)s1, 0.f, 0.f}));
+        *(bf16x4*)(XIN + ioff(fl, rq)) = to_bf4(rl);
+        *(bf16x4*)(XIN + ioff(fh, rq)) = to_bf4(rh);
+        if (c == 0) {  // quad-uniform: condition input features 0..3 of these rows
+          const bf16x4 cs = to_bf4(cv);
           *(bf16x4*)(CIN + ioff(qd, rq)) = cs;
           arena4(xc0, LY::Kp(LC0), qd, b0, rq, cs);
         }
