@@ -320,9 +320,10 @@ __device__ __forceinline__ void chain_body(const FastNet& net, const RowArgs& a,
     wload(wC0, Wf(LC0), LY::Kp(LC0), wave);
     wload_part<0, NKI / 2>(wE0, Wf(LE0), Ip, wave);
     stamp();
-    // eps: 8 latents × 16 rows, 4 per thread (host-given, or Philox as philox_normal)
-    if (tid < 2 * R) {
-      const int row = tid >> 1, j0 = (tid & 1) * 4;
+    // eps: 8 latents × 16 rows, 4 per thread (host-given, or Philox as philox_normal), on the last
+    // wave: it has one x-tile task fewer than waves 0-2
+    if (tid >= NT - 2 * R) {
+      const int k = tid - (NT - 2 * R), row = k >> 1, j0 = (k & 1) * 4;
       f32x4 e = {0.f, 0.f, 0.f, 0.f};
       if (row < nrows)
         e = a.eps ? gld<f32x4>(a.eps + (size_t)(b0 + row) * Z + j0)

@@ -85,46 +85,53 @@ __device__ __forceinline__ float adam_math(float p, float g, float& m, float& v,
 // LDS image of one 32×32 tile: fp32 rows padded to 36 floats (16-B aligned rows)
 constexpr int WT_LD = 36;
 
-// The fp32 master state of weights (o, i..i+3) of layer L (padded coordinates), loaded before the
-// gradient exists (it does not depend on it) so the epilogue is arithmetic and stores only.
-struct Pre4 {
-  float p[4], m[4], v[4];
+// EPT consecutive fp32 values (the per-thread share of a tile's epilogue)
+template <int EPT> struct VecF;
+template <> struct VecF<2> { typedef float T __attribute__((ext_vector_type(2))); };
+template <> struct VecF<4> { typedef f32x4 T; };
+
+// The fp32 master state of weights (o, i..i+EPT-1) of layer L (padded coordinates), loaded before
+// the gradient exists (it does not depend on it) so the epilogue is arithmetic and stores only.
+template <int EPT>
+struct PreN {
+  float p[EPT], m[EPT], v[EPT];
   int64_t base;
-  int nv;  // valid elements (0: padding)
+  int nv;    // valid elements (0: padding)
+  bool vec;  // whole aligned vector runs (layer-uniform)
 };
-template <int MODE>
-__device__ __forceinline__ Pre4 load4(const LayerDev& L, int o, int i, const AdamArgs& a) {
-  Pre4 s;
+template <int MODE, int EPT>
+__device__ __forceinline__ PreN<EPT> loadn(const LayerDev& L, int o, int i, const AdamArgs& a) {
+  using V = typename VecF<EPT>::T;
+  PreN<EPT> s;
   s.nv = 0;
   s.base = 0;
 #pragma unroll
-  for (int c = 0; c < 4; ++c) s.p[c] = s.m[c] = s.v[c] = 0.f;
-  // wave-uniform: every run of the layer is a 16-B aligned float4 (K % 4 == 0, segment offsets % 4
-  // == 0).  The choice must not be per lane: divergent scalar and vector paths share destination
-  // registers, and the vector path then waits (vmcnt(0)) for every load in flight — the tile's
-  // operand loads included — before it can issue
-  const bool vec = (L.K & 3) == 0 && ((L.pw[0] | L.pw[1]) & 3) == 0;
+  for (int c = 0; c < EPT; ++c) s.p[c] = s.m[c] = s.v[c] = 0.f;
+  // wave-uniform: every run of the layer is an aligned EPT-vector (K % EPT == 0, segment offsets
+  // % EPT == 0).  The choice must not be per lane: divergent scalar and vector paths share
+  // destination registers, and the vector path then waits (vmcnt(0)) for every load in flight
+  s.vec = (L.K % EPT) == 0 && ((L.pw[0] | L.pw[1]) % EPT) == 0;
   if (o >= L.N || i >= L.K) return s;
   const int seg = (L.nseg == 2 && o >= L.seg_rows0) ? 1 : 0;
   s.base = L.pw[seg] + (int64_t)(seg ? o - L.seg_rows0 : o) * L.K + i;
-  s.nv = min(4, L.K - i);
+  s.nv = min(EPT, L.K - i);
   if (MODE == PM_GRAD) return s;
-  if (vec) {
-    const f32x4 p4 = *(const f32x4*)(a.params + s.base);
+  if (s.vec) {
+    const V pv = *(const V*)(a.params + s.base);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) s.p[c] = p4[c];
+    for (int c = 0; c < EPT; ++c) s.p[c] = pv[c];
     if (MODE == PM_ADAM) {
-      const f32x4 m4 = *(const f32x4*)(a.m + s.base), v4 = *(const f32x4*)(a.v + s.base);
+      const V mv = *(const V*)(a.m + s.base), vv = *(const V*)(a.v + s.base);
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        s.m[c] = m4[c];
-        s.v[c] = v4[c];
+      for (int c = 0; c < EPT; ++c) {
+        s.m[c] = mv[c];
+        s.v[c] = vv[c];
       }
     }
     return s;
   }
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
+  for (int c = 0; c < EPT; ++c) {
     if (c < s.nv) {
       s.p[c] = a.params[s.base + c];
       if (MODE == PM_ADAM) {
@@ -137,25 +144,36 @@ __device__ __forceinline__ Pre4 load4(const LayerDev& L, int o, int i, const Ada
 }
 // write the gradient (GRAD), apply Adam (ADAM) or keep (PACK); returns the values for the operand
 // copies (0 in the padding)
-template <int MODE>
-__device__ __forceinline__ f32x4 apply4(Pre4 s, f32x4 g4, const AdamArgs& a) {
-  f32x4 w = {0.f, 0.f, 0.f, 0.f};
+template <int MODE, int EPT>
+__device__ __forceinline__ typename VecF<EPT>::T applyn(PreN<EPT> s, typename VecF<EPT>::T g,
+                                                        const AdamArgs& a) {
+  using V = typename VecF<EPT>::T;
+  V w = {};
   if (MODE == PM_GRAD) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
-      if (c < s.nv) a.grads[s.base + c] = g4[c];
+    for (int c = 0; c < EPT; ++c)
+      if (c < s.nv) a.grads[s.base + c] = g[c];
     return w;
   }
   if (MODE == PM_ADAM) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) s.p[c] = adam_math(s.p[c], g4[c], s.m[c], s.v[c], a);
-    if (s.nv == 4 && (s.base & 3) == 0) {
-      *(f32x4*)(a.params + s.base) = f32x4{s.p[0], s.p[1], s.p[2], s.p[3]};
-      *(f32x4*)(a.m + s.base) = f32x4{s.m[0], s.m[1], s.m[2], s.m[3]};
-      *(f32x4*)(a.v + s.base) = f32x4{s.v[0], s.v[1], s.v[2], s.v[3]};
+    for (int c = 0; c < EPT; ++c) s.p[c] = adam_math(s.p[c], g[c], s.m[c], s.v[c], a);
+    if (s.vec) {
+      if (s.nv == EPT) {
+        V pv, mv, vv;
+#pragma unroll
+        for (int c = 0; c < EPT; ++c) {
+          pv[c] = s.p[c];
+          mv[c] = s.m[c];
+          vv[c] = s.v[c];
+        }
+        *(V*)(a.params + s.base) = pv;
+        *(V*)(a.m + s.base) = mv;
+        *(V*)(a.v + s.base) = vv;
+      }
     } else {
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
+      for (int c = 0; c < EPT; ++c) {
         if (c < s.nv) {
           a.params[s.base + c] = s.p[c];
           a.m[s.base + c] = s.m[c];
@@ -165,11 +183,11 @@ __device__ __forceinline__ f32x4 apply4(Pre4 s, f32x4 g4, const AdamArgs& a) {
     }
   }
 #pragma unroll
-  for (int c = 0; c < 4; ++c) w[c] = c < s.nv ? s.p[c] : 0.f;
+  for (int c = 0; c < EPT; ++c) w[c] = c < s.nv ? s.p[c] : 0.f;
   return w;
 }
 
-// the master state of bias o (padded coordinate) of layer L, loaded early like Pre4
+// the master state of bias o (padded coordinate) of layer L, loaded early like PreN
 struct PreB {
   float p, m, v;
   int64_t idx;  // -1: padding
@@ -243,20 +261,23 @@ __device__ __forceinline__ void store_operands(const LayerDev& L, int o0, int i0
   }
 }
 
-// Shared by wgrad_kernel and param_kernel: thread (o = tid/8, i = 4·(tid%8)) < 256 of the tile
-// owns the gradient g4 of weights (o0+o, i0+i..+3) (state st from load4); threads < 32 own bias
+// Shared by wgrad_kernel and param_kernel: thread (o = tid/(32/EPT), i = EPT·(tid%(32/EPT))) <
+// 1024/EPT of the tile owns the gradient g of weights (o0+o, i0+i..+EPT-1) (state st from loadn);
+// threads < 32 own bias
 // o0+tid (tiles with i0 == 0).  wt: an LDS tile image (32 × WT_LD floats) the caller no longer
 // needs.  Every thread of the block calls it (barrier inside).
-template <typename T, int MODE, int NTHR>
-__device__ __forceinline__ void tile_epilogue(const LayerDev& L, int o0, int i0, const Pre4& st, const PreB& sb,
-                                              f32x4 g4, float db, const AdamArgs& aa, float* wt) {
-  const int tid = threadIdx.x, o = tid >> 3, i4 = (tid & 7) * 4;
-  f32x4 w = {0.f, 0.f, 0.f, 0.f};
-  if (tid < 256) w = apply4<MODE>(st, g4, aa);
+template <typename T, int MODE, int NTHR, int EPT>
+__device__ __forceinline__ void tile_epilogue(const LayerDev& L, int o0, int i0, const PreN<EPT>& st, const PreB& sb,
+                                              typename VecF<EPT>::T g, float db, const AdamArgs& aa, float* wt) {
+  using V = typename VecF<EPT>::T;
+  constexpr int TPR = 32 / EPT;  // threads per tile row
+  const int tid = threadIdx.x, o = tid / TPR, iv = (tid % TPR) * EPT;
+  V w = {};
+  if (tid < 32 * TPR) w = applyn<MODE, EPT>(st, g, aa);
   WSTAMP(4);
   if (i0 == 0 && tid < 32) apply_bias<MODE>(L, o0 + tid, sb, db, aa);
   if (MODE == PM_GRAD || (CVAE_DIAG_NOWPACK && MODE == PM_ADAM)) return;
-  if (tid < 256) *(f32x4*)(wt + o * WT_LD + i4) = w;
+  if (tid < 32 * TPR) *(V*)(wt + o * WT_LD + iv) = w;
   __syncthreads();
   WSTAMP(5);
   store_operands<T, NTHR>(L, o0, i0, wt);
@@ -307,7 +328,11 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
   const T* G = (const T*)L.gT;
   const T* X = (const T*)L.xT;
   const bool bias_tile = td.i0 == 0;
-  const int o = tid >> 3, i4 = (tid & 7) * 4;
+  // epilogue ownership: EPT = 2 weights per thread, all 512 threads (Adam's correctly rounded sqrt
+  // and two divisions per weight are the epilogue's cost)
+  constexpr int EPT = 2, TPR = 32 / EPT;
+  using VE = typename VecF<EPT>::T;
+  const int o = tid / TPR, iv = (tid % TPR) * EPT;
 
   WSTAMP(0);
   f32x4 acc[2][2];
@@ -354,9 +379,9 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
     }
   };
   // the master state the epilogue updates (independent of the gradient), issued FIRST: the
-  // compiler's waits inside load4's paths then cover nothing but these loads, never the operands
-  Pre4 st = {};
-  if (tid < 256) st = load4<MODE>(L, td.o0 + o, td.i0 + i4, aa);
+  // compiler's waits inside loadn's paths then cover nothing but these loads, never the operands
+  PreN<EPT> st = {};
+  if (tid < 32 * TPR) st = loadn<MODE, EPT>(L, td.o0 + o, td.i0 + iv, aa);
   PreB sb = {0.f, 0.f, 0.f, -1};
   if (bias_tile && tid < 32) sb = loadb<MODE>(L, td.o0 + tid, aa);
 #pragma unroll
@@ -400,10 +425,10 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
   }
   __syncthreads();
   WSTAMP(2);
-  f32x4 g4 = {0.f, 0.f, 0.f, 0.f};
-  if (tid < 256) {
+  VE g4 = {};
+  if (tid < 32 * TPR) {
 #pragma unroll
-    for (int w = 0; w < WG_NW; ++w) g4 += *(const f32x4*)(red + w * 32 * WT_LD + o * WT_LD + i4);
+    for (int w = 0; w < WG_NW; ++w) g4 += *(const VE*)(red + w * 32 * WT_LD + o * WT_LD + iv);
   }
   float db = 0.f;
   if (bias_tile && tid < 32) {
@@ -411,7 +436,7 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
     for (int w = 0; w < WG_NW; ++w) db += dbp[w * 32 + tid];
   }
   __syncthreads();  // red becomes the image of the new weights
-  tile_epilogue<T, MODE, WG_THREADS>(L, td.o0, td.i0, st, sb, g4, db, aa, red);
+  tile_epilogue<T, MODE, WG_THREADS, EPT>(L, td.o0, td.i0, st, sb, g4, db, aa, red);
 #if CVAE_DIAG_STAMPS
   __syncthreads();
   WSTAMP(3);
@@ -434,7 +459,7 @@ __global__ __launch_bounds__(CVAE_THREADS) void param_kernel(NetDev net, const T
   const TileDesc td = tiles[blockIdx.x];
   const LayerDev& L = net.L[td.layer];
   const int tid = threadIdx.x;
-  const Pre4 st = load4<MODE>(L, td.o0 + (tid >> 3), td.i0 + (tid & 7) * 4, aa);
+  const PreN<4> st = loadn<MODE, 4>(L, td.o0 + (tid >> 3), td.i0 + (tid & 7) * 4, aa);
   PreB sb = {0.f, 0.f, 0.f, -1};
   if (td.i0 == 0 && tid < 32) sb = loadb<MODE>(L, td.o0 + tid, aa);
   f32x4 g4 = {0.f, 0.f, 0.f, 0.f};
@@ -448,5 +473,5 @@ __global__ __launch_bounds__(CVAE_THREADS) void param_kernel(NetDev net, const T
       db = aa.grads[L.pb[seg] + (seg ? ob - L.seg_rows0 : ob)] * aa.grad_scale;
     }
   }
-  tile_epilogue<T, MODE, CVAE_THREADS>(L, td.o0, td.i0, st, sb, g4, db, aa, wt);
+  tile_epilogue<T, MODE, CVAE_THREADS, 4>(L, td.o0, td.i0, st, sb, g4, db, aa, wt);
 }

@@ -58,7 +58,8 @@ __global__ __launch_bounds__(512) void kA(const __bf16* W, __bf16* out, int nste
       const int s = s0 + b;
       const __bf16* in = img(s);
       __bf16* o = img(s + 1);
-      if (MODE & 4) wl(w[(b + NB - 1) % NB], s + NB - 1);  // issue first: overlaps this step's compute?
+      const bool first = (MODE & 4) || ((MODE & 8) && (wave & 1));  // 8: odd waves first (staggered)
+      if (first) wl(w[(b + NB - 1) % NB], s + NB - 1);
       bf16x8 x[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) x[c] = xfrag(in, c);
@@ -69,8 +70,13 @@ __global__ __launch_bounds__(512) void kA(const __bf16* W, __bf16* out, int nste
 #pragma unroll
       for (int i = 0; i < 4; ++i) h[i] = (__bf16)fmaxf(acc[i] * 0.01f, 0.f);
       *(bf16x4*)(o + n * 16 + 4 * q) = h;
-      if (!(MODE & 2)) *(G bf16x4*)(out + ((size_t)blockIdx.x * nstep + s) * 2048 + n * 16 + 4 * q) = h;
-      if (!(MODE & 4)) wl(w[(b + NB - 1) % NB], s + NB - 1);
+      if ((MODE & 16) && wave < 4) {  // half the waves store the step's 4 KB as 16-B pieces
+        const u32x4 v = {(unsigned)acc[0], (unsigned)acc[1], (unsigned)acc[2], (unsigned)acc[3]};
+        *(G u32x4*)((char*)out + (((size_t)blockIdx.x * nstep + s) * 2048) * 2 + (wave * 64 + lane) * 16) = v;
+      } else if (!(MODE & 2) && !(MODE & 16)) {
+        *(G bf16x4*)(out + ((size_t)blockIdx.x * nstep + s) * 2048 + n * 16 + 4 * q) = h;
+      }
+      if (!first) wl(w[(b + NB - 1) % NB], s + NB - 1);
       lbar();
     }
   }
@@ -200,6 +206,9 @@ int main() {
     per_step("A LA=5", [&](int s) { hipLaunchKernelGGL((kA<0, 6>), dim3(64), dim3(512), 8192, 0, W, out, s); });
     per_step("A LA=2 issue first", [&](int s) { hipLaunchKernelGGL((kA<4, 3>), dim3(64), dim3(512), 8192, 0, W, out, s); });
     per_step("A LA=3 issue first", [&](int s) { hipLaunchKernelGGL((kA<4, 4>), dim3(64), dim3(512), 8192, 0, W, out, s); });
+    per_step("A LA=2 16B stores, 4 waves", [&](int s) { hipLaunchKernelGGL((kA<16, 3>), dim3(64), dim3(512), 8192, 0, W, out, s); });
+    per_step("A LA=2 staggered", [&](int s) { hipLaunchKernelGGL((kA<8, 3>), dim3(64), dim3(512), 8192, 0, W, out, s); });
+    per_step("A LA=3 staggered", [&](int s) { hipLaunchKernelGGL((kA<8, 4>), dim3(64), dim3(512), 8192, 0, W, out, s); });
     per_step("A LA=2 issue first no st", [&](int s) { hipLaunchKernelGGL((kA<6, 3>), dim3(64), dim3(512), 8192, 0, W, out, s); });
     per_step("A LA=2 no stores", [&](int s) { hipLaunchKernelGGL((kA<2, 3>), dim3(64), dim3(512), 8192, 0, W, out, s); });
     per_step("A LA=2 no loads", [&](int s) { hipLaunchKernelGGL((kA<1, 3>), dim3(64), dim3(512), 8192, 0, W, out, s); });
