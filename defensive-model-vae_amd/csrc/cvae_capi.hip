@@ -6,6 +6,7 @@
 #include <cmath>
 #include <cstdio>
 #include <algorithm>
+#include <array>
 #include <cstring>
 #include <cstdlib>
 #include <type_traits>
@@ -453,12 +454,16 @@ bool fast_layout_matches(const cvae_handle* h) {
       (const char*)n.bias_all != h->arena + LY::bias_base)
     return false;
   const int64_t Bp2 = 2 * (int64_t)n.Bp;
-  const int nt = (int)h->tiles.size();
-  if (nt != fchain::Tiles<NKI>::total()) return false;
-  for (int b = 0; b < nt; ++b) {
+  // the fast kernel's tiles (some 64 inputs wide) cover exactly the handle's 32×32 tile set
+  std::vector<std::array<int, 3>> mine, theirs;
+  for (int b = 0; b < fchain::Tiles<NKI>::total(); ++b) {
     const TileDesc t = fchain::Tiles<NKI>::at(b);
-    if (t.layer != h->tiles[b].layer || t.o0 != h->tiles[b].o0 || t.i0 != h->tiles[b].i0) return false;
+    for (int s = 0; s < fchain::Tiles<NKI>::ni(t.layer); ++s) mine.push_back({t.layer, t.o0, t.i0 + 32 * s});
   }
+  for (const TileDesc& t : h->tiles) theirs.push_back({t.layer, t.o0, t.i0});
+  std::sort(mine.begin(), mine.end());
+  std::sort(theirs.begin(), theirs.end());
+  if (mine != theirs) return false;
   for (int l = 0; l < LY::NL; ++l) {
     const LayerDev& L = n.L[l];
     const LayerDev F = fchain::fast_layer<NKI>(l, h->arena, n.Bp, n.I);
@@ -547,7 +552,7 @@ template <int MODE>
 int launch_wgrad(cvae_handle* h, int batch, const AdamArgs& aa, const LossArgs& la, hipStream_t s) {
   const int nt = (int)h->tiles.size();
   if (h->fast_nki == 19)
-    return klaunch(h, fchain::fastwgrad_kernel<19, MODE>, dim3(nt + 1), dim3(WG_THREADS), 0, s,
+    return klaunch(h, fchain::fastwgrad_kernel<19, MODE>, dim3(fchain::Tiles<19>::total() + 1), dim3(WG_THREADS), 0, s,
                    fchain::FastNet{h->arena, h->net.Bp, h->net.S, h->net.D, h->net.I}, bk_of(h, batch), aa, la);
   if (h->cfg.dtype == CVAE_BF16)
     return klaunch(h, wgrad_kernel<__bf16, MODE>, dim3(nt), dim3(WG_THREADS), 0, s, h->net,
@@ -572,7 +577,7 @@ int launch_fused(cvae_handle* h, const void* x, const int64_t* idx, int batch, c
   f.sync = h->d_sync;
   f.Bk = bk_of(h, batch);
   f.nchain = rup_i(batch, 32) / fchain::R;
-  const int nt = (int)h->tiles.size();
+  const int nt = fchain::Tiles<19>::total();
   int rc = tmark(h, s, "fused_step");
   if (rc) return rc;
   return klaunch(h, fchain::fused_step_kernel<19>, dim3(f.nchain + nt), dim3(fchain::NT), h->fast_lds, s,

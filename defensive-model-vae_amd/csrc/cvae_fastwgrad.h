@@ -33,7 +33,16 @@ __device__ __forceinline__ int64_t pick(int l, F f) {
 template <int NKI>
 struct Tiles {
   using LY = Layout<NKI>;
-  __host__ __device__ static constexpr int count(int l) { return (LY::Np(l) / 32) * (LY::Kp(l) / 32); }
+  // input tiles per workgroup (wgrad_body<NI>).  NI = 2 for D3 (38 tiles of 32 × 64 instead of
+  // 76, 243 workgroups: one per CU) measured no faster than 280 workgroups with 24 CUs doubled
+  // (7.18 vs 7.23 µs): a 64-wide tile costs what two co-resident tiles do.  Kept at 1.
+  __host__ __device__ static constexpr int ni(int) { return 1; }
+  __host__ __device__ static constexpr int ni_max() {
+    int m = 1;
+    for (int l = 0; l < LY::NL; ++l) m = ni(l) > m ? ni(l) : m;
+    return m;
+  }
+  __host__ __device__ static constexpr int count(int l) { return (LY::Np(l) / 32) * (LY::Kp(l) / (32 * ni(l))); }
   __host__ __device__ static constexpr int start(int l) {
     int t = 0;
     for (int k = 0; k < l; ++k) t += count(k);
@@ -44,7 +53,9 @@ struct Tiles {
   // the divisor of a layer's tile index (the inner tile count) is a power of two for this
   // architecture: the decode is shifts and masks
   __host__ __device__ static constexpr bool i_outer(int l) { return LY::Kp(l) > LY::Np(l); }
-  __host__ __device__ static constexpr int inner(int l) { return i_outer(l) ? LY::Np(l) / 32 : LY::Kp(l) / 32; }
+  __host__ __device__ static constexpr int inner(int l) {
+    return i_outer(l) ? LY::Np(l) / 32 : LY::Kp(l) / (32 * ni(l));
+  }
   __host__ __device__ static constexpr bool pow2_inner() {
     for (int l = 0; l < LY::NL; ++l)
       if (inner(l) & (inner(l) - 1)) return false;
@@ -63,13 +74,14 @@ struct Tiles {
     const int loc = s - (int)pick<LY::NL>(l, [](int k) { return (int64_t)start(k); });
     const int sh = (int)pick<LY::NL>(l, [](int k) { return (int64_t)log2i(inner(k)); });
     const bool io = pick<LY::NL>(l, [](int k) { return (int64_t)i_outer(k); }) != 0;
+    const int w = 32 * (int)pick<LY::NL>(l, [](int k) { return (int64_t)ni(k); });  // input width
     const int a = loc >> sh, c = loc & ((1 << sh) - 1);
-    return TileDesc{l, 32 * (io ? c : a), 32 * (io ? a : c), 0};
+    return TileDesc{l, 32 * (io ? c : a), w * (io ? a : c), 0};
 #else
     int l = 0;
     while (l + 1 < LY::NL && s >= start(l + 1)) ++l;
     const int loc = s - start(l), a = loc / inner(l), c = loc % inner(l);
-    return TileDesc{l, 32 * (i_outer(l) ? c : a), 32 * (i_outer(l) ? a : c), 0};
+    return TileDesc{l, 32 * (i_outer(l) ? c : a), 32 * ni(l) * (i_outer(l) ? a : c), 0};
 #endif
   }
 };
@@ -123,9 +135,13 @@ __global__ __launch_bounds__(WG_THREADS) void fastwgrad_kernel(FastNet fn, int B
     if (threadIdx.x < 64 && la.partials) finish_loss(la, fn.S, fn.D, Z);
     return;
   }
+  __shared__ __attribute__((aligned(16))) WgradLds<Tiles<NKI>::ni_max()> sh;
   const TileDesc td = Tiles<NKI>::at(blockIdx.x);
   const LayerDev L = fast_layer<NKI>(td.layer, fn.arena, fn.Bp, fn.I);
-  wgrad_body<__bf16, MODE>(L, td, Bk, aa, la, false, fn.S, fn.D, Z);
+  if (Tiles<NKI>::ni(td.layer) == 2)  // block-uniform
+    wgrad_body<__bf16, MODE, false, 2>(L, td, Bk, aa, la, false, fn.S, fn.D, Z, sh.red, sh.dbp);
+  else
+    wgrad_body<__bf16, MODE, false, 1>(L, td, Bk, aa, la, false, fn.S, fn.D, Z, sh.red, sh.dbp);
 }
 
 // ---------------------------------------------------------------- the fused training step
@@ -168,14 +184,16 @@ struct ReadyTiles {
     const int loc = tb - (int)pick<NL>(k, [](int j) { return (int64_t)start(j); });
     const int sh = (int)pick<NL>(k, [](int j) { return (int64_t)T::log2i(T::inner(ready_layer(j))); });
     const bool io = pick<NL>(k, [](int j) { return (int64_t)T::i_outer(ready_layer(j)); }) != 0;
+    const int w = 32 * (int)pick<NL>(k, [](int j) { return (int64_t)T::ni(ready_layer(j)); });
     const int a = loc >> sh, c = loc & ((1 << sh) - 1);
 #else
     int k = 0;
     while (k + 1 < NL && tb >= start(k + 1)) ++k;
     const int l = ready_layer(k), loc = tb - start(k), a = loc / T::inner(l), c = loc % T::inner(l);
     const bool io = T::i_outer(l);
+    const int w = 32 * T::ni(l);
 #endif
-    return TileDesc{l, 32 * (io ? c : a), 32 * (io ? a : c), 0};
+    return TileDesc{l, 32 * (io ? c : a), w * (io ? a : c), 0};
   }
 };
 
@@ -219,7 +237,11 @@ __global__ __launch_bounds__(NT) void fused_step_kernel(FastNet fn, RowArgs a, F
   if (FUSED_DIAG == 2) return;
 #endif
   const LayerDev L = fast_layer<NKI>(td.layer, fn.arena, fn.Bp, fn.I);
-  wgrad_body<__bf16, PM_ADAM, true>(L, td, f.Bk, f.aa, f.la, tb == NTL - 1, fn.S, fn.D, Z);
+  __shared__ __attribute__((aligned(16))) WgradLds<Tiles<NKI>::ni_max()> sh;
+  if (Tiles<NKI>::ni(td.layer) == 2)
+    wgrad_body<__bf16, PM_ADAM, true, 2>(L, td, f.Bk, f.aa, f.la, tb == NTL - 1, fn.S, fn.D, Z, sh.red, sh.dbp);
+  else
+    wgrad_body<__bf16, PM_ADAM, true, 1>(L, td, f.Bk, f.aa, f.la, tb == NTL - 1, fn.S, fn.D, Z, sh.red, sh.dbp);
   if (threadIdx.x == 0 &&
       __hip_atomic_fetch_add(f.sync + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == NTL - 1) {
 #pragma unroll

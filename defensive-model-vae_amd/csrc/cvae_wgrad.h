@@ -230,7 +230,7 @@ __device__ __forceinline__ void apply_bias(const LayerDev& L, int o, PreB b, flo
 // (n-tile t, chunk kc) lane ln holds elements (16t + (ln & 15), KC·kc + frag_k(ln >> 4, e)) at
 // ((t·Kp/KC + kc)·64 + ln)·EPL (frag_off), so a tile is 2 n-tiles × 32/KC chunks of contiguous
 // 1-KB blocks per copy.
-template <typename T, int NTHR>
+template <typename T, int NTHR, int LD = WT_LD>
 __device__ __forceinline__ void store_operands(const LayerDev& L, int o0, int i0, const float* wt) {
   using V = typename Op<T>::V;
   constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC, CPT = 32 / KC;
@@ -247,12 +247,12 @@ __device__ __forceinline__ void store_operands(const LayerDev& L, int o0, int i0
     V val;
     if (wb) {  // Wb = Wᵀ: rows = inputs i, K = outputs o
 #pragma unroll
-      for (int e = 0; e < EPL; ++e) val[e] = to_t<T>(wt[(kl + frag_k<T>(q, e)) * WT_LD + nl]);
+      for (int e = 0; e < EPL; ++e) val[e] = to_t<T>(wt[(kl + frag_k<T>(q, e)) * LD + nl]);
       gst<V>((T*)L.Wb + ((size_t)(((i0 >> 4) + bt) * (L.Np / KC) + (o0 + kl) / KC) * 64 + ln) * EPL, val);
     } else {
 #pragma unroll
       for (int e = 0; e < EPL; e += 4) {  // 4 consecutive K positions per half-fragment
-        const f32x4 v4 = *(const f32x4*)(wt + nl * WT_LD + kl + frag_k<T>(q, e));
+        const f32x4 v4 = *(const f32x4*)(wt + nl * LD + kl + frag_k<T>(q, e));
 #pragma unroll
         for (int c = 0; c < 4; ++c) val[e + c] = to_t<T>(v4[c]);
       }
@@ -261,26 +261,27 @@ __device__ __forceinline__ void store_operands(const LayerDev& L, int o0, int i0
   }
 }
 
-// Shared by wgrad_kernel and param_kernel: thread (o = tid/(32/EPT), i = EPT·(tid%(32/EPT))) <
-// 1024/EPT of the tile owns the gradient g of weights (o0+o, i0+i..+EPT-1) (state st from loadn);
-// threads < 32 own bias
-// o0+tid (tiles with i0 == 0).  wt: an LDS tile image (32 × WT_LD floats) the caller no longer
-// needs.  Every thread of the block calls it (barrier inside).
-template <typename T, int MODE, int NTHR, int EPT>
+// Shared by wgrad_kernel and param_kernel.  The tile is 32 outputs × 32·NI inputs; thread
+// (o = tid/TPR, i = EPT·(tid%TPR)), TPR = 32·NI/EPT, owns the gradient g of weights
+// (o0+o, i0+i..+EPT-1) (state st from loadn); threads < 32 own bias o0+tid (tiles with i0 == 0).
+// wt: an LDS tile image (32 rows of 32·NI + 4 floats) the caller no longer needs.  Every thread of
+// the block calls it (barrier inside).
+template <typename T, int MODE, int NTHR, int EPT, int NI = 1>
 __device__ __forceinline__ void tile_epilogue(const LayerDev& L, int o0, int i0, const PreN<EPT>& st, const PreB& sb,
                                               typename VecF<EPT>::T g, float db, const AdamArgs& aa, float* wt) {
   using V = typename VecF<EPT>::T;
-  constexpr int TPR = 32 / EPT;  // threads per tile row
+  constexpr int TW = 32 * NI, LD = TW + 4, TPR = TW / EPT;  // tile width, image row stride, threads per row
   const int tid = threadIdx.x, o = tid / TPR, iv = (tid % TPR) * EPT;
   V w = {};
   if (tid < 32 * TPR) w = applyn<MODE, EPT>(st, g, aa);
   WSTAMP(4);
   if (i0 == 0 && tid < 32) apply_bias<MODE>(L, o0 + tid, sb, db, aa);
   if (MODE == PM_GRAD || (CVAE_DIAG_NOWPACK && MODE == PM_ADAM)) return;
-  if (tid < 32 * TPR) *(V*)(wt + o * WT_LD + iv) = w;
+  if (tid < 32 * TPR) *(V*)(wt + o * LD + iv) = w;
   __syncthreads();
   WSTAMP(5);
-  store_operands<T, NTHR>(L, o0, i0, wt);
+#pragma unroll
+  for (int s = 0; s < NI; ++s) store_operands<T, NTHR, LD>(L, o0, i0 + 32 * s, wt + 32 * s);
   WSTAMP(6);
 }
 
@@ -313,48 +314,56 @@ __device__ void finish_loss(const LossArgs& l, int S, int D, int Z) {
 // 8 waves per tile: the batch (K) is cut into 8 wave slices whose loads are all in flight at once
 constexpr int WG_NW = 8, WG_THREADS = 64 * WG_NW;
 
-// One workgroup = tile td of layer L (loss_block: this workgroup also finishes the loss; S, D, Z:
-// its shape).  SC1: the arena rows were handed over inside the launch (fused_step_kernel): every
-// load of them is an sc1 buffer load.
-template <typename T, int MODE, bool SC1 = false>
+// LDS of one dW workgroup for tiles up to 32·NI inputs wide
+template <int NI>
+struct WgradLds {
+  float red[WG_NW * 32 * (32 * NI + 4)];  // per-wave partial tiles, then the new weights' image
+  float dbp[WG_NW * 32];                  // per-wave bias partials
+};
+
+// One workgroup = tile td of layer L: 32 outputs × 32·NI inputs (NI = 2: two 32-wide input tiles
+// sharing the G rows).  loss_block: this workgroup also finishes the loss (S, D, Z: its shape).
+// SC1: the arena rows were handed over inside the launch (fused_step_kernel): every load of them
+// is an sc1 buffer load.
+template <typename T, int MODE, bool SC1 = false, int NI = 1>
 __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td, int Bk, const AdamArgs& aa,
-                                           const LossArgs& la, bool loss_block, int S, int D, int Z) {
+                                           const LossArgs& la, bool loss_block, int S, int D, int Z,
+                                           float* red, float* dbp) {
   using V = typename Op<T>::V;
   constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC;
-  __shared__ __attribute__((aligned(16))) float red[WG_NW * 32 * WT_LD];
-  __shared__ float dbp[WG_NW * 32];
+  constexpr int NX = 2 * NI, TW = 32 * NI, LD = TW + 4;  // X fragments per chunk, tile width, image stride
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int r16 = lane & 15, kq = (lane >> 4) * EPL;
   const T* G = (const T*)L.gT;
   const T* X = (const T*)L.xT;
   const bool bias_tile = td.i0 == 0;
-  // epilogue ownership: EPT = 2 weights per thread, all 512 threads (Adam's correctly rounded sqrt
-  // and two divisions per weight are the epilogue's cost)
-  constexpr int EPT = 2, TPR = 32 / EPT;
+  // epilogue ownership: EPT = 2·NI weights per thread, all 512 threads (Adam's correctly rounded
+  // sqrt and two divisions per weight are the epilogue's cost)
+  constexpr int EPT = 2 * NI, TPR = TW / EPT;
   using VE = typename VecF<EPT>::T;
   const int o = tid / TPR, iv = (tid % TPR) * EPT;
 
   WSTAMP(0);
-  f32x4 acc[2][2];
+  f32x4 acc[2][NX];
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
-    for (int n = 0; n < 2; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int n = 0; n < NX; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
   float gs[2] = {0.f, 0.f};  // bias partials: Σ of this lane's G fragment elements
   // tile-major arena (aoff): this lane's 16-B pieces of rows o / i at batch offset kq of a chunk;
   // one chunk of KC batch rows advances KC/16 row tiles = (KC/16)·Kf·16 elements
   const int Kg = L.Np, Kx = L.Kp;
   const T* gp[2];
-  const T* xp[2];
+  const T* xp[NX];
 #pragma unroll
   for (int m = 0; m < 2; ++m) gp[m] = G + aoff(td.o0 + m * 16 + r16, kq, Kg);
 #pragma unroll
-  for (int n = 0; n < 2; ++n) xp[n] = X + aoff(td.i0 + n * 16 + r16, kq, Kx);
+  for (int n = 0; n < NX; ++n) xp[n] = X + aoff(td.i0 + n * 16 + r16, kq, Kx);
   // this wave's chunks: c = wave + WG_NW*j; PF chunks of loads kept in flight
   const int nk = Bk / KC;
   const int nmine = nk > wave ? (nk - wave + WG_NW - 1) / WG_NW : 0;
   constexpr int PF = 4;
-  V ga[PF][2], xb[PF][2];
+  V ga[PF][2], xb[PF][NX];
   __amdgpu_buffer_rsrc_t rg, rx;
   if (SC1) {
     rg = __builtin_amdgcn_make_buffer_rsrc((void*)G, (short)0, 0x7fffffff, 0x00020000);
@@ -368,14 +377,14 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
         ga[u][m] = __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(
                                              rg, (int)((gp[m] + ct * Kg - G) * sizeof(T)), 0, 16));
 #pragma unroll
-      for (int n = 0; n < 2; ++n)
+      for (int n = 0; n < NX; ++n)
         xb[u][n] = __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(
                                              rx, (int)((xp[n] + ct * Kx - X) * sizeof(T)), 0, 16));
     } else {
 #pragma unroll
       for (int m = 0; m < 2; ++m) ga[u][m] = gld<V>(gp[m] + ct * Kg);
 #pragma unroll
-      for (int n = 0; n < 2; ++n) xb[u][n] = gld<V>(xp[n] + ct * Kx);
+      for (int n = 0; n < NX; ++n) xb[u][n] = gld<V>(xp[n] + ct * Kx);
     }
   };
   // the master state the epilogue updates (independent of the gradient), issued FIRST: the
@@ -395,7 +404,7 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
 #pragma unroll
         for (int m = 0; m < 2; ++m)
 #pragma unroll
-          for (int n = 0; n < 2; ++n) acc[m][n] = mfma_chunk(ga[u][m], xb[u][n], acc[m][n]);
+          for (int n = 0; n < NX; ++n) acc[m][n] = mfma_chunk(ga[u][m], xb[u][n], acc[m][n]);
         if (bias_tile) {
 #pragma unroll
           for (int m = 0; m < 2; ++m)
@@ -408,13 +417,13 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
     }
   }
   WSTAMP(1);
-  float* rw = red + wave * 32 * WT_LD;
+  float* rw = red + wave * 32 * LD;
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
-    for (int n = 0; n < 2; ++n)
+    for (int n = 0; n < NX; ++n)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) rw[(m * 16 + (lane >> 4) * 4 + i) * WT_LD + n * 16 + r16] = acc[m][n][i];
+      for (int i = 0; i < 4; ++i) rw[(m * 16 + (lane >> 4) * 4 + i) * LD + n * 16 + r16] = acc[m][n][i];
   if (bias_tile) {
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
@@ -428,7 +437,7 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
   VE g4 = {};
   if (tid < 32 * TPR) {
 #pragma unroll
-    for (int w = 0; w < WG_NW; ++w) g4 += *(const VE*)(red + w * 32 * WT_LD + o * WT_LD + iv);
+    for (int w = 0; w < WG_NW; ++w) g4 += *(const VE*)(red + w * 32 * LD + o * LD + iv);
   }
   float db = 0.f;
   if (bias_tile && tid < 32) {
@@ -436,7 +445,7 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
     for (int w = 0; w < WG_NW; ++w) db += dbp[w * 32 + tid];
   }
   __syncthreads();  // red becomes the image of the new weights
-  tile_epilogue<T, MODE, WG_THREADS, EPT>(L, td.o0, td.i0, st, sb, g4, db, aa, red);
+  tile_epilogue<T, MODE, WG_THREADS, EPT, NI>(L, td.o0, td.i0, st, sb, g4, db, aa, red);
 #if CVAE_DIAG_STAMPS
   __syncthreads();
   WSTAMP(3);
@@ -447,8 +456,9 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
 template <typename T, int MODE>
 __global__ __launch_bounds__(WG_THREADS) void wgrad_kernel(NetDev net, const TileDesc* __restrict__ tiles,
                                                            int Bk, AdamArgs aa, LossArgs la) {
+  __shared__ __attribute__((aligned(16))) WgradLds<1> sh;
   const TileDesc td = tiles[blockIdx.x];
-  wgrad_body<T, MODE>(net.L[td.layer], td, Bk, aa, la, blockIdx.x == 0, net.S, net.D, net.Z);
+  wgrad_body<T, MODE>(net.L[td.layer], td, Bk, aa, la, blockIdx.x == 0, net.S, net.D, net.Z, sh.red, sh.dbp);
 }
 
 // Adam from a (reduced) gradient buffer, or repack of the operand copies.
