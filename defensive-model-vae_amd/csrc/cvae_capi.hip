@@ -529,8 +529,8 @@ int train_fwd_bwd_impl(cvae_handle* h, const void* x, const int64_t* idx, int ba
     ra.nsteps = h->n_steps[cvae_handle::ST_TRAIN];
     ra.stamps = h->d_stamps;
     const int grid = rup_i(batch, 32) / fchain::R;
-    return klaunch(h, fchain::fastchain_kernel<19>, dim3(grid), dim3(fchain::NT), h->fast_lds, s,
-                   fchain::FastNet{h->arena, h->net.Bp, h->net.S, h->net.D, h->net.I}, ra);
+    return klaunch(h, fchain::fastchain_kernel<19>, dim3(grid), dim3(fchain::NT), h->fast_lds, s, h->arena, x, idx,
+                   h->net.Bp, batch, h->net.S, h->net.D, h->net.I, ra);
   }
   return launch_rowchain<T, RC_TRAIN>(h, ra, s);
 }
@@ -552,8 +552,9 @@ template <int MODE>
 int launch_wgrad(cvae_handle* h, int batch, const AdamArgs& aa, const LossArgs& la, hipStream_t s) {
   const int nt = (int)h->tiles.size();
   if (h->fast_nki == 19)
-    return klaunch(h, fchain::fastwgrad_kernel<19, MODE>, dim3(fchain::Tiles<19>::total() + 1), dim3(WG_THREADS), 0, s,
-                   fchain::FastNet{h->arena, h->net.Bp, h->net.S, h->net.D, h->net.I}, bk_of(h, batch), aa, la);
+    return klaunch(h, fchain::fastwgrad_kernel<19, MODE>, dim3(fchain::Tiles<19>::total() + 1), dim3(WG_THREADS),
+                   0, s, h->arena, aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), h->net.S, h->net.D, h->net.I,
+                   aa, la);
   if (h->cfg.dtype == CVAE_BF16)
     return klaunch(h, wgrad_kernel<__bf16, MODE>, dim3(nt), dim3(WG_THREADS), 0, s, h->net,
                    (const TileDesc*)h->d_tiles, bk_of(h, batch), aa, la);

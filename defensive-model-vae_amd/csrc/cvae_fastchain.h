@@ -740,10 +740,18 @@ __device__ __forceinline__ void chain_body(const FastNet& net, const RowArgs& a,
   }
 }
 
+// The arguments the first loads need come first as scalars: the hardware preloads them into
+// SGPRs at wave launch (-amdgpu-kernarg-preload-count), so the x-tile loads issue without waiting
+// for a kernel-argument round trip; the rest arrive in RowArgs meanwhile.
 template <int NKI>
-__global__ __launch_bounds__(NT) void fastchain_kernel(FastNet net, RowArgs a) {
+__global__ __launch_bounds__(NT) void fastchain_kernel(char* arena, const void* x, const int64_t* idx, int Bp,
+                                                       int batch, int S, int D, int I, RowArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  chain_body<NKI>(net, a, smem, nullptr, blockIdx.x);
+  RowArgs ra = a;
+  ra.x = x;
+  ra.idx = idx;
+  ra.batch = batch;
+  chain_body<NKI>(FastNet{arena, Bp, S, D, I}, ra, smem, nullptr, blockIdx.x);
 }
 
 }  // namespace fchain

@@ -129,8 +129,17 @@ __host__ __device__ inline LayerDev fast_layer(int l, char* arena, int Bp, int I
   return L;
 }
 
+// Scalars first (SGPR-preloaded at wave launch, as fastchain_kernel's): the arena and master-state
+// pointers every first load needs.
 template <int NKI, int MODE>
-__global__ __launch_bounds__(WG_THREADS) void fastwgrad_kernel(FastNet fn, int Bk, AdamArgs aa, LossArgs la) {
+__global__ __launch_bounds__(WG_THREADS) void fastwgrad_kernel(char* arena, float* params, float* mst, float* vst,
+                                                                int Bp, int Bk, int S, int D, int I, AdamArgs a,
+                                                                LossArgs la) {
+  const FastNet fn{arena, Bp, S, D, I};
+  AdamArgs aa = a;
+  aa.params = params;
+  aa.m = mst;
+  aa.v = vst;
   if ((int)blockIdx.x == Tiles<NKI>::total()) {  // one extra block finishes the loss beside the tiles
     if (threadIdx.x < 64 && la.partials) finish_loss(la, fn.S, fn.D, Z);
     return;

@@ -37,7 +37,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     tmp = LIB + ".tmp"
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wno-unused-result", "-Wno-pass-failed", "-mllvm", "-amdgpu-mfma-vgpr-form", "-o", tmp]
+           "-Wno-unused-result", "-Wno-pass-failed", "-mllvm", "-amdgpu-mfma-vgpr-form",
+           "-mllvm", "-amdgpu-kernarg-preload-count=16", "-o", tmp]
     cmd += os.environ.get("CVAE_EXTRA_FLAGS", "").split()  # diagnostic builds only (with CVAE_LIB)
     cmd += [os.path.join(CSRC, s) for s in SOURCES]
     if verbose:
