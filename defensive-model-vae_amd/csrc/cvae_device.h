@@ -193,8 +193,20 @@ __device__ __forceinline__ f32x4 philox_normal4(uint64_t seed, uint64_t offset, 
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
 // ------------------------------------------------------------------ wave reduction
+// Sum over the wave in a fixed order (deterministic): DPP within each 16-lane row (quad xor 1,
+// quad xor 2, half-row mirror, row mirror: every lane then holds its row's sum), then the four
+// row sums read out as scalars — 4 DPP adds and 4 readlanes instead of 6 ds_bpermute round trips.
+// The result is wave-uniform.
+#define CVAE_DPP_ADD(v, ctrl) \
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), ctrl, 0xF, 0xF, false))
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  CVAE_DPP_ADD(v, 0xB1);   // quad_perm [1,0,3,2]
+  CVAE_DPP_ADD(v, 0x4E);   // quad_perm [2,3,0,1]
+  CVAE_DPP_ADD(v, 0x141);  // row_half_mirror
+  CVAE_DPP_ADD(v, 0x140);  // row_mirror
+  auto rd = [](float x, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
+  };
+  return (rd(v, 0) + rd(v, 16)) + (rd(v, 32) + rd(v, 48));
 }
+#undef CVAE_DPP_ADD
