@@ -70,8 +70,12 @@ struct LossArgs {
   float* loss_accum;      // [5] nullable, += loss * batch
 };
 
+#ifndef CVAE_DIAG_NOADAM
+#define CVAE_DIAG_NOADAM 0  // timing only: the update is p − lr·g (no moments)
+#endif
 // One element of torch's Adam, in its op order; m and v are updated in place.
 __device__ __forceinline__ float adam_math(float p, float g, float& m, float& v, const AdamArgs& a) {
+  if (CVAE_DIAG_NOADAM) return p + a.lr_neg_step * g;
   // exp_avg.lerp_(grad, 1 - beta1): weight < 0.5 branch of at::lerp
   m = a.beta1_w < 0.5f ? m + a.beta1_w * (g - m) : g - (g - m) * (1.f - a.beta1_w);
   // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, value=1 - beta2)
