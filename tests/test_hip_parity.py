@@ -356,3 +356,57 @@ def test_fused_step_equals_two_launch_step(cvae, monkeypatch):
         assert torch.equal(e1.m, e2.m) and torch.equal(e1.v, e2.v), B
         assert torch.equal(e1.loss, e2.loss) and torch.equal(e1.loss_accum, e2.loss_accum), B
     assert e2.sync_words() == [0, 0, 0, 0, 0]
+
+
+def _bf16_run(cvae, sd, x, idx_list, monkeypatch=None, env=None):
+    if monkeypatch is not None:
+        if env:
+            monkeypatch.setenv(*env)
+        else:
+            monkeypatch.delenv("CVAE_GENERIC", raising=False)
+    m, e = _model(cvae, 100, 6, 8, sd=sd, dtype="bf16", max_batch=200)
+    if monkeypatch is not None and env:
+        monkeypatch.delenv(env[0])
+    losses = []
+    for idx in idx_list:
+        e.train_step(x, idx=idx, eps=torch.zeros(idx.numel(), 8).cuda() + 0.25)
+        losses.append(e.loss.clone())
+    torch.cuda.synchronize()
+    return e, torch.stack(losses)
+
+
+def test_fast_and_generic_kernels_agree(cvae, monkeypatch):
+    """The specialised bf16 kernels (fastchain + fastwgrad) and the generic interpreter
+    (CVAE_GENERIC=1 at handle creation) compute the same training steps, up to fp32 summation
+    order: losses and parameters after 3 steps, ragged batch included."""
+    torch.manual_seed(0)
+    ref = OracleCVAE(100, 6, 8)
+    x = torch.randn(300, 100, 6).to("cuda", torch.bfloat16)
+    idxs = [torch.randint(0, 300, (B,), generator=torch.Generator().manual_seed(B)).cuda() for B in (200, 77, 160)]
+    ef, lf = _bf16_run(cvae, ref.state_dict(), x, idxs, monkeypatch)
+    eg, lg = _bf16_run(cvae, ref.state_dict(), x, idxs, monkeypatch, ("CVAE_GENERIC", "1"))
+    np.testing.assert_allclose(lf.cpu().numpy(), lg.cpu().numpy(), rtol=2e-3, atol=1e-6)
+    dp = (ef.params - eg.params).norm() / (ef.params - torch.cat([p.detach().flatten() for p in ref.parameters()]).cuda()).norm()
+    assert float(dp) < 2e-2, float(dp)  # relative to the 3-step update
+
+
+def test_misaligned_input_runs_generic_chain(cvae):
+    """x whose data pointer is not 16-B aligned takes the generic row chain (the fast chain loads
+    16-B vectors) with the fast dW kernel behind it; the result matches the aligned run."""
+    torch.manual_seed(0)
+    ref = OracleCVAE(100, 6, 8)
+    B = 64
+    xa = torch.randn(B, 100, 6).to("cuda", torch.bfloat16)
+    flat = torch.empty(B * 600 + 1, dtype=torch.bfloat16, device="cuda")
+    flat[1:] = xa.flatten()
+    xm = flat[1:].view(B, 100, 6)
+    assert xm.data_ptr() % 16 != 0 and xm.is_contiguous()
+    m1, e1 = _model(cvae, 100, 6, 8, sd=ref.state_dict(), dtype="bf16", max_batch=B)
+    m2, e2 = _model(cvae, 100, 6, 8, sd=ref.state_dict(), dtype="bf16", max_batch=B)
+    eps = torch.randn(B, 8).cuda()
+    for _ in range(2):
+        e1.train_step(xa, eps=eps)
+        e2.train_step(xm, eps=eps)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(e1.loss.cpu().numpy(), e2.loss.cpu().numpy(), rtol=2e-3, atol=1e-6)
+    assert float((e1.params - e2.params).norm() / e1.params.norm()) < 1e-3
