@@ -162,6 +162,75 @@ __global__ void rewrite(u32x4* W, int n16, unsigned v) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += gridDim.x * blockDim.x) W[i] = u32x4{v, v, v, v};
 }
 
+// ---- C: one loader wave streams the weights by LDS-DMA into an NS-slot ring and never joins a
+// barrier; the 8 compute waves synchronise through LDS counters instead of s_barrier.
+__device__ __forceinline__ bool spin_ge(volatile unsigned* c, unsigned target, unsigned* err) {
+  for (unsigned it = 0; *c < target; ++it) {
+    __builtin_amdgcn_s_sleep(1);
+    if (it > (1u << 22)) {
+      err[0] = 1;
+      return false;
+    }
+  }
+  return true;
+}
+template <int NS, int MODE, int L = 1>  // MODE bit1: no global stores; L loader waves
+__global__ __launch_bounds__(64 * (8 + L)) void kC(const __bf16* W, __bf16* out, int nstep, unsigned* err) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* ring = smem + 8192;
+  volatile unsigned* ctr = (volatile unsigned*)(smem + 8192 + NS * WSTEP);  // [0] ready steps, [1] done waves
+  auto img = [&](int i) { return (__bf16*)(smem + (i & 1) * 4096); };
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid < 512) ((u32x4*)smem)[tid] = u32x4{0, 0, 0, 0};
+  if (tid == 0) {
+    ctr[0] = 0;
+    ctr[1] = 0;
+  }
+  __syncthreads();
+  if (wave >= 8) {
+    constexpr int FPL = 32 / L;  // 1-KB pieces per loader wave per step
+    const int lw = wave - 8;
+    for (int s = 0; s < nstep; ++s) {
+      if (s >= NS && !spin_ge(ctr + 1, 8u * (s - NS + 1), err)) return;
+      const char* src = (const char*)W + (size_t)(s % NWSTEPS) * WSTEP + lw * FPL * 1024 + lane * 16;
+      LDSP char* dst = (LDSP char*)ring + (s % NS) * WSTEP + lw * FPL * 1024;
+#pragma unroll
+      for (int f = 0; f < FPL; ++f)
+        __builtin_amdgcn_global_load_lds((const G void*)(src + f * 1024), (LDSP void*)(dst + f * 1024), 16, 0, 0);
+      if (s >= 1) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(FPL) : "memory");  // step s-1 landed
+        if (lane == 0) __hip_atomic_fetch_add((unsigned*)ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_add((unsigned*)ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return;
+  }
+  const int n16 = lane & 15, q = lane >> 4, n = wave * 16 + n16;
+  for (int s = 0; s < nstep; ++s) {
+    if (!spin_ge(ctr, (unsigned)L * (s + 1), err)) return;
+    const __bf16* in = img(s);
+    __bf16* o = img(s + 1);
+    const char* slot = ring + (s % NS) * WSTEP + wave * 4 * 1024 + lane * 16;
+    bf16x8 x[4], w[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) w[c] = *(const bf16x8*)(slot + c * 1024);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) x[c] = xfrag(in, c);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[c], w[c], acc, 0, 0, 0);
+    bf16x4 h;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h[i] = (__bf16)fmaxf(acc[i] * 0.01f, 0.f);
+    *(bf16x4*)(o + n * 16 + 4 * q) = h;
+    if (!(MODE & 2)) *(G bf16x4*)(out + ((size_t)blockIdx.x * nstep + s) * 2048 + n * 16 + 4 * q) = h;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_add((unsigned*)(ctr + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (!spin_ge(ctr + 1, 8u * (s + 1), err)) return;
+  }
+}
+
 template <typename F>
 float timeit(F launch) {
   hipEvent_t a, b;
@@ -198,8 +267,23 @@ int main() {
   hipFuncSetAttribute((const void*)kB<4, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, 8192 + 2 * WSTEP);
   hipFuncSetAttribute((const void*)kB<8, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 8192 + 2 * WSTEP);
   const int sh = 8192 + 2 * WSTEP;
-  for (int c = 0; c < 2; ++c) {
+  unsigned* err;
+  hipMalloc(&err, 4);
+  hipMemset(err, 0, 4);
+  hipFuncSetAttribute((const void*)kC<2, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, 8192 + 2 * WSTEP + 64);
+  hipFuncSetAttribute((const void*)kC<3, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, 8192 + 3 * WSTEP + 64);
+  hipFuncSetAttribute((const void*)kC<3, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 8192 + 3 * WSTEP + 64);
+  hipFuncSetAttribute((const void*)kC<3, 0, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 8192 + 3 * WSTEP + 64);
+  hipFuncSetAttribute((const void*)kC<3, 0, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 8192 + 3 * WSTEP + 64);
+  hipFuncSetAttribute((const void*)kC<3, 2, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 8192 + 3 * WSTEP + 64);
+  for (int c = 0; c < 1; ++c) {
     cold = c == 1;
+    per_step("C ring NS=2", [&](int s) { hipLaunchKernelGGL((kC<2, 0>), dim3(64), dim3(576), 8192 + 2 * WSTEP + 64, 0, W, out, s, err); });
+    per_step("C ring NS=3", [&](int s) { hipLaunchKernelGGL((kC<3, 0>), dim3(64), dim3(576), 8192 + 3 * WSTEP + 64, 0, W, out, s, err); });
+    per_step("C ring NS=3 no stores", [&](int s) { hipLaunchKernelGGL((kC<3, 2>), dim3(64), dim3(576), 8192 + 3 * WSTEP + 64, 0, W, out, s, err); });
+    per_step("C ring NS=3 L=4", [&](int s) { hipLaunchKernelGGL((kC<3, 0, 4>), dim3(64), dim3(768), 8192 + 3 * WSTEP + 64, 0, W, out, s, err); });
+    per_step("C ring NS=3 L=8", [&](int s) { hipLaunchKernelGGL((kC<3, 0, 8>), dim3(64), dim3(1024), 8192 + 3 * WSTEP + 64, 0, W, out, s, err); });
+    per_step("C ring NS=3 L=8 no st", [&](int s) { hipLaunchKernelGGL((kC<3, 2, 8>), dim3(64), dim3(1024), 8192 + 3 * WSTEP + 64, 0, W, out, s, err); });
     per_step("A LA=1", [&](int s) { hipLaunchKernelGGL((kA<0, 2>), dim3(64), dim3(512), 8192, 0, W, out, s); });
     per_step("A LA=2", [&](int s) { hipLaunchKernelGGL((kA<0, 3>), dim3(64), dim3(512), 8192, 0, W, out, s); });
     per_step("A LA=3", [&](int s) { hipLaunchKernelGGL((kA<0, 4>), dim3(64), dim3(512), 8192, 0, W, out, s); });
@@ -220,5 +304,8 @@ int main() {
     per_step("B L=4 LA=3", [&](int s) { hipLaunchKernelGGL((kB<4, 3>), dim3(64), dim3(768), sh, 0, W, out, s); });
     per_step("B L=8 LA=2", [&](int s) { hipLaunchKernelGGL((kB<8, 2>), dim3(64), dim3(1024), sh, 0, W, out, s); });
   }
+  unsigned herr = 0;
+  hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost);
+  printf("spin time-outs: %u\n", herr);
   return 0;
 }
