@@ -460,9 +460,9 @@ __device__ __forceinline__ void chain_body(const FastNet& net, const RowArgs& a,
       f32x4 sd, z;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        sd[i] = expf(0.5f * lv[i]);
+        sd[i] = __expf(0.5f * lv[i]);
         z[i] = y[i] + ep[i] * sd[i];
-        if (4 * q + i < nrows) s_kl += 1.f + lv[i] - y[i] * y[i] - expf(lv[i]);
+        if (4 * q + i < nrows) s_kl += 1.f + lv[i] - y[i] * y[i] - __expf(lv[i]);
       }
       *(f32x4*)(MULV + j * R + 4 * q) = y;
       *(f32x4*)(MULV + (Z + j) * R + 4 * q) = lv;
@@ -656,7 +656,7 @@ __device__ __forceinline__ void chain_body(const FastNet& net, const RowArgs& a,
           for (int i = 0; i < 4; ++i) {
             const bool live = 4 * q + i < nrows;
             gm[i] = live ? a.w_kld * mu[i] * inv_BZ + acc[i] : 0.f;
-            gl[i] = live ? a.w_kld * 0.5f * (expf(lv[i]) - 1.f) * inv_BZ + acc[i] * ep[i] * 0.5f * sd[i] : 0.f;
+            gl[i] = live ? a.w_kld * 0.5f * (__expf(lv[i]) - 1.f) * inv_BZ + acc[i] * ep[i] * 0.5f * sd[i] : 0.f;
           }
           const bf16x4 hm = to_bf4(gm), hl = to_bf4(gl);
           *(bf16x4*)(GFC + ioff(j, q)) = hm;
