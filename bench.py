@@ -37,14 +37,15 @@ PEAK = {"bf16": 2500.0, "fp32": 157.3}  # dense TFLOP/s, MI355X_MICROARCH.md chi
 HBM_PEAK_GBS = 8000.0                      # HBM3E peak, MI355X_MICROARCH.md
 
 
-def fwd_macs(S, D, Z, H, C=2):
-    """F of SURVEY §8d: forward multiply-accumulates per trajectory (4+4 layers)."""
+def fwd_macs(S, D, Z, H, C=2, n_enc=4, n_dec=4):
+    """F of SURVEY §8d: forward multiply-accumulates per trajectory (4+4 layers by default)."""
     I = S * D
-    return (C * H + H * H) + (I * H + 3 * H * H) + 2 * (2 * H * Z) + ((Z + H) * H + 2 * H * H + H * I)
+    return ((C * H + H * H) + (I * H + (n_enc - 1) * H * H) + 2 * (2 * H * Z)
+            + ((Z + H) * H + (n_dec - 2) * H * H + H * I))
 
 
-def flops_per_traj(S, D, Z, H, C=2):
-    F = fwd_macs(S, D, Z, H, C)
+def flops_per_traj(S, D, Z, H, C=2, n_enc=4, n_dec=4):
+    F = fwd_macs(S, D, Z, H, C, n_enc, n_dec)
     I = S * D
     return {"total": 2 * (3 * F - C * H - I * H),
             "rowchain": 2 * F + 2 * (F - C * H - I * H),  # forward + every dX
@@ -94,11 +95,11 @@ def measured_traffic(path, kernel, batch, dtype):
     return None if k is None else k["traffic_bytes"]
 
 
-def cpu_baseline(B, S, D, Z, H, seconds):
+def cpu_baseline(B, S, D, Z, H, seconds, n_enc=4, n_dec=4):
     from oracle.cvae_oracle import OracleCVAE, oracle_step
     threads = torch.get_num_threads()
     torch.manual_seed(0)
-    model = OracleCVAE(S, D, Z, H)
+    model = OracleCVAE(S, D, Z, H, n_enc, n_dec)
     opt = torch.optim.Adam(model.parameters(), lr=1e-3)
     x = torch.randn(B, S, D, generator=torch.Generator().manual_seed(1234))
     times = []
@@ -112,7 +113,7 @@ def cpu_baseline(B, S, D, Z, H, seconds):
     med = times[len(times) // 2]
     return {"value": round(B / med, 1), "unit": "trajectories/s", "cores": threads, "kind": "port",
             "sample": f"{len(times)} steps of the oracle step (Training_VAE.py:345-363 body, torch-CPU fp32, "
-                      f"B={B} S={S} D={D} Z={Z} H={H}), median {med * 1e3:.2f} ms/step"}
+                      f"B={B} S={S} D={D} Z={Z} H={H}, {n_enc}+{n_dec} layers), median {med * 1e3:.2f} ms/step"}
 
 
 def main():
@@ -125,6 +126,11 @@ def main():
     ap.add_argument("--dim", type=int, default=6)
     ap.add_argument("--latent", type=int, default=8)
     ap.add_argument("--hidden", type=int, default=128)
+    ap.add_argument("--n-enc", type=int, default=4)
+    ap.add_argument("--n-dec", type=int, default=4)
+    ap.add_argument("--workload", default="cfg2", choices=["cfg2", "wide"],
+                    help="cfg2: the headline (S=100, Z=8, 4+4 layers); wide: BASELINE cfg5's shape "
+                         "(S=200, Z=512, 8+8 layers; bf16 operands, the fp8 variant is not built)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -147,9 +153,12 @@ def main():
     from cvae_amd import ConditionalTrajectoryVAE
     from cvae_amd.dist import DataParallelStep
 
+    if args.workload == "wide":
+        args.seq_len, args.latent, args.n_enc, args.n_dec = 200, 512, 8, 8
     B, S, D, Z, H = args.batch, args.seq_len, args.dim, args.latent, args.hidden
+    NE, ND = args.n_enc, args.n_dec
     torch.manual_seed(0)
-    model = ConditionalTrajectoryVAE(S, D, Z, H)
+    model = ConditionalTrajectoryVAE(S, D, Z, H, NE, ND)
     eng = model.attach(dtype=args.dtype, max_batch=B, device=dev, seed=4321 + rank)
     x = torch.randn(B, S, D, generator=torch.Generator().manual_seed(1234 + rank))
     x = eng.as_input(x)  # resident in HBM, operand dtype
@@ -194,9 +203,9 @@ def main():
         assert torch.isfinite(eng.loss).all(), "non-finite loss"
 
     if rank == 0:
-        fl = flops_per_traj(S, D, Z, H)
+        fl = flops_per_traj(S, D, Z, H, n_enc=NE, n_dec=ND)
         tsize = 2 if args.dtype == "bf16" else 4
-        bt = bytes_per_traj(S, D, Z, H, tsize)
+        bt = bytes_per_traj(S, D, Z, H, tsize, n_enc=NE, n_dec=ND)
         n_par = eng.n_params
         flop = {"rowchain": fl["rowchain"] * B, "wgrad": fl["wgrad"] * B, "wgrad_adam": fl["wgrad"] * B}
         nbytes = {"rowchain": bt["rowchain"] * B, "wgrad": bt["wgrad"] * B + 4 * n_par,
@@ -205,25 +214,28 @@ def main():
         flop["fused_step"] = flop["rowchain"] + flop["wgrad_adam"]
         nbytes["fused_step"] = nbytes["rowchain"] + nbytes["wgrad_adam"]
         dom = max((k for k in kt if k in flop), key=lambda k: kt[k][0])
-        traffic = measured_traffic(args.traffic_file, dom, B, args.dtype)
+        wide = (S, D, Z, H, NE, ND) != (100, 6, 8, 128, 4, 4)
+        traffic = None if wide else measured_traffic(args.traffic_file, dom, B, args.dtype)
         roof = roofline(dom, kt[dom][0], flop[dom], nbytes[dom], args.dtype, traffic)
         roof["kernels_ms"] = {k: round(v[0], 5) for k, v in kt.items()}
         if b2b:
             roof["kernels_back_to_back_ms"] = {k: round(v, 5) for k, v in b2b.items()}
         value = world * B * args.steps / t
-        res = {"metric": "trajectories/sec per ELBO step, batch=1024 seq_len=100; 1/2/4/8 MI355X",
+        metric = ("trajectories/sec per ELBO step, batch=1024 seq_len=100; 1/2/4/8 MI355X" if not wide else
+                  f"trajectories/sec per ELBO step, batch={B} seq_len={S} (BASELINE cfg5 shape, bf16 not fp8)")
+        res = {"metric": metric,
                "value": round(value, 1), "unit": "trajectories/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(t / args.steps * 1e3, 5), "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
                "data": "synthetic x~N(0,1) (seeded), random-init weights (torch.manual_seed(0))",
                "config": {"workload": f"Training_VAE step, B_local={B} S={S} D={D} Z={Z} H={H}, "
-                                      f"4+4 layers, {args.dtype} operands / fp32 master+Adam",
+                                      f"{NE}+{ND} layers, {args.dtype} operands / fp32 master+Adam",
                           "global_batch": B * world, "seq_len": S, "state_dim": D, "latent_dim": Z,
                           "hidden_dim": H, "parallelism": f"dp{world}"},
                "roofline": roof,
                "flop_per_traj": fl["total"]}
         if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(B, S, D, Z, H, args.cpu_seconds)
+            res["cpu_baseline"] = cpu_baseline(B, S, D, Z, H, args.cpu_seconds, NE, ND)
             res["speedup_vs_cpu"] = round(value / res["cpu_baseline"]["value"], 1)
         print(json.dumps(res), flush=True)
     if world > 1:

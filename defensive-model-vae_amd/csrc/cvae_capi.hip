@@ -92,10 +92,8 @@ int build_plan(cvae_handle* h) {
   n.ZHp = rup_i(n.Z + n.H, 32); n.Zp2 = rup_i(2 * n.Z, 32); n.Cp = 32;
   n.dtype = c.dtype;
   h->tsize = c.dtype == CVAE_BF16 ? 2 : 4;
-  h->R = c.dtype == CVAE_BF16 ? RowsPerTile<__bf16>::R : RowsPerTile<float>::R;
   // arena rows: whole row tiles, and a multiple of the K chunk of the wgrad GEMM
   n.Bp = rup_i(c.max_batch, 32);
-  h->max_row_tiles = rup_i(c.max_batch, 32) / h->R;
 
   // layer table (in = K, out = N) in state_dict order
   struct LD { int K, N, relu; };
@@ -140,12 +138,22 @@ int build_plan(cvae_handle* h) {
     n.bias_off[l] = n.nbias;
     n.nbias += n.L[l].Np;
   }
-  // LDS budget of the row-chain kernel
-  const LdsPlan lp = lds_plan(n, h->R, h->tsize);
-  h->lds_bytes = lp.total;
-  if (lp.total > 160 * 1024)
-    return fail(CVAE_E_INVALID, "configuration needs " + std::to_string(lp.total) +
-                                    " B of LDS per row tile (> 160 KiB); reduce seq_len*dim or latent_dim");
+  // LDS budget of the row-chain kernel: the largest row tile (16, 8 or 4 rows) whose state fits
+  // in 160 KiB.  Tiles under 16 rows leave MFMA rows idle (duplicated rows), so they only serve
+  // the wide configurations (latent 512, seq_len 200: SURVEY cfg5) that need them.
+  // CVAE_ROW_TILE=<4|8|16> in the environment caps the tile (A/B measurements)
+  const char* rt_env = std::getenv("CVAE_ROW_TILE");
+  const int rt_cap = rt_env ? std::atoi(rt_env) : CVAE_ROWS;
+  h->R = 0;
+  for (int R : {CVAE_ROWS, 8, 4}) {
+    if (R > CVAE_ROWS || (R > rt_cap && R > 4)) continue;
+    const LdsPlan lp = lds_plan(n, R, h->tsize);
+    if (lp.total <= 160 * 1024) { h->R = R; h->lds_bytes = lp.total; break; }
+  }
+  if (!h->R)
+    return fail(CVAE_E_INVALID, "configuration needs " + std::to_string(lds_plan(n, 4, h->tsize).total) +
+                                    " B of LDS per 4-row tile (> 160 KiB); reduce seq_len*dim or latent_dim");
+  h->max_row_tiles = rup_i(c.max_batch, 32) / h->R;
   if (c.dim < 3) return fail(CVAE_E_INVALID, "dim must be >= 3 (channel 0 = time, 1:3 = x,y)");
   if (c.hidden_dim % 4 || c.latent_dim % 4)
     return fail(CVAE_E_INVALID, "hidden_dim and latent_dim must be multiples of 4 (4-feature epilogue vectors)");
@@ -357,9 +365,8 @@ int alloc_arena(cvae_handle* h) {
   return CVAE_OK;
 }
 
-template <typename T>
-int set_lds_attrs(cvae_handle* h) {
-  constexpr int R = RowsPerTile<T>::R;
+template <typename T, int R>
+int set_lds_attrs_r(cvae_handle* h) {
   HIPCK(hipFuncSetAttribute((const void*)rowchain_kernel<T, R, RC_TRAIN>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, h->lds_bytes));
   HIPCK(hipFuncSetAttribute((const void*)rowchain_kernel<T, R, RC_FWD>,
@@ -367,6 +374,13 @@ int set_lds_attrs(cvae_handle* h) {
   HIPCK(hipFuncSetAttribute((const void*)rowchain_kernel<T, R, RC_DECODE>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, h->lds_bytes));
   return CVAE_OK;
+}
+template <typename T>
+int set_lds_attrs(cvae_handle* h) {
+  if (h->R == CVAE_ROWS) return set_lds_attrs_r<T, CVAE_ROWS>(h);
+  if (h->R == 8) return set_lds_attrs_r<T, 8>(h);
+  if (h->R == 4) return set_lds_attrs_r<T, 4>(h);
+  return fail(CVAE_E_INVALID, "no row-chain instance for this row tile");
 }
 
 // ---- timing helpers (no syncs).  With timing on, tmark(name) names the next kernel launch and
@@ -402,9 +416,8 @@ int klaunch(cvae_handle* h, void (*kernel)(KArgs...), dim3 grid, dim3 block, siz
   return CVAE_OK;
 }
 
-template <typename T, int MODE>
-int launch_rowchain(cvae_handle* h, RowArgs a, hipStream_t s) {
-  constexpr int R = RowsPerTile<T>::R;
+template <typename T, int MODE, int R>
+int launch_rowchain_r(cvae_handle* h, RowArgs a, hipStream_t s) {
   // the grid covers roundup(batch, 32) rows: the wgrad K range (a multiple of the 32-deep bf16
   // chunk) then only reads rows this launch wrote (zeros past the batch)
   const int grid = rup_i(a.batch, 32) / R;
@@ -415,6 +428,13 @@ int launch_rowchain(cvae_handle* h, RowArgs a, hipStream_t s) {
   a.nsteps = h->n_steps[st];
   a.stamps = h->d_stamps;
   return klaunch(h, rowchain_kernel<T, R, MODE>, dim3(grid), dim3(RC_THREADS), h->lds_bytes, s, h->net, a);
+}
+template <typename T, int MODE>
+int launch_rowchain(cvae_handle* h, RowArgs a, hipStream_t s) {
+  if (h->R == CVAE_ROWS) return launch_rowchain_r<T, MODE, CVAE_ROWS>(h, a, s);
+  if (h->R == 8) return launch_rowchain_r<T, MODE, 8>(h, a, s);
+  if (h->R == 4) return launch_rowchain_r<T, MODE, 4>(h, a, s);
+  return fail(CVAE_E_INVALID, "no row-chain instance for this row tile");
 }
 
 int check_batch(cvae_handle* h, int batch) {
@@ -488,7 +508,7 @@ int plan_fast(cvae_handle* h) {
   h->fast_nki = 0;
   const char* env = std::getenv("CVAE_GENERIC");
   if ((env && env[0] == '1') || c.dtype != CVAE_BF16 || c.hidden_dim != fchain::H || c.latent_dim != fchain::Z ||
-      c.n_enc != 4 || c.n_dec != 4 || n.I % 8 != 0 || n.nbias > 16 * fchain::NT)
+      c.n_enc != 4 || c.n_dec != 4 || n.I % 8 != 0 || n.nbias > 16 * fchain::NT || h->R != 16)
     return CVAE_OK;
   for (int nki : kFastNki) {
     if (n.Ip != 32 * nki) continue;

@@ -184,7 +184,7 @@ struct RowArgs {
 struct LdsPlan {
   int sx, sp, shc, sdec, scin;   // row strides (elements of T)
   int mw;                        // mask words per row
-  int oXin, oP0, oP1, oHc, oDec, oCin, oMuLv, oEps, oStd, oDz, oU, oRch0, oGd0, oStart, oRow, oMask, oPart, oBias, oSteps;
+  int oXin, oP0, oP1, oHc, oDec, oCin, oMuLv, oDz, oU, oRch0, oGd0, oStart, oRow, oMask, oPart, oBias, oSteps;
   int total;
 };
 
@@ -210,8 +210,6 @@ __host__ __device__ inline LdsPlan lds_plan(const NetDev& n, int R, int tsize) {
   p.oDec = take(R * p.sdec * tsize);
   p.oCin = take(R * p.scin * tsize);
   p.oMuLv = take(R * n.Zp2 * 4);
-  p.oEps = take(R * n.Z * 4);
-  p.oStd = take(R * n.Z * 4);
   p.oDz = take(R * n.Z * 4);
   const int ub = (2 * n.S > n.H ? 2 * n.S : n.H) * R * 4;
   p.oU = take(ub);
@@ -489,8 +487,6 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
   T* const Dec = (T*)(smem + P.oDec);
   T* const Cin = (T*)(smem + P.oCin);
   float* const MuLv = (float*)(smem + P.oMuLv);
-  float* const Eps = (float*)(smem + P.oEps);
-  float* const Std = (float*)(smem + P.oStd);
   float* const Dz = (float*)(smem + P.oDz);
   float* const Rch0 = (float*)(smem + P.oRch0);
   float* const Gd0 = (float*)(smem + P.oGd0);
@@ -906,8 +902,6 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
           z = mu + ep * sd;
           s_kl += 1.f + lv - mu * mu - expf(lv);
         }
-        Eps[r * Z + j] = ep;
-        Std[r * Z + j] = sd;
         Dec[r * P.sdec + j] = to_t<T>(z);
         if (TRAIN && !CVAE_DIAG_NOSTORE) gst<T>(xd0 + aoff(j, b0 + r, net.L[lD(net, 0)].Kp), to_t<T>(z));
       }
@@ -950,8 +944,13 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
           if (c < Z) {
             g = a.w_kld * MuLv[r * net.Zp2 + j] * inv_BZ + dz;
           } else {
+            // eps and std are recomputed (same draw, same expf) rather than kept in LDS: at
+            // latent 512 two R x Z fp32 buffers would not fit beside the rest of the tile state
             const float lv = MuLv[r * net.Zp2 + Z + j];
-            g = a.w_kld * 0.5f * (expf(lv) - 1.f) * inv_BZ + dz * Eps[r * Z + j] * 0.5f * Std[r * Z + j];
+            const float sd = expf(0.5f * lv);
+            const float ep = a.eps ? gld<float>(a.eps + (size_t)(b0 + r) * Z + j)
+                                   : philox_normal(a.seed, a.offset, (uint32_t)(b0 + r), (uint32_t)j);
+            g = a.w_kld * 0.5f * (expf(lv) - 1.f) * inv_BZ + dz * ep * 0.5f * sd;
           }
         }
         P0b[r * P.sp + c] = to_t<T>(g);

@@ -48,9 +48,22 @@ def test_unsupported_config_reports_error(cl):
     from cvae_amd import config_info
     from cvae_amd._lib import CvaeError
     with pytest.raises(CvaeError, match="LDS"):
-        config_info(200, 6, 512, 128, 8, 8, dtype="bf16")
+        config_info(1000, 6, 2048, 128, 8, 8, dtype="bf16")
     with pytest.raises(CvaeError, match="dim"):
         config_info(10, 2, 8)
+
+
+def test_wide_cfg5_config_plans(cl):
+    """BASELINE cfg5's shape (S=200, Z=512, 8+8 layers) plans with a smaller row tile: its tile
+    state fits 160 KiB of LDS with 8 rows (bf16) / 4 rows (fp32), not 16."""
+    from cvae_amd import config_info
+    for dt in ("bf16", "fp32"):
+        n, nt, lds = config_info(200, 6, 512, 128, 8, 8, dtype=dt)
+        assert nt == 2 * (2 + 8 + 2 + 8) and 0 < lds <= 160 * 1024
+        H, I, Z = 128, 1200, 512
+        want = (2 * H + H) + (H * H + H) + (I * H + H) + 7 * (H * H + H) + 2 * (2 * H * Z + Z) \
+            + ((Z + H) * H + H) + 6 * (H * H + H) + (H * I + I)
+        assert n == want
 
 
 def test_engine_refuses_without_gpu(cl):

@@ -410,3 +410,93 @@ def test_misaligned_input_runs_generic_chain(cvae):
     torch.cuda.synchronize()
     np.testing.assert_allclose(e1.loss.cpu().numpy(), e2.loss.cpu().numpy(), rtol=2e-3, atol=1e-6)
     assert float((e1.params - e2.params).norm() / e1.params.norm()) < 1e-3
+
+
+# ---- BASELINE cfg5 shape: latent 512, 8 + 8 layers, seq_len 200 (bf16 operands here; the fp8
+# variant is not built).  The generic row chain runs it with 8-row tiles (bf16) or 4-row tiles
+# (fp32): the tile state does not fit 16 rows in 160 KiB of LDS at this width.
+WIDE = dict(S=200, D=6, Z=512, n_enc=8, n_dec=8)
+
+
+def _wide(cvae, dtype, B, seed=0):
+    torch.manual_seed(seed)
+    ref = OracleCVAE(WIDE["S"], WIDE["D"], WIDE["Z"], 128, WIDE["n_enc"], WIDE["n_dec"])
+    m = cvae.ConditionalTrajectoryVAE(WIDE["S"], WIDE["D"], WIDE["Z"], 128, WIDE["n_enc"], WIDE["n_dec"])
+    m.load_state_dict(ref.state_dict())
+    eng = m.attach(dtype=dtype, max_batch=max(B, 32), device="cuda:0")
+    x = torch.randn(B, WIDE["S"], WIDE["D"], generator=torch.Generator().manual_seed(1234))
+    eps = torch.randn(B, WIDE["Z"], generator=torch.Generator().manual_seed(4321))
+    return ref, m, eng, x, eps
+
+
+def _oracle_grads(ref, x, eps):
+    rel, start = relative(x)
+    r, mu, lv, hc = ref(rel, start, eps)
+    ls = oracle_loss(r, rel, mu, lv, hc, **WD)
+    ls[0].backward()
+    return np.array([float(v.detach()) for v in ls]), {k: p.grad.numpy() for k, p in ref.named_parameters()}
+
+
+@pytest.mark.parametrize("B", [37, 128])
+def test_wide_cfg5_fp32_vs_oracle(cvae, B):
+    ref, m, eng, x, eps = _wide(cvae, "fp32", B)
+    assert list(m.state_dict().keys()) == list(ref.state_dict().keys())
+    loss = eng.forward_backward(x, eps=eps).cpu().numpy()
+    want, gw = _oracle_grads(ref, x, eps)
+    np.testing.assert_allclose(loss, want, rtol=5e-5, atol=1e-7)
+    g = _grads(m, eng)
+    for k in gw:
+        assert rel_l2(g[k], gw[k]) < 2e-4, (k, rel_l2(g[k], gw[k]))
+
+
+def test_wide_cfg5_bf16_matches_bf16_emulation(cvae):
+    """bf16 kernels at the cfg5 shape against the CPU emulation of their rounding points (tight),
+    and against the fp32 reference (the bf16 operand-rounding distance, loose)."""
+    B = 64
+    ref, m, eng, x, eps = _wide(cvae, "bf16", B)
+    x = x.to(torch.bfloat16).float()
+    loss = eng.forward_backward(x, eps=eps).cpu().numpy()
+    p = {k: v.numpy() for k, v in ref.state_dict().items()}
+    ne, nd = WIDE["n_enc"], WIDE["n_dec"]
+    r, mu, lv, hc, c = cvae_np.forward(p, x.numpy(), eps.numpy(), n_enc=ne, n_dec=nd, q=cvae_np.bf16)
+    np.testing.assert_allclose(loss, cvae_np.losses(r, c["rel"], mu, lv), rtol=3e-3, atol=1e-6)
+    gw = cvae_np.backward(p, c, r, mu, lv, n_enc=ne, n_dec=nd)
+    g = _grads(m, eng)
+    for k in cvae_np.param_keys(ne, nd):
+        assert rel_l2(g[k], gw[k]) < 3e-2, (k, rel_l2(g[k], gw[k]))
+    want, _ = _oracle_grads(ref, x, eps)
+    np.testing.assert_allclose(loss, want, rtol=3e-2, atol=1e-6)
+
+
+def test_wide_cfg5_bf16_training_full_batch(cvae):
+    """B=1024 at the cfg5 shape: the fused train step stays finite and lowers the ELBO; the
+    two-launch split path (data-parallel route) equals it bit for bit."""
+    ref, m, eng, x, _ = _wide(cvae, "bf16", 1024)
+    m2 = cvae.ConditionalTrajectoryVAE(WIDE["S"], WIDE["D"], WIDE["Z"], 128, WIDE["n_enc"], WIDE["n_dec"])
+    m2.load_state_dict(ref.state_dict())
+    e2 = m2.attach(dtype="bf16", max_batch=1024, device="cuda:0")
+    x = x.cuda()
+    eps = torch.randn(1024, WIDE["Z"], generator=torch.Generator().manual_seed(7))
+    for _ in range(3):
+        eng.train_step(x, eps=eps)
+        e2.forward_backward(x, eps=eps)
+        e2.adam_step(1.0)
+    torch.cuda.synchronize()
+    assert torch.equal(eng.params, e2.params)
+    first = eng.train_step(x).clone()
+    for _ in range(30):
+        last = eng.train_step(x)
+    torch.cuda.synchronize()
+    assert torch.isfinite(eng.params).all()
+    assert float(last[0]) < float(first[0])
+
+
+def test_wide_cfg5_generate(cvae):
+    """Batched generation (decode mode) at the cfg5 shape vs the oracle decoder."""
+    ref, m, eng, _, _ = _wide(cvae, "fp32", 48)
+    st = torch.randn(48, 2) * 20
+    z = torch.randn(48, WIDE["Z"])
+    rel, ab = m.generate(st, z=z.cuda())
+    with torch.no_grad():
+        want = ref.decode(z, ref.condition_encoder(st))
+    assert rel_l2(rel.cpu().numpy(), want.numpy()) < 1e-5
