@@ -154,3 +154,57 @@ def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidd
             if log:
                 log(f"Model saved to {model_save_path}")
     return model, loss_history, weighted
+
+
+def default_paths(data_path, latent_dim, epochs):
+    """The reference's save paths (Training_VAE.py:283-287): model and loss names from the dataset
+    file name ('trajectory_sce1_cond.npy' → 'vae_offset_sce1_cond_ld8_epoch3000_loss2.*')."""
+    name = os.path.splitext(os.path.basename(data_path))[0].replace("trajectory_", "", 1)
+    stem = f"vae_offset_{name}_ld{latent_dim}_epoch{epochs}_loss2"
+    return os.path.join("training", "models", stem + ".pth"), os.path.join("training", "loss", stem + ".png")
+
+
+def main(argv=None):
+    """``python -m cvae_amd.train --data training/DefensiveDataProcessed/trajectory_sce1_cond.npy``:
+    the reference's ``__main__`` in mode='training' (Training_VAE.py:271-394) with its parameters
+    as flags (same defaults: seq_len 10, dim 3, latent 8, batch 38, lr 1e-3, 3000 epochs, weights
+    0.1/0.1/1.0/1.0).  Under ``torch.distributed.run`` every rank trains its share over RCCL."""
+    import argparse
+    ap = argparse.ArgumentParser(description=main.__doc__)
+    ap.add_argument("--data", required=True, help="(N, seq_len, dim) .npy (Traj_Data_Process output)")
+    ap.add_argument("--seq-len", type=int, default=10)
+    ap.add_argument("--dim", type=int, default=3)
+    ap.add_argument("--latent", type=int, default=8)
+    ap.add_argument("--hidden", type=int, default=128)
+    ap.add_argument("--batch-size", type=int, default=38, help="per rank under data parallelism")
+    ap.add_argument("--lr", type=float, default=1e-3)
+    ap.add_argument("--epochs", type=int, default=3000)
+    ap.add_argument("--weights", type=float, nargs=4, default=(0.1, 0.1, 1.0, 1.0),
+                    metavar=("RECON", "KLD", "START", "TIME"))
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--eps", default="host", choices=["host", "philox"])
+    ap.add_argument("--seed", type=int, default=None)
+    ap.add_argument("--model-out", default=None)
+    ap.add_argument("--loss-out", default=None)
+    a = ap.parse_args(argv)
+    model_out, loss_out = default_paths(a.data, a.latent, a.epochs)
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    device = None
+    if world_size > 1:
+        import torch.distributed as tdist
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+        tdist.init_process_group("nccl", device_id=device)
+    try:
+        train(a.data, a.seq_len, a.dim, a.latent, batch_size=a.batch_size, lr=a.lr, epochs=a.epochs,
+              hidden_dim=a.hidden, weights=tuple(a.weights), model_save_path=a.model_out or model_out,
+              loss_save_path=a.loss_out or loss_out, dtype=a.dtype, eps=a.eps, device=device, seed=a.seed)
+    finally:
+        if world_size > 1:
+            torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -500,3 +500,17 @@ def test_wide_cfg5_generate(cvae):
     with torch.no_grad():
         want = ref.decode(z, ref.condition_encoder(st))
     assert rel_l2(rel.cpu().numpy(), want.numpy()) < 1e-5
+
+
+def test_train_cli_end_to_end(cvae, golden, tmp_path):
+    """python -m cvae_amd.train (the reference __main__ as a CLI): two epochs on the sce1 rows,
+    checkpoint with the 24 reference keys and the loss CSV written."""
+    from cvae_amd.train import main
+    data = tmp_path / "trajectory_sce1_cond.npy"
+    np.save(data, golden("sce_fixed.npz")["sce1_x"].astype(np.float64))
+    mo, lo = tmp_path / "m.pth", tmp_path / "loss.png"
+    main(["--data", str(data), "--epochs", "2", "--seed", "0", "--model-out", str(mo), "--loss-out", str(lo)])
+    sd = torch.load(mo, weights_only=True)
+    assert list(sd.keys()) == list(OracleCVAE(10, 3, 8).state_dict().keys())
+    rows = (tmp_path / "loss.csv").read_text().strip().splitlines()
+    assert rows[0].split(",")[0] == "total_loss" and len(rows) == 3
