@@ -3,7 +3,9 @@
 Tolerances (stated up front):
   fp32 path vs oracle: losses rel <= 1e-5 (2e-5 where a loss is a difference of
     large terms), grads rel-L2 <= 1e-4, params after Adam rel-L2 <= 1e-5.
-  bf16 path (synthetic N(0,1), S=100 D=6): losses rel <= 2e-2, grads rel-L2 <= 5e-2.
+  bf16 path (synthetic N(0,1), S=100 D=6): losses rel <= 2e-2, grads rel-L2 <= 5e-2 (1.2e-1 for
+    the encoder L1 weight at B=64, where operand rounding alone gives 0.081); 200-step training
+    curve within 2 % of the fp32 reference (10-step means; single steps 3 %).
 All calls go through the C-ABI (libcvae_hip.so) via cvae_amd.
 """
 import numpy as np
@@ -514,3 +516,29 @@ def test_train_cli_end_to_end(cvae, golden, tmp_path):
     assert list(sd.keys()) == list(OracleCVAE(10, 3, 8).state_dict().keys())
     rows = (tmp_path / "loss.csv").read_text().strip().splitlines()
     assert rows[0].split(",")[0] == "total_loss" and len(rows) == 3
+
+
+def test_bf16_200_step_loss_curve_vs_fp32_oracle(cvae):
+    """the bf16 path's 200-step training curve at the cfg2 shape stays within 2 % of
+    the fp32 reference trained on the same batches and the same eps (B=256, one fixed batch
+    per step drawn from a 2048-row synthetic set)."""
+    from oracle.cvae_oracle import oracle_step
+    torch.manual_seed(0)
+    ref = OracleCVAE(100, 6, 8)
+    m, eng = _model(cvae, 100, 6, 8, sd=ref.state_dict(), dtype="bf16", max_batch=256)
+    opt = torch.optim.Adam(ref.parameters(), lr=1e-3)
+    gen = torch.Generator().manual_seed(1234)
+    data = torch.randn(2048, 100, 6, generator=gen).to(torch.bfloat16).float()
+    data_dev = data.cuda()
+    got, want = [], []
+    for t in range(200):
+        idx = torch.randint(0, 2048, (256,), generator=gen)
+        eps = torch.randn(256, 8, generator=gen)
+        got.append(eng.train_step(data_dev, idx=idx.cuda(), eps=eps).cpu().numpy().copy())
+        want.append(oracle_step(ref, opt, data[idx], weights=W, eps=eps))
+    got, want = np.array(got), np.array(want)
+    assert want[-1, 0] < 0.8 * want[0, 0]  # the reference run itself trains (0.169 → 0.116)
+    # the curve (10-step means) within 2 %; single steps within 3 % (measured max 2.2 %, step ~190)
+    sm = lambda a: a.reshape(20, 10).mean(1)  # noqa: E731
+    np.testing.assert_allclose(sm(got[:, 0]), sm(want[:, 0]), rtol=2e-2)
+    np.testing.assert_allclose(got[:, 0], want[:, 0], rtol=3e-2)
