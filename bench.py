@@ -33,7 +33,7 @@ for _p in (ROOT, os.path.join(ROOT, "defensive-model-vae_amd")):
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-PEAK = {"bf16": 2500.0, "fp32": 157.3}  # dense TFLOP/s, MI355X_MICROARCH.md chip table
+PEAK = {"bf16": 2500.0, "fp32": 157.3, "fp8": 5000.0}  # dense TFLOP/s, MI355X_MICROARCH.md chip table
 HBM_PEAK_GBS = 8000.0                      # HBM3E peak, MI355X_MICROARCH.md
 
 
@@ -131,7 +131,7 @@ def main():
     ap.add_argument("--workload", default="cfg2", choices=["cfg2", "wide"],
                     help="cfg2: the headline (S=100, Z=8, 4+4 layers); wide: BASELINE cfg5's shape "
                          "(S=200, Z=512, 8+8 layers; bf16 operands, the fp8 variant is not built)")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp8"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-b2b", action="store_true",
@@ -204,7 +204,7 @@ def main():
 
     if rank == 0:
         fl = flops_per_traj(S, D, Z, H, n_enc=NE, n_dec=ND)
-        tsize = 2 if args.dtype == "bf16" else 4
+        tsize = 4 if args.dtype == "fp32" else 2  # fp8: bf16 activations
         bt = bytes_per_traj(S, D, Z, H, tsize, n_enc=NE, n_dec=ND)
         n_par = eng.n_params
         flop = {"rowchain": fl["rowchain"] * B, "wgrad": fl["wgrad"] * B, "wgrad_adam": fl["wgrad"] * B}

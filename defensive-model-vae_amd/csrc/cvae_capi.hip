@@ -80,6 +80,8 @@ struct cvae_handle {
 namespace {
 
 int rup_i(int v, int a) { return (v + a - 1) / a * a; }
+// 16-bit activation/arena types: bf16, and CVAE_FP8 (bf16 activations, e4m3 forward operands)
+inline bool is16(const cvae_handle* h) { return h->cfg.dtype != CVAE_F32; }
 
 int build_plan(cvae_handle* h) {
   const cvae_config& c = h->cfg;
@@ -91,7 +93,7 @@ int build_plan(cvae_handle* h) {
   n.Ip = rup_i(n.I, 32); n.Hp = rup_i(n.H, 32); n.Hcp = rup_i(2 * n.H, 32);
   n.ZHp = rup_i(n.Z + n.H, 32); n.Zp2 = rup_i(2 * n.Z, 32); n.Cp = 32;
   n.dtype = c.dtype;
-  h->tsize = c.dtype == CVAE_BF16 ? 2 : 4;
+  h->tsize = c.dtype == CVAE_F32 ? 4 : 2;  // CVAE_FP8 keeps bf16 activations (only forward W/X operands are e4m3)
   // arena rows: whole row tiles, and a multiple of the K chunk of the wgrad GEMM
   n.Bp = rup_i(c.max_batch, 32);
 
@@ -120,6 +122,7 @@ int build_plan(cvae_handle* h) {
   for (int l = 0; l < (int)ld.size(); ++l) {
     LayerDev& L = n.L[l];
     L.K = ld[l].K; L.N = ld[l].N; L.Kp = rup_i(L.K, 32); L.Np = rup_i(L.N, 32); L.relu = ld[l].relu;
+    L.f8 = c.dtype == CVAE_FP8 && L.Kp % 64 == 0;  // fp8 forward GEMM where K pairs up (cvae_device.h)
     if (l == lFC(n)) {
       L.nseg = 2; L.seg_rows0 = n.Z;
       L.pw[0] = add(n.Z, L.K); L.pb[0] = add(n.Z, 0);
@@ -198,7 +201,7 @@ std::vector<StepSpec> build_steps(const NetDev& n, int mode) {
   auto fwd = [&](int l, int xbuf, int epi) {
     StepSpec s = blank();
     const LayerDev& L = n.L[l];
-    s.W = L.Wf; s.bias_off = n.bias_off[l]; s.Kp = L.Kp; s.Np = L.Np; s.N = L.N;
+    s.W = L.Wf; s.bias_off = n.bias_off[l]; s.Kp = L.Kp; s.Np = L.Np; s.N = L.N; s.f8 = L.f8;
     s.xbuf = xbuf; s.epi = epi;
     return s;
   };
@@ -301,7 +304,7 @@ int alloc_arena(cvae_handle* h) {
   std::vector<Off> lo(n.n_layers);
   for (int l = 0; l < n.n_layers; ++l) {
     LayerDev& L = n.L[l];
-    lo[l].wf = take((int64_t)L.Np * L.Kp * ts);
+    lo[l].wf = take((int64_t)L.Np * L.Kp * ts + (L.f8 ? (int64_t)sizeof(F8Scale) : 0));
     lo[l].wb = take((int64_t)L.Kp * L.Np * ts);
     lo[l].bias = n.bias_off[l];  // planned in build_plan
   }
@@ -326,7 +329,7 @@ int alloc_arena(cvae_handle* h) {
   h->arena_bytes = total;
   for (int l = 0; l < n.n_layers; ++l) {
     LayerDev& L = n.L[l];
-    L.Wf = h->arena + lo[l].wf;
+    L.Wf = h->arena + lo[l].wf + (L.f8 ? sizeof(F8Scale) : 0);  // f8: F8Scale header in front
     L.Wb = h->arena + lo[l].wb;
     L.bias = (float*)(h->arena + bias_base) + lo[l].bias;
     L.xT = h->arena + lo[l].xT;
@@ -575,7 +578,7 @@ int launch_wgrad(cvae_handle* h, int batch, const AdamArgs& aa, const LossArgs& 
     return klaunch(h, fchain::fastwgrad_kernel<19, MODE>, dim3(fchain::Tiles<19>::total() + 1), dim3(WG_THREADS),
                    0, s, h->arena, aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), h->net.S, h->net.D, h->net.I,
                    aa, la);
-  if (h->cfg.dtype == CVAE_BF16)
+  if (is16(h))
     return klaunch(h, wgrad_kernel<__bf16, MODE>, dim3(nt), dim3(WG_THREADS), 0, s, h->net,
                    (const TileDesc*)h->d_tiles, bk_of(h, batch), aa, la);
   return klaunch(h, wgrad_kernel<float, MODE>, dim3(nt), dim3(WG_THREADS), 0, s, h->net,
@@ -619,7 +622,8 @@ int cvae_abi_version(void) { return CVAE_ABI_VERSION; }
 int cvae_create(const cvae_config* cfg, int device, cvae_handle** out) {
   if (!cfg || !out) return fail(CVAE_E_INVALID, "null argument");
   if (cfg->seq_len < 1 || cfg->dim < 1 || cfg->latent_dim < 1 || cfg->hidden_dim < 1 || cfg->n_enc < 1 ||
-      cfg->n_dec < 1 || cfg->max_batch < 1 || (cfg->dtype != CVAE_F32 && cfg->dtype != CVAE_BF16))
+      cfg->n_dec < 1 || cfg->max_batch < 1 ||
+      (cfg->dtype != CVAE_F32 && cfg->dtype != CVAE_BF16 && cfg->dtype != CVAE_FP8))
     return fail(CVAE_E_INVALID, "invalid cvae_config");
   cvae_handle* h = new cvae_handle();
   h->cfg = *cfg;
@@ -629,7 +633,7 @@ int cvae_create(const cvae_config* cfg, int device, cvae_handle** out) {
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) { delete h; return fail(CVAE_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e)); }
   rc = alloc_arena(h);
-  if (!rc) rc = h->cfg.dtype == CVAE_BF16 ? set_lds_attrs<__bf16>(h) : set_lds_attrs<float>(h);
+  if (!rc) rc = is16(h) ? set_lds_attrs<__bf16>(h) : set_lds_attrs<float>(h);
   if (!rc) rc = plan_fast(h);
   if (rc) { cvae_destroy(h); return rc; }
   *out = h;
@@ -684,7 +688,9 @@ int cvae_pack_weights(cvae_handle* h, const float* params, void* stream) {
   AdamArgs aa{};
   aa.params = (float*)params;
   const int nt = (int)h->tiles.size();
-  if (h->cfg.dtype == CVAE_BF16)
+  if (h->cfg.dtype == CVAE_FP8)  // per-layer e4m3 weight scales first: the pack reads them
+    hipLaunchKernelGGL(f8_scale_kernel, dim3(h->net.n_layers), dim3(CVAE_THREADS), 0, s, h->net, (const float*)params);
+  if (is16(h))
     hipLaunchKernelGGL((param_kernel<__bf16, PM_PACK>), dim3(nt), dim3(CVAE_THREADS), 0, s, h->net, h->d_tiles, aa);
   else
     hipLaunchKernelGGL((param_kernel<float, PM_PACK>), dim3(nt), dim3(CVAE_THREADS), 0, s, h->net, h->d_tiles, aa);
@@ -703,7 +709,7 @@ int cvae_forward(cvae_handle* h, const void* x, const int64_t* idx, int batch, c
   a.recon_out = recon; a.mu_out = mu; a.lv_out = logvar; a.hc_out = hc;
   a.partials = h->d_partials;
   hipStream_t s = (hipStream_t)stream;
-  return h->cfg.dtype == CVAE_BF16 ? launch_rowchain<__bf16, RC_FWD>(h, a, s) : launch_rowchain<float, RC_FWD>(h, a, s);
+  return is16(h) ? launch_rowchain<__bf16, RC_FWD>(h, a, s) : launch_rowchain<float, RC_FWD>(h, a, s);
 }
 
 int cvae_condition(cvae_handle* h, const float* start, int batch, float* hc, void* stream) {
@@ -714,7 +720,7 @@ int cvae_condition(cvae_handle* h, const float* start, int batch, float* hc, voi
   a.batch = batch; a.start_in = start; a.hc_out = hc;
   a.partials = h->d_partials;
   hipStream_t s = (hipStream_t)stream;
-  return h->cfg.dtype == CVAE_BF16 ? launch_rowchain<__bf16, RC_DECODE>(h, a, s)
+  return is16(h) ? launch_rowchain<__bf16, RC_DECODE>(h, a, s)
                                    : launch_rowchain<float, RC_DECODE>(h, a, s);
 }
 
@@ -727,7 +733,7 @@ int cvae_decode(cvae_handle* h, const float* z, const float* start, const float*
   a.batch = batch; a.z_in = z; a.start_in = start; a.hc_in = hc; a.recon_out = out;
   a.partials = h->d_partials;
   hipStream_t s = (hipStream_t)stream;
-  return h->cfg.dtype == CVAE_BF16 ? launch_rowchain<__bf16, RC_DECODE>(h, a, s)
+  return is16(h) ? launch_rowchain<__bf16, RC_DECODE>(h, a, s)
                                    : launch_rowchain<float, RC_DECODE>(h, a, s);
 }
 
@@ -740,7 +746,7 @@ int cvae_train_fwd_bwd(cvae_handle* h, const void* x, const int64_t* idx, int ba
   hipStream_t s = (hipStream_t)stream;
   tbegin(h);
   RowArgs ra;
-  rc = h->cfg.dtype == CVAE_BF16 ? train_fwd_bwd_impl<__bf16>(h, x, idx, batch, eps, seed, offset, w, s, ra)
+  rc = is16(h) ? train_fwd_bwd_impl<__bf16>(h, x, idx, batch, eps, seed, offset, w, s, ra)
                                  : train_fwd_bwd_impl<float>(h, x, idx, batch, eps, seed, offset, w, s, ra);
   if (rc) return rc;
   AdamArgs aa{};
@@ -759,7 +765,7 @@ int cvae_adam(cvae_handle* h, float* params, const float* grads, float* m, float
   const int nt = (int)h->tiles.size();
   int rc = tmark(h, s, "adam");
   if (rc) return rc;
-  if (h->cfg.dtype == CVAE_BF16)
+  if (is16(h))
     return klaunch(h, param_kernel<__bf16, PM_ADAM>, dim3(nt), dim3(CVAE_THREADS), 0, s, h->net,
                    (const TileDesc*)h->d_tiles, aa);
   return klaunch(h, param_kernel<float, PM_ADAM>, dim3(nt), dim3(CVAE_THREADS), 0, s, h->net,
@@ -779,7 +785,7 @@ int cvae_train_step(cvae_handle* h, const void* x, const int64_t* idx, int batch
   AdamArgs aa = make_adam(params, nullptr, m, v, step, lr, beta1, beta2, adam_eps, 1.f);
   if (use_fused(h, x)) return launch_fused(h, x, idx, batch, eps, seed, offset, w, aa, loss_out, loss_accum, s);
   RowArgs ra;
-  rc = h->cfg.dtype == CVAE_BF16 ? train_fwd_bwd_impl<__bf16>(h, x, idx, batch, eps, seed, offset, w, s, ra)
+  rc = is16(h) ? train_fwd_bwd_impl<__bf16>(h, x, idx, batch, eps, seed, offset, w, s, ra)
                                  : train_fwd_bwd_impl<float>(h, x, idx, batch, eps, seed, offset, w, s, ra);
   if (rc) return rc;
   const LossArgs la = make_loss(h, ra, loss_out, loss_accum);
@@ -822,7 +828,7 @@ int cvae_bench_kernels(cvae_handle* h, const void* x, const int64_t* idx, int ba
       int rc2 = CVAE_OK;
       RowArgs ra;
       if (which == 0) {
-        rc2 = h->cfg.dtype == CVAE_BF16 ? train_fwd_bwd_impl<__bf16>(h, x, idx, batch, nullptr, 1, r, &w, s, ra)
+        rc2 = is16(h) ? train_fwd_bwd_impl<__bf16>(h, x, idx, batch, nullptr, 1, r, &w, s, ra)
                                         : train_fwd_bwd_impl<float>(h, x, idx, batch, nullptr, 1, r, &w, s, ra);
       } else if (which == 1) {
         AdamArgs aa = make_adam(params, nullptr, m, v, step0 + r, lr, b1, b2, ae, 1.f);

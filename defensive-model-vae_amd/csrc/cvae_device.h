@@ -31,9 +31,9 @@ struct LayerDev {
   int K, N, Kp, Np;      // real / padded in-out dims
   int relu;              // 1: ReLU after this layer
   int nseg, seg_rows0;   // parameter segments along N (fc fuses mu‖logvar: 2 segments)
-  int pad_;
+  int f8;                // CVAE_FP8: Wf holds OCP e4m3 fragments (pair-chunk order, f8_wf_off), see below
   int64_t pw[2], pb[2];  // flat fp32 offsets of weight / bias of each segment
-  void* Wf;              // [Np][Kp] T
+  void* Wf;              // [Np][Kp] T  (f8: [Np][Kp] e4m3, preceded by the F8Scale header)
   void* Wb;              // [Kp][Np] T
   float* bias;           // [Np] fp32
   void* xT;              // [Kp][Bp] T   input of the layer (feature-major)
@@ -115,6 +115,41 @@ __host__ __device__ inline size_t frag_off(int n, int k, int Kp) {
   const int q = EPL == 8 ? (kk & 15) >> 2 : kk >> 2;
   const int e = EPL == 8 ? (kk & 3) + ((kk >> 4) << 2) : kk & 3;
   return ((size_t)(t * (Kp / KC) + kc) * 64 + q * 16 + r) * EPL + e;
+}
+
+// ------------------------------------------------------------------ fp8 forward operands (CVAE_FP8)
+// BASELINE cfg5 asks for fp8 MFMA GEMMs.  With dtype CVAE_FP8 every forward layer whose padded K
+// is a multiple of 64 multiplies OCP e4m3 weights by e4m3 activations (v_mfma_f32_16x16x32_fp8_fp8,
+// fp32 accumulate); activations, arena, dX (Wb) and dW stay bf16, master weights/Adam/loss fp32.
+// Weights carry a per-layer power-of-two scale s (F8Scale, written on the device by
+// cvae_pack_weights from the layer's |W| max with 4x headroom): Wf = e4m3(s·W), and the
+// forward epilogue multiplies the accumulator by 1/s.  Activations are converted unscaled
+// (saturating at ±448).  Layout: a 16-B lane fragment holds TWO 32-wide K chunks (2c in bytes
+// 0-7, 2c+1 in bytes 8-15), each in frag_k order — so a step loads 16 B per (n-tile, K/64
+// pair) exactly like a bf16 step over half the K: the weight stream halves.
+struct F8Scale { float s, inv_s; float pad_[62]; };  // 256 B in front of Wf
+constexpr float F8_MAX = 448.f;
+__host__ __device__ inline size_t f8_wf_off(int n, int kc, int Kp) {  // byte offset of lane-fragment (n-tile, chunk kc) lane 0
+  return ((size_t)((n >> 4) * (Kp / 64) + (kc >> 1)) * 64) * 16 + (kc & 1) * 8;
+}
+__device__ __forceinline__ const F8Scale* f8_header(const void* Wf) {
+  return (const F8Scale*)((const char*)Wf - sizeof(F8Scale));
+}
+// 8 values → 8 e4m3 bytes (RNE, saturated to ±448), element e in byte e
+__device__ __forceinline__ long f8x8(const float (&v)[8]) {
+  int w0 = 0, w1 = 0;
+  auto c = [](float x) { return fminf(fmaxf(x, -F8_MAX), F8_MAX); };
+  w0 = __builtin_amdgcn_cvt_pk_fp8_f32(c(v[0]), c(v[1]), w0, false);
+  w0 = __builtin_amdgcn_cvt_pk_fp8_f32(c(v[2]), c(v[3]), w0, true);
+  w1 = __builtin_amdgcn_cvt_pk_fp8_f32(c(v[4]), c(v[5]), w1, false);
+  w1 = __builtin_amdgcn_cvt_pk_fp8_f32(c(v[6]), c(v[7]), w1, true);
+  return (long)(unsigned)w0 | ((long)(unsigned)w1 << 32);
+}
+__device__ __forceinline__ long f8x8(bf16x8 x) {
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = (float)x[e];
+  return f8x8(v);
 }
 
 template <typename T> __device__ __forceinline__ T to_t(float v);

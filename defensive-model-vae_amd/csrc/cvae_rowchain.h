@@ -129,6 +129,7 @@ struct StepSpec {
   int concat;        // skip columns >= N (destination is part of a concatenation)
   int hc_out;        // inference: also write h_c (fp32) to RowArgs::hc_out
   int kf1, kf2;      // feature rows of the g1 / g2 arena matrices (aoff)
+  int f8;            // CVAE_FP8 forward step (e4m3 W and X)
 };
 
 // ... and as the kernel reads it: 64 B, copied into LDS by the prologue and read back every step
@@ -150,7 +151,8 @@ static_assert(sizeof(StepDesc) == 64, "StepDesc is 4 x 16 B");
 inline StepDesc encode_step(const StepSpec& s) {
   StepDesc d{};
   d.W = s.W; d.g1 = s.g1; d.g2 = s.g2;
-  d.Kp = s.Kp; d.Np = s.Np; d.N = s.N; d.bias_off = s.bias_off;
+  d.Kp = s.f8 ? (s.Kp / 2) | (1 << 30) : s.Kp;  // f8: the weight stream counts 64-wide K pairs
+  d.Np = s.Np; d.N = s.N; d.bias_off = s.bias_off;
   d.code = s.xbuf | (s.epi << 4) | ((s.dst1 + 1) << 8) | ((s.dst2 + 1) << 12) | (s.concat << 16) |
            (s.hc_out << 17) | ((s.mask_out + 1) << 20) | ((s.mask_in + 1) << 26);
   d.off1 = s.off1; d.off2 = s.off2;
@@ -285,7 +287,7 @@ __device__ __forceinline__ bf16x8 xchunk<__bf16>(const __bf16* p, int q) {
 template <typename T, int R, bool BIAS, class Epi>
 __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T* __restrict__ W, int Kp, int Np,
                                       WBlock<T>& pre, const T* nW, int nKp, int nNp, const float* biasL,
-                                      Epi&& epi) {
+                                      Epi&& epi, bool f8 = false, float inv_s = 1.f) {
   using V = typename Op<T>::V;
   constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC, MT = R >= 16 ? R / 16 : 1;
   const int lane = threadIdx.x & 63, wave = wave_id();
@@ -333,22 +335,55 @@ __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T
     // all LDS reads of the block first (one lgkmcnt wait per block, not per chunk), then the
     // MFMAs unconditionally: chunks past K read a clamped (valid) address and are zeroed, so a
     // short block costs a few idle MFMAs instead of branches and per-chunk waits
-    V xa[NKB][MT];
+    bool f8_done = false;
+    if constexpr (EPL == 8) {
+      if (f8) {  // CVAE_FP8 forward step: a 16-B fragment = two 32-wide K chunks of e4m3 (Kp, nk count K/64 pairs)
+        long x8[NKB][MT][2];
 #pragma unroll
-    for (int u = 0; u < NKB; ++u) {
-      const int kc = min(blk * NKB + u, nk - 1);
+        for (int u = 0; u < NKB; ++u) {
+          const int kc = min(blk * NKB + u, nk - 1);
 #pragma unroll
-      for (int m = 0; m < MT; ++m) xa[u][m] = xchunk<T>(Xs + tile_row<R>(m, r16) * ldx + kc * KC, lane >> 4);
+          for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh)
+              x8[u][m][hh] = f8x8(xchunk<T>(Xs + tile_row<R>(m, r16) * ldx + kc * 2 * KC + hh * KC, lane >> 4));
+        }
+#pragma unroll
+        for (int u = 0; u < NKB; ++u) {
+          const bool on = blk * NKB + u < nk;
+#pragma unroll
+          for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int j = 0; j < RC_NT; ++j) {
+              typedef long l2 __attribute__((ext_vector_type(2)));
+              const l2 wa = __builtin_bit_cast(l2, cur.b[u][j]);
+              if (!CVAE_DIAG_NOMFMA) {
+                acc[j][m] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(wa[0], on ? x8[u][m][0] : 0l, acc[j][m], 0, 0, 0);
+                acc[j][m] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(wa[1], on ? x8[u][m][1] : 0l, acc[j][m], 0, 0, 0);
+              }
+            }
+        }
+        f8_done = true;
+      }
     }
+    if (!f8_done) {
+      V xa[NKB][MT];
 #pragma unroll
-    for (int u = 0; u < NKB; ++u) {
-      const bool on = blk * NKB + u < nk;
+      for (int u = 0; u < NKB; ++u) {
+        const int kc = min(blk * NKB + u, nk - 1);
 #pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        const V xb = on ? xa[u][m] : V{};
+        for (int m = 0; m < MT; ++m) xa[u][m] = xchunk<T>(Xs + tile_row<R>(m, r16) * ldx + kc * KC, lane >> 4);
+      }
 #pragma unroll
-        for (int j = 0; j < RC_NT; ++j)
-          if (!CVAE_DIAG_NOMFMA) acc[j][m] = mfma_chunk(cur.b[u][j], xb, acc[j][m]);
+      for (int u = 0; u < NKB; ++u) {
+        const bool on = blk * NKB + u < nk;
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          const V xb = on ? xa[u][m] : V{};
+#pragma unroll
+          for (int j = 0; j < RC_NT; ++j)
+            if (!CVAE_DIAG_NOMFMA) acc[j][m] = mfma_chunk(cur.b[u][j], xb, acc[j][m]);
+        }
       }
     }
     // issued behind the MFMAs: all waves issue their loads right after a barrier, and the CU's
@@ -363,7 +398,7 @@ __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T
       for (int j = 0; j < RC_NT; ++j)
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
-          epi(tile_row<R>(m, r16), g * RC_GW + j * 16 + (lane >> 4) * 4, acc[j][m], b4[j]);
+          epi(tile_row<R>(m, r16), g * RC_GW + j * 16 + (lane >> 4) * 4, f8 ? acc[j][m] * inv_s : acc[j][m], b4[j]);
           acc[j][m] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
 #if CVAE_DIAG_SUB
@@ -525,7 +560,7 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
   WBlock<T> pre;
   {
     const StepDesc s0 = a.steps[0];
-    load_block(pre, (const T*)s0.W, s0.Kp, s0.Np, wave, 0);
+    load_block(pre, (const T*)s0.W, s0.Kp & 0x3FFFFFFF, s0.Np, wave, 0);
   }
   stamp();
 
@@ -722,14 +757,16 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
     const T* const W = (const T*)sptr(q0.x, q0.y);
     T* const g1 = (T*)sptr(q0.z, q0.w);
     T* const g2 = (T*)sptr(q1.x, q1.y);
-    const int Kp = (int)sgpr(q1.z), Np = (int)sgpr(q1.w), N = (int)sgpr(q2.x), bias_off = (int)sgpr(q2.y);
+    const uint32_t kraw = sgpr(q1.z);
+    const bool f8 = (kraw >> 30) & 1;  // CVAE_FP8 forward step (Kp then counts K/2: the e4m3 pair chunks)
+    const int Kp = (int)(kraw & 0x3FFFFFFFu), Np = (int)sgpr(q1.w), N = (int)sgpr(q2.x), bias_off = (int)sgpr(q2.y);
     const uint32_t code = sgpr(q2.z);
     const int off1 = (int)sgpr(q2.w), off2 = (int)sgpr(q3.x);
     const uint32_t goff = sgpr(q3.y);
     const int kf1 = (int)sgpr(q3.z), kf2 = (int)sgpr(q3.w);
     const int goff1 = (int)(goff & 0xFFFF), goff2 = (int)(goff >> 16);
     const T* const nW = has_next ? (const T*)sptr(n0.x, n0.y) : (const T*)nullptr;
-    const int nKp = (int)sgpr(n1.z), nNp = (int)sgpr(n1.w);
+    const int nKp = (int)(sgpr(n1.z) & 0x3FFFFFFFu), nNp = (int)sgpr(n1.w);
     const int xbuf = code & 15, kind = (code >> 4) & 15;
     const int dst1 = (int)((code >> 8) & 15) - 1, dst2 = (int)((code >> 12) & 15) - 1;
     const bool concat = (code >> 16) & 1, hc_o = (code >> 17) & 1;
@@ -752,7 +789,8 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
     // One dense instance per epilogue kind (the switch is wave-uniform): each epilogue compiles
     // straight-line with only its own live values.
     auto run = [&](auto&& epi) {
-      dense<T, R, true>(buf(xbuf), ld_of(xbuf), W, Kp, Np, pre, nW, nKp, nNp, biasL, epi);
+      dense<T, R, true>(buf(xbuf), ld_of(xbuf), W, Kp, Np, pre, nW, nKp, nNp, biasL, epi, f8,
+                        f8 ? f8_header(W)->inv_s : 1.f);
     };
     auto run_nb = [&](auto&& epi) {  // backward steps: no bias
       dense<T, R, false>(buf(xbuf), ld_of(xbuf), W, Kp, Np, pre, nW, nKp, nNp, biasL, epi);

@@ -253,6 +253,16 @@ __device__ __forceinline__ void store_operands(const LayerDev& L, int o0, int i0
 #pragma unroll
       for (int e = 0; e < EPL; ++e) val[e] = to_t<T>(wt[(kl + frag_k<T>(q, e)) * LD + nl]);
       gst<V>((T*)L.Wb + ((size_t)(((i0 >> 4) + bt) * (L.Np / KC) + (o0 + kl) / KC) * 64 + ln) * EPL, val);
+    } else if (EPL == 8 && L.f8) {  // CVAE_FP8: e4m3(s·W), 8 B per lane into its K-pair fragment
+      const float sc = f8_header(L.Wf)->s;
+      float f[8];
+#pragma unroll
+      for (int e = 0; e < 8; e += 4) {
+        const f32x4 v4 = *(const f32x4*)(wt + nl * LD + kl + frag_k<T>(q, e));
+#pragma unroll
+        for (int c = 0; c < 4; ++c) f[e + c] = v4[c] * sc;
+      }
+      gst<long>((long*)((char*)L.Wf + f8_wf_off(o0 + bt * 16, (i0 + kl) / 32, L.Kp) + (size_t)ln * 16), f8x8(f));
     } else {
 #pragma unroll
       for (int e = 0; e < EPL; e += 4) {  // 4 consecutive K positions per half-fragment
@@ -489,3 +499,34 @@ __global__ __launch_bounds__(CVAE_THREADS) void param_kernel(NetDev net, const T
   }
   tile_epilogue<T, MODE, CVAE_THREADS, 4>(L, td.o0, td.i0, st, sb, g4, db, aa, wt);
 }
+
+// CVAE_FP8: the per-layer weight scale of the e4m3 forward operand (cvae_device.h F8Scale), one
+// block per layer: s = 2^floor(log2(448 / (4·max|W|))) — a power of two (exact to apply and to
+// undo), with 4x headroom so Adam's drift between packs stays inside e4m3's range (beyond it the
+// conversion saturates).  Run by cvae_pack_weights before the pack; Adam then writes Wf with s.
+__global__ __launch_bounds__(CVAE_THREADS) void f8_scale_kernel(NetDev net, const float* __restrict__ params) {
+  const LayerDev& L = net.L[blockIdx.x];
+  if (!L.f8) return;
+  float m = 0.f;
+  const int n = L.N * L.K;
+  for (int j = threadIdx.x; j < n; j += CVAE_THREADS) {
+    const int o = j / L.K, i = j - o * L.K;
+    const int seg = (L.nseg == 2 && o >= L.seg_rows0) ? 1 : 0;
+    m = fmaxf(m, fabsf(params[L.pw[seg] + (int64_t)(seg ? o - L.seg_rows0 : o) * L.K + i]));
+  }
+  __shared__ float red[CVAE_THREADS];
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int k = CVAE_THREADS / 2; k > 0; k >>= 1) {
+    if ((int)threadIdx.x < k) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + k]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float amax = red[0];
+    const float sc = amax > 0.f ? exp2f(floorf(log2f(F8_MAX / (4.f * amax)))) : 1.f;
+    F8Scale* hd = (F8Scale*)((char*)L.Wf - sizeof(F8Scale));
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    gst<f32x2>(&hd->s, f32x2{sc, 1.f / sc});  // vector store
+  }
+}
+

@@ -23,7 +23,7 @@ class CvaeLossWeights(C.Structure):
     _fields_ = [("recon", C.c_float), ("kld", C.c_float), ("start", C.c_float), ("time", C.c_float)]
 
 
-CVAE_F32, CVAE_BF16 = 0, 1
+CVAE_F32, CVAE_BF16, CVAE_FP8 = 0, 1, 2
 
 _SIGS = {
     "cvae_create": (C.c_int, [C.POINTER(CvaeConfig), C.c_int, C.POINTER(C.c_void_p)]),

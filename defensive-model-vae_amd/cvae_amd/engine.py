@@ -18,9 +18,11 @@ import ctypes as C
 
 import torch
 
-from ._lib import CVAE_BF16, CVAE_F32, CvaeConfig, CvaeLossWeights, check, lib, ptr
+from ._lib import CVAE_BF16, CVAE_F32, CVAE_FP8, CvaeConfig, CvaeLossWeights, check, lib, ptr
 
-DTYPES = {"fp32": (CVAE_F32, torch.float32), "bf16": (CVAE_BF16, torch.bfloat16)}
+# "fp8": bf16 activations with OCP e4m3 forward GEMM operands (BASELINE cfg5; cvae.h CVAE_FP8)
+DTYPES = {"fp32": (CVAE_F32, torch.float32), "bf16": (CVAE_BF16, torch.bfloat16),
+          "fp8": (CVAE_FP8, torch.bfloat16)}
 DEFAULT_WEIGHTS = (0.1, 0.1, 1.0, 1.0)  # Training_VAE.py:300-306
 
 

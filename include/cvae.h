@@ -28,7 +28,11 @@ extern "C" {
 
 #define CVAE_ABI_VERSION 1
 
-enum cvae_dtype { CVAE_F32 = 0, CVAE_BF16 = 1 };
+enum cvae_dtype {
+  CVAE_F32 = 0,
+  CVAE_BF16 = 1,
+  CVAE_FP8 = 2  /* bf16 activations + OCP e4m3 forward GEMM operands with per-layer scales (BASELINE cfg5) */
+};
 
 enum cvae_status {
   CVAE_OK = 0,

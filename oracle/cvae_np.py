@@ -48,17 +48,66 @@ def _ident(a):
     return a
 
 
-def _lin(x, p, name, q=_ident):
+E4M3_MAX = 448.0
+
+
+def e4m3(a):
+    """Round-to-nearest-even to OCP fp8 e4m3 (saturated at ±448), returned as float32 — the
+    rounding of v_cvt_pk_fp8_f32 behind the CVAE_FP8 kernels (cvae_device.h f8x8)."""
+    import torch  # the e4m3 cast (torch.float8_e4m3fn) is the only use of torch here
+
+    a = np.clip(np.ascontiguousarray(a, np.float32), -E4M3_MAX, E4M3_MAX)
+    return torch.from_numpy(a).to(torch.float8_e4m3fn).float().numpy()
+
+
+def f8_scale(*ws):
+    """Per-layer power-of-two weight scale of the fp8 operand: 2^floor(log2(448 / (4·max|W|)))
+    (cvae_wgrad.h f8_scale_kernel; fc_mu and fc_logvar share one, they are one fused layer)."""
+    amax = max(float(np.abs(w).max()) for w in ws)
+    return np.float32(2.0 ** np.floor(np.log2(E4M3_MAX / (4.0 * amax)))) if amax > 0 else np.float32(1.0)
+
+
+def _lin(x, p, name, q=_ident, sc=None):
+    if sc is not None:  # fp8 forward GEMM: e4m3(bf16 activations) x e4m3(s·W), result / s
+        w8 = e4m3(p[name + ".weight"].astype(np.float32) * sc)
+        return (e4m3(q(x)) @ w8.T) / sc + p[name + ".bias"]
     return q(x) @ q(p[name + ".weight"]).T + p[name + ".bias"]
 
 
-def forward(p, x, eps, n_enc=4, n_dec=4, dt=np.float32, q=None):
+def fp8_layers(p, seq_len, dim, latent_dim, hidden_dim=128, n_enc=4, n_dec=4):
+    """{layer name: scale} of the layers the CVAE_FP8 path runs in e4m3: padded K % 64 == 0
+    (cvae_capi.hip build_plan), K = the layer's input width."""
+    I, H, Z = seq_len * dim, hidden_dim, latent_dim
+    ks = {"condition_encoder.0": 2, "condition_encoder.2": H, "fc": 2 * H}
+    for i in range(n_enc):
+        ks[f"encoder.{2 * i + 1}"] = I if i == 0 else H
+    for i in range(n_dec):
+        ks[f"decoder.{2 * i}"] = Z + H if i == 0 else H
+    out = {}
+    for name, k in ks.items():
+        if (k + 31) // 32 * 32 % 64:
+            continue
+        if name == "fc":
+            s = f8_scale(p["fc_mu.weight"], p["fc_logvar.weight"])
+            out["fc_mu"] = out["fc_logvar"] = s
+        else:
+            out[name] = f8_scale(p[name + ".weight"])
+    return out
+
+
+def forward(p, x, eps, n_enc=4, n_dec=4, dt=np.float32, q=None, f8=None):
     """x: (B,S,D) absolute trajectories.  Returns (recon, mu, logvar, h_c, cache).
 
     q: operand quantiser (``bf16`` emulates the bf16 kernel path exactly: GEMM operands and
     stored activations rounded, accumulation and recon/loss in fp32, loss target = q(x_rel)).
+    f8: {layer name: scale} (``fp8_layers``) — those forward GEMMs run as e4m3 x e4m3 (CVAE_FP8).
     """
     q = q or _ident
+    f8 = f8 or {}
+
+    def lin(x, p, name, q=q):  # the layer's fp8 scale, if it has one
+        return _lin(x, p, name, q, f8.get(name))
+
     p = {k: v.astype(dt) for k, v in p.items()}
     x = x.astype(dt)
     B, S, D = x.shape
@@ -70,23 +119,23 @@ def forward(p, x, eps, n_enc=4, n_dec=4, dt=np.float32, q=None):
     a = rel.reshape(B, S * D)
     c["enc_in"] = [a]
     for i in range(n_enc):
-        a = np.maximum(_lin(a, p, f"encoder.{2 * i + 1}", q), 0)
+        a = np.maximum(lin(a, p, f"encoder.{2 * i + 1}"), 0)
         c["enc_in"].append(a)
-    h1 = np.maximum(_lin(start, p, "condition_encoder.0", q), 0)
-    hc = np.maximum(_lin(h1, p, "condition_encoder.2", q), 0)
+    h1 = np.maximum(lin(start, p, "condition_encoder.0"), 0)
+    hc = np.maximum(lin(h1, p, "condition_encoder.2"), 0)
     c["hc1"], c["hc"] = h1, hc
     h = np.concatenate([a, hc], 1)
     c["h"] = h
-    mu, lv = _lin(h, p, "fc_mu", q), _lin(h, p, "fc_logvar", q)
+    mu, lv = lin(h, p, "fc_mu"), lin(h, p, "fc_logvar")
     std = np.exp(dt(0.5) * lv)
     z = mu + c["eps"] * std
     c["std"] = std
     d = np.concatenate([z, hc], 1)
     c["dec_in"] = [d]
     for i in range(n_dec - 1):
-        d = np.maximum(_lin(d, p, f"decoder.{2 * i}", q), 0)
+        d = np.maximum(lin(d, p, f"decoder.{2 * i}"), 0)
         c["dec_in"].append(d)
-    r = _lin(d, p, f"decoder.{2 * (n_dec - 1)}", q).reshape(B, S, D)
+    r = lin(d, p, f"decoder.{2 * (n_dec - 1)}").reshape(B, S, D)
     return r, mu, lv, hc, c
 
 

@@ -57,7 +57,7 @@ def test_wide_cfg5_config_plans(cl):
     """BASELINE cfg5's shape (S=200, Z=512, 8+8 layers) plans with a smaller row tile: its tile
     state fits 160 KiB of LDS with 8 rows (bf16) / 4 rows (fp32), not 16."""
     from cvae_amd import config_info
-    for dt in ("bf16", "fp32"):
+    for dt in ("bf16", "fp32", "fp8"):
         n, nt, lds = config_info(200, 6, 512, 128, 8, 8, dtype=dt)
         assert nt == 2 * (2 + 8 + 2 + 8) and 0 < lds <= 160 * 1024
         H, I, Z = 128, 1200, 512
@@ -87,3 +87,26 @@ def test_model_init_and_state_dict_match_reference_layout(cl):
     assert list(sa.keys()) == list(sb.keys())
     for k in sa:
         assert torch.equal(sa[k], sb[k]), k
+
+
+def test_fp8_emulation_rounding_and_layer_choice():
+    """The CPU emulation of the CVAE_FP8 path (checker for test_hip_parity's fp8 tests): OCP e4m3
+    round-to-nearest-even with saturation, power-of-two weight scales with 4x headroom, and the
+    layers that run in fp8 (padded K % 64 == 0)."""
+    import numpy as np
+    from oracle import cvae_np
+    a = np.array([1.0625, 1.1875, 1.09375, 500.0, -1e4, 0.001, 2.0 ** -10, 240.0, 272.0], np.float32)
+    np.testing.assert_array_equal(cvae_np.e4m3(a),
+                                  [1.0, 1.25, 1.125, 448.0, -448.0, 2.0 ** -9, 0.0, 240.0, 256.0])
+    assert cvae_np.f8_scale(np.array([0.05, -0.1], np.float32)) == 1024.0  # 2^floor(log2(448 / 0.4))
+    torch_sd = OracleCVAE(100, 6, 8).state_dict()
+    p = {k: v.numpy() for k, v in torch_sd.items()}
+    f8 = cvae_np.fp8_layers(p, 100, 6, 8)
+    # cfg2: K=600 (pad 608) and K=Z+H=136 (pad 160) and K=2 stay bf16; every 128/256-wide K is fp8
+    assert set(f8) == {"condition_encoder.2", "encoder.3", "encoder.5", "encoder.7", "fc_mu", "fc_logvar",
+                       "decoder.2", "decoder.4", "decoder.6"}
+    assert f8["fc_mu"] == f8["fc_logvar"]
+    p5 = {k: v.numpy() for k, v in OracleCVAE(200, 6, 512, 128, 8, 8).state_dict().items()}
+    f85 = cvae_np.fp8_layers(p5, 200, 6, 512, 128, 8, 8)
+    assert "encoder.1" in f85 and "decoder.0" in f85 and "condition_encoder.0" not in f85
+
