@@ -187,8 +187,14 @@ struct LdsPlan {
   int sx, sp, shc, sdec, scin;   // row strides (elements of T)
   int mw;                        // mask words per row
   int oXin, oP0, oP1, oHc, oDec, oCin, oMuLv, oDz, oU, oRch0, oGd0, oStart, oRow, oMask, oPart, oBias, oSteps;
+  int oF8;                       // CVAE_FP8: e4m3 image of a wide step's input (R x F8_LD bytes)
   int total;
 };
+// CVAE_FP8 steps with K <= 256 convert their input once per step into an e4m3 LDS image in
+// fragment order ([row][chunk][q][8 B]; row stride 288 B keeps 8 rows x 4 lane groups on
+// distinct banks) instead of in every wave and column group (measured at cfg5: row chain 140 ->
+// 131 us).  Wider inputs (encoder L1, decoder L0) convert per chunk: their image would not fit.
+constexpr int F8_IMG_K = 256, F8_LD = F8_IMG_K + 32;
 
 __host__ __device__ inline int rup(int v, int a) { return (v + a - 1) / a * a; }
 
@@ -223,6 +229,7 @@ __host__ __device__ inline LdsPlan lds_plan(const NetDev& n, int R, int tsize) {
   p.oPart = take(RC_NW * 8 * 4);
   p.oBias = take((n.nbias + 4) * 4);  // + 4 zero floats: the bias of backward steps
   p.oSteps = take(64 * (int)sizeof(StepDesc));
+  p.oF8 = take(n.dtype == 2 /* CVAE_FP8 */ ? R * F8_LD : 0);
   p.total = o;
   return p;
 }
@@ -287,7 +294,8 @@ __device__ __forceinline__ bf16x8 xchunk<__bf16>(const __bf16* p, int q) {
 template <typename T, int R, bool BIAS, class Epi>
 __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T* __restrict__ W, int Kp, int Np,
                                       WBlock<T>& pre, const T* nW, int nKp, int nNp, const float* biasL,
-                                      Epi&& epi, bool f8 = false, float inv_s = 1.f) {
+                                      Epi&& epi, bool f8 = false, float inv_s = 1.f,
+                                      const uint8_t* f8img = nullptr) {
   using V = typename Op<T>::V;
   constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC, MT = R >= 16 ? R / 16 : 1;
   const int lane = threadIdx.x & 63, wave = wave_id();
@@ -346,7 +354,8 @@ __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T
           for (int m = 0; m < MT; ++m)
 #pragma unroll
             for (int hh = 0; hh < 2; ++hh)
-              x8[u][m][hh] = f8x8(xchunk<T>(Xs + tile_row<R>(m, r16) * ldx + kc * 2 * KC + hh * KC, lane >> 4));
+              x8[u][m][hh] = f8img ? *(const long*)(f8img + tile_row<R>(m, r16) * F8_LD + (kc * 2 + hh) * KC + (lane >> 4) * 8)
+                                   : f8x8(xchunk<T>(Xs + tile_row<R>(m, r16) * ldx + kc * 2 * KC + hh * KC, lane >> 4));
         }
 #pragma unroll
         for (int u = 0; u < NKB; ++u) {
@@ -531,6 +540,7 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
   uint8_t* const Mask = (uint8_t*)(smem + P.oMask);
   float* const Part = (float*)(smem + P.oPart);
   float* const BiasL = (float*)(smem + P.oBias);
+  uint8_t* const F8img = (uint8_t*)(smem + P.oF8);  // CVAE_FP8 only (0 B otherwise)
   // LDS buffer by id (a select chain on a uniform value: no runtime-indexed pointer array)
   auto buf = [&](int id) -> T* {
     return id == B_XIN ? Xin : id == B_P0 ? P0b : id == B_P1 ? P1b : id == B_HC ? Hc : id == B_DEC ? Dec : Cin;
@@ -785,12 +795,25 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
     // the step's bias lives in LDS (copied once in the prologue): the epilogue issues no
     // global loads, so it never waits behind the weight prefetch (vmcnt retires in order)
     const float* const biasL = BiasL + (bias_off >= 0 ? bias_off : net.nbias);
+    // CVAE_FP8 wide step: its input converted once into the e4m3 image (F8_IMG_K above)
+    const bool f8img = f8 && 2 * Kp <= F8_IMG_K;
+    if constexpr (Op<T>::EPL == 8) {
+      if (f8img) {
+        const T* const X8 = buf(xbuf);
+        const int ldx8 = ld_of(xbuf), nch = 2 * Kp / 32;
+        for (int it = threadIdx.x; it < R * nch * 4; it += RC_THREADS) {
+          const int q = it & 3, rc = it >> 2, r = rc / nch, c = rc - r * nch;
+          *(long*)(F8img + r * F8_LD + c * 32 + q * 8) = f8x8(xchunk<T>(X8 + r * ldx8 + c * 32, q));
+        }
+        lds_barrier();
+      }
+    }
 
     // One dense instance per epilogue kind (the switch is wave-uniform): each epilogue compiles
     // straight-line with only its own live values.
     auto run = [&](auto&& epi) {
       dense<T, R, true>(buf(xbuf), ld_of(xbuf), W, Kp, Np, pre, nW, nKp, nNp, biasL, epi, f8,
-                        f8 ? f8_header(W)->inv_s : 1.f);
+                        f8 ? f8_header(W)->inv_s : 1.f, f8img ? F8img : nullptr);
     };
     auto run_nb = [&](auto&& epi) {  // backward steps: no bias
       dense<T, R, false>(buf(xbuf), ld_of(xbuf), W, Kp, Np, pre, nW, nKp, nNp, biasL, epi);
