@@ -368,15 +368,22 @@ int alloc_arena(cvae_handle* h) {
   return CVAE_OK;
 }
 
-template <typename T, int R>
-int set_lds_attrs_r(cvae_handle* h) {
-  HIPCK(hipFuncSetAttribute((const void*)rowchain_kernel<T, R, RC_TRAIN>,
+template <typename T, int R, bool F8>
+int set_lds_attrs_rf(cvae_handle* h) {
+  HIPCK(hipFuncSetAttribute((const void*)rowchain_kernel<T, R, RC_TRAIN, F8>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, h->lds_bytes));
-  HIPCK(hipFuncSetAttribute((const void*)rowchain_kernel<T, R, RC_FWD>,
+  HIPCK(hipFuncSetAttribute((const void*)rowchain_kernel<T, R, RC_FWD, F8>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, h->lds_bytes));
-  HIPCK(hipFuncSetAttribute((const void*)rowchain_kernel<T, R, RC_DECODE>,
+  HIPCK(hipFuncSetAttribute((const void*)rowchain_kernel<T, R, RC_DECODE, F8>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, h->lds_bytes));
   return CVAE_OK;
+}
+// CVAE_FP8 runs its own instantiation (F8 = true): the bf16/fp32 kernels carry no fp8 code
+template <typename T, int R>
+int set_lds_attrs_r(cvae_handle* h) {
+  if constexpr (std::is_same<T, __bf16>::value)
+    if (h->cfg.dtype == CVAE_FP8) return set_lds_attrs_rf<T, R, true>(h);
+  return set_lds_attrs_rf<T, R, false>(h);
 }
 template <typename T>
 int set_lds_attrs(cvae_handle* h) {
@@ -430,7 +437,10 @@ int launch_rowchain_r(cvae_handle* h, RowArgs a, hipStream_t s) {
   a.steps = h->d_steps[st];
   a.nsteps = h->n_steps[st];
   a.stamps = h->d_stamps;
-  return klaunch(h, rowchain_kernel<T, R, MODE>, dim3(grid), dim3(RC_THREADS), h->lds_bytes, s, h->net, a);
+  if constexpr (std::is_same<T, __bf16>::value)
+    if (h->cfg.dtype == CVAE_FP8)
+      return klaunch(h, rowchain_kernel<T, R, MODE, true>, dim3(grid), dim3(RC_THREADS), h->lds_bytes, s, h->net, a);
+  return klaunch(h, rowchain_kernel<T, R, MODE, false>, dim3(grid), dim3(RC_THREADS), h->lds_bytes, s, h->net, a);
 }
 template <typename T, int MODE>
 int launch_rowchain(cvae_handle* h, RowArgs a, hipStream_t s) {

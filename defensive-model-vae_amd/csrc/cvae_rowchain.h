@@ -193,7 +193,8 @@ struct LdsPlan {
 // CVAE_FP8 steps with K <= 256 convert their input once per step into an e4m3 LDS image in
 // fragment order ([row][chunk][q][8 B]; row stride 288 B keeps 8 rows x 4 lane groups on
 // distinct banks) instead of in every wave and column group (measured at cfg5: row chain 140 ->
-// 131 us).  Wider inputs (encoder L1, decoder L0) convert per chunk: their image would not fit.
+// 131 us).  Wider inputs (encoder L1, decoder L0) convert per chunk (measured: an image in the
+// dead ping-pong buffer bought nothing).
 constexpr int F8_IMG_K = 256, F8_LD = F8_IMG_K + 32;
 
 __host__ __device__ inline int rup(int v, int a) { return (v + a - 1) / a * a; }
@@ -346,10 +347,13 @@ __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T
     bool f8_done = false;
     if constexpr (EPL == 8) {
       if (f8) {  // CVAE_FP8 forward step: a 16-B fragment = two 32-wide K chunks of e4m3 (Kp, nk count K/64 pairs)
+        // chunk pairs past K are skipped (uniform branches; no loads inside): a 128-wide K is
+        // 2 pairs of a 4-pair block, and issuing the idle half cost 25 % more MFMAs per launch
         long x8[NKB][MT][2];
 #pragma unroll
         for (int u = 0; u < NKB; ++u) {
           const int kc = min(blk * NKB + u, nk - 1);
+          if (blk * NKB + u >= nk) continue;
 #pragma unroll
           for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -359,7 +363,7 @@ __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T
         }
 #pragma unroll
         for (int u = 0; u < NKB; ++u) {
-          const bool on = blk * NKB + u < nk;
+          if (blk * NKB + u >= nk) continue;
 #pragma unroll
           for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -367,8 +371,8 @@ __device__ __forceinline__ void dense(const T* __restrict__ Xs, int ldx, const T
               typedef long l2 __attribute__((ext_vector_type(2)));
               const l2 wa = __builtin_bit_cast(l2, cur.b[u][j]);
               if (!CVAE_DIAG_NOMFMA) {
-                acc[j][m] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(wa[0], on ? x8[u][m][0] : 0l, acc[j][m], 0, 0, 0);
-                acc[j][m] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(wa[1], on ? x8[u][m][1] : 0l, acc[j][m], 0, 0, 0);
+                acc[j][m] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(wa[0], x8[u][m][0], acc[j][m], 0, 0, 0);
+                acc[j][m] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(wa[1], x8[u][m][1], acc[j][m], 0, 0, 0);
               }
             }
         }
@@ -517,7 +521,9 @@ __device__ __forceinline__ uint32_t mask4(const uint8_t* mk, int mw, int row, in
   return mk[row * mw + (f0 >> 2)];
 }
 
-template <typename T, int R, int MODE>
+// F8: the CVAE_FP8 instantiation (bf16 activations, e4m3 forward steps); without it every step's
+// fp8 flag is a constant false and the fp8 code folds away.
+template <typename T, int R, int MODE, bool F8 = false>
 __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using V = typename Op<T>::V;
@@ -768,7 +774,7 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
     T* const g1 = (T*)sptr(q0.z, q0.w);
     T* const g2 = (T*)sptr(q1.x, q1.y);
     const uint32_t kraw = sgpr(q1.z);
-    const bool f8 = (kraw >> 30) & 1;  // CVAE_FP8 forward step (Kp then counts K/2: the e4m3 pair chunks)
+    const bool f8 = F8 && ((kraw >> 30) & 1);  // CVAE_FP8 forward step (Kp then counts K/2: the e4m3 pair chunks)
     const int Kp = (int)(kraw & 0x3FFFFFFFu), Np = (int)sgpr(q1.w), N = (int)sgpr(q2.x), bias_off = (int)sgpr(q2.y);
     const uint32_t code = sgpr(q2.z);
     const int off1 = (int)sgpr(q2.w), off2 = (int)sgpr(q3.x);
@@ -796,7 +802,7 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
     // global loads, so it never waits behind the weight prefetch (vmcnt retires in order)
     const float* const biasL = BiasL + (bias_off >= 0 ? bias_off : net.nbias);
     // CVAE_FP8 wide step: its input converted once into the e4m3 image (F8_IMG_K above)
-    const bool f8img = f8 && 2 * Kp <= F8_IMG_K;
+    const bool f8img = F8 && f8 && 2 * Kp <= F8_IMG_K;
     if constexpr (Op<T>::EPL == 8) {
       if (f8img) {
         const T* const X8 = buf(xbuf);

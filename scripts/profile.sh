@@ -8,7 +8,7 @@ STEPS=${STEPS:-50}
 OUT=$GRAFT_REPO_ROOT/gpurun_out/prof
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-BENCH="$GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-b2b --steps $STEPS --warmup 5"
+BENCH="$GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-b2b --steps $STEPS --warmup 5 ${BENCH_EXTRA:-}"  # BENCH_EXTRA: e.g. --workload wide --dtype fp8
 P=${PASSES:-trace,sq1,sq2,sq3,ta,fetch,write}
 has() { case ",$P," in *",$1,"*) return 0;; *) return 1;; esac; }
 if has trace; then
