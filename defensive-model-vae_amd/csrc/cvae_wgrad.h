@@ -477,11 +477,7 @@ __global__ __launch_bounds__(WG_THREADS) void wgrad_kernel(NetDev net, const Til
 
 // Adam from a (reduced) gradient buffer, or repack of the operand copies.
 template <typename T, int MODE>
-__global__ __launch_bounds__(CVAE_THREADS) void param_kernel(NetDev net, const TileDesc* __restrict__ tiles,
-                                                             AdamArgs aa) {
-  __shared__ __attribute__((aligned(16))) float wt[32 * WT_LD];
-  const TileDesc td = tiles[blockIdx.x];
-  const LayerDev& L = net.L[td.layer];
+__device__ __forceinline__ void param_body(const LayerDev& L, const TileDesc& td, const AdamArgs& aa, float* wt) {
   const int tid = threadIdx.x;
   const PreN<4> st = loadn<MODE, 4>(L, td.o0 + (tid >> 3), td.i0 + (tid & 7) * 4, aa);
   PreB sb = {0.f, 0.f, 0.f, -1};
@@ -498,6 +494,14 @@ __global__ __launch_bounds__(CVAE_THREADS) void param_kernel(NetDev net, const T
     }
   }
   tile_epilogue<T, MODE, CVAE_THREADS, 4>(L, td.o0, td.i0, st, sb, g4, db, aa, wt);
+}
+
+template <typename T, int MODE>
+__global__ __launch_bounds__(CVAE_THREADS) void param_kernel(NetDev net, const TileDesc* __restrict__ tiles,
+                                                             AdamArgs aa) {
+  __shared__ __attribute__((aligned(16))) float wt[32 * WT_LD];
+  const TileDesc td = tiles[blockIdx.x];
+  param_body<T, MODE>(net.L[td.layer], td, aa, wt);
 }
 
 // CVAE_FP8: the per-layer weight scale of the e4m3 forward operand (cvae_device.h F8Scale), one

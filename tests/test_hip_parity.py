@@ -120,6 +120,30 @@ def test_split_path_equals_fused(cvae, golden):
     assert torch.equal(e1.m, e2.m) and torch.equal(e1.v, e2.v)
 
 
+def test_split_path_equals_fused_fast_kernels(cvae):
+    """The data-parallel route at the benchmark's shape (bf16: fastwgrad<PM_GRAD> → param_kernel
+    Adam) == the fused fastwgrad<PM_ADAM> step, bit for bit, and a grad_scale applied in the Adam
+    kernel equals pre-scaling the gradient."""
+    torch.manual_seed(0)
+    ref = OracleCVAE(100, 6, 8)
+    m1, e1 = _model(cvae, 100, 6, 8, sd=ref.state_dict(), dtype="bf16", max_batch=256)
+    m2, e2 = _model(cvae, 100, 6, 8, sd=ref.state_dict(), dtype="bf16", max_batch=256)
+    m3, e3 = _model(cvae, 100, 6, 8, sd=ref.state_dict(), dtype="bf16", max_batch=256)
+    x = e1.as_input(torch.randn(256, 100, 6, generator=torch.Generator().manual_seed(5)))
+    eps = torch.randn(256, 8, generator=torch.Generator().manual_seed(6)).cuda()
+    for _ in range(3):
+        e1.train_step(x, eps=eps)
+        e2.forward_backward(x, eps=eps)
+        e2.adam_step(1.0)
+        e3.forward_backward(x, eps=eps)
+        e3.grads.mul_(4.0)
+        e3.adam_step(0.25)
+    torch.cuda.synchronize()
+    assert torch.equal(e1.params, e2.params)
+    assert torch.equal(e1.m, e2.m) and torch.equal(e1.v, e2.v)
+    assert torch.equal(e2.params, e3.params)  # ×4 then ×0.25: exact in fp32
+
+
 def test_traj20_reference_train_loop(cvae, golden):
     """20 steps of Training_VAE.py's loop on sce1 (B=32, ragged 6-row batches) replayed on device."""
     d = golden("traj20_sce1.npz")
