@@ -305,6 +305,24 @@ def test_generate_absolute(cvae):
                                rtol=1e-6, atol=1e-4)
 
 
+def test_load_model_and_generate_trajectory_matches_reference(cvae, golden, tmp_path):
+    """Tools.py:18-65 drop-in: the reference function's own outputs on the shipped sce1 checkpoint
+    (generate_sce1.npz, made by tests/golden/make_generate_goldens.py) from the same seeds —
+    same z draw from the global CPU generator, same absolute trajectory (fp32 path)."""
+    from cvae_amd import generate_trajectories, load_model_and_generate_trajectory
+    w = golden("sce_fixed.npz")
+    g = golden("generate_sce1.npz")
+    path = tmp_path / "vae_offset_sce1_cond_ld8_epoch3000.pth"
+    torch.save({k[2:]: torch.from_numpy(w[k]) for k in w.files if k.startswith("w/")}, path)
+    for s, (sx, sy), want in zip(g["seeds"], g["starts"], g["traj"]):
+        torch.manual_seed(int(s))
+        got = load_model_and_generate_trajectory(str(path), float(sx), float(sy), seq_len=10, dim=3, latent_dim=8)
+        assert got.shape == (10, 3)
+        np.testing.assert_allclose(got, want, rtol=1e-5, atol=2e-4)
+    allg = generate_trajectories(str(path), g["starts"], seq_len=10, dim=3, latent_dim=8, z=torch.from_numpy(g["z"]))
+    np.testing.assert_allclose(allg, g["traj"], rtol=1e-5, atol=2e-4)
+
+
 @pytest.mark.parametrize("B", [64, 1024])
 def test_bf16_path_matches_bf16_emulation(cvae, B):
     """The bf16 kernels against an exact CPU emulation of their rounding points
