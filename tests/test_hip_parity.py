@@ -652,3 +652,45 @@ def test_fp8_training_full_batch_cfg5(cvae):
     assert torch.isfinite(eng.params).all()
     assert float(last[0]) < float(first[0])
 
+
+
+def _port(socket):
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_rccl_allreduce_split_step_equals_fused(cvae):
+    """The DP step's exchange on the real backend: fwd/bwd → RCCL all_reduce (the "nccl" backend,
+    a world-1 group on this one-GPU box) → Adam, plus the epoch loss all_reduce, equals the fused
+    step bit for bit (cvae_amd/dist.py DataParallelStep; Training_VAE.py:351-363)."""
+    import os
+    import torch.distributed as tdist
+    from cvae_amd import dist as dp
+    import socket
+    assert not tdist.is_initialized()
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    tdist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_port(socket)}", rank=0,
+                             world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        torch.manual_seed(0)
+        ref = OracleCVAE(100, 6, 8)
+        m1, e1 = _model(cvae, 100, 6, 8, sd=ref.state_dict(), dtype="bf16", max_batch=256)
+        m2, e2 = _model(cvae, 100, 6, 8, sd=ref.state_dict(), dtype="bf16", max_batch=256)
+        step = dp.DataParallelStep(e2)
+        step.broadcast_params()
+        x = e1.as_input(torch.randn(256, 100, 6, generator=torch.Generator().manual_seed(7)))
+        eps = torch.randn(256, 8, generator=torch.Generator().manual_seed(8)).cuda()
+        for _ in range(3):
+            e1.train_step(x, eps=eps)
+            e2.forward_backward(x, eps=eps)
+            tdist.all_reduce(e2.grads, op=tdist.ReduceOp.SUM)
+            e2.adam_step(1.0)
+        acc1 = e1.loss_accum.clone()
+        acc2 = step.epoch_loss_sums()
+        torch.cuda.synchronize()
+        assert torch.equal(e1.params, e2.params)
+        assert torch.equal(e1.m, e2.m) and torch.equal(e1.v, e2.v)
+        assert torch.equal(acc1, acc2) and float(e2.loss_accum.abs().sum()) == 0.0
+    finally:
+        tdist.destroy_process_group()
