@@ -2,13 +2,20 @@
 
 One "step" = Training_VAE.py:345-363 on one batch: relative transform → forward →
 conditional_vae_loss → backward → Adam, here the fused HIP path
-(rowchain kernel + wgrad⊕Adam kernel; with N>1: rowchain → wgrad → RCCL
-all-reduce of the flat gradient → Adam kernel).
+(rowchain kernel + wgrad⊕Adam kernel; with N>1, or --dp at N=1: rowchain → wgrad →
+RCCL all-reduce of the flat gradient → Adam kernel).
 
-Workload (BASELINE configs[1]/[2]): synthetic x ~ N(0,1) of shape (1024,100,6) per GPU,
-bf16 operands (fp32 master weights/Adam/loss), latent 8, hidden 128, weights
-(0.1,0.1,1,1), lr 1e-3, eps from the in-kernel Philox generator.  Data resident in
-HBM before timing.  N>1: B_local=1024 per rank (weak scaling), global B = 1024·N.
+Workloads:
+  cfg2 (default; BASELINE configs[1]/[2]): synthetic x ~ N(0,1) of shape (1024,100,6) per GPU,
+       bf16 operands (fp32 master weights/Adam/loss), latent 8, hidden 128, weights
+       (0.1,0.1,1,1), lr 1e-3, eps from the in-kernel Philox generator.  Data resident in
+       HBM before timing.  N>1: B_local=1024 per rank (weak scaling), global B = 1024·N.
+  cfg1 (BASELINE configs[0]): the reference's own data, StaticBlindTown05 = sce1 (38×10×3,
+       from the committed fixture tests/golden/sce_fixed.npz), B=32 (--batch 38 = the
+       reference's default), fp32, the reference loop: one host permutation per epoch
+       (DataLoader(shuffle=True)), batches 32|6, host eps — what `python Training_VAE.py`
+       runs, with the epoch's rows gathered on the device.
+  wide (BASELINE configs[4] shape): S=200, Z=512, 8+8 layers, bf16 (or --dtype fp8).
 
 Prints ONE JSON line (rank 0).  `roofline` is the dominant kernel's algorithmic
 FLOP per launch ÷ its average HIP-event duration over the timed region;
@@ -95,25 +102,47 @@ def measured_traffic(path, kernel, batch, dtype):
     return None if k is None else k["traffic_bytes"]
 
 
-def cpu_baseline(B, S, D, Z, H, seconds, n_enc=4, n_dec=4):
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(B, S, D, Z, H, seconds, n_enc=4, n_dec=4, data=None):
+    """The oracle step (Training_VAE.py:345-363 restated in torch-CPU) on the host cores: synthetic
+    N(0,1) rows, or (data) the real dataset with the reference loop's per-epoch permutation."""
     from oracle.cvae_oracle import OracleCVAE, oracle_step
     threads = torch.get_num_threads()
     torch.manual_seed(0)
     model = OracleCVAE(S, D, Z, H, n_enc, n_dec)
     opt = torch.optim.Adam(model.parameters(), lr=1e-3)
-    x = torch.randn(B, S, D, generator=torch.Generator().manual_seed(1234))
-    times = []
-    oracle_step(model, opt, x)  # warm-up
+    if data is None:
+        x = torch.randn(B, S, D, generator=torch.Generator().manual_seed(1234))
+        batches = lambda: [x]  # noqa: E731
+    else:
+        n = data.shape[0]
+        batches = lambda: [data[p] for p in torch.randperm(n).split(B)]  # noqa: E731
+    oracle_step(model, opt, batches()[0])  # warm-up
+    rows, t_tot, steps = 0, 0.0, 0
     t_end = time.perf_counter() + seconds
-    while time.perf_counter() < t_end or len(times) < 3:
-        t0 = time.perf_counter()
-        oracle_step(model, opt, x)
-        times.append(time.perf_counter() - t0)
-    times.sort()
-    med = times[len(times) // 2]
-    return {"value": round(B / med, 1), "unit": "trajectories/s", "cores": threads, "kind": "port",
-            "sample": f"{len(times)} steps of the oracle step (Training_VAE.py:345-363 body, torch-CPU fp32, "
-                      f"B={B} S={S} D={D} Z={Z} H={H}, {n_enc}+{n_dec} layers), median {med * 1e3:.2f} ms/step"}
+    while time.perf_counter() < t_end or steps < 3:
+        for xb in batches():
+            t0 = time.perf_counter()
+            oracle_step(model, opt, xb)
+            t_tot += time.perf_counter() - t0
+            rows += xb.shape[0]
+            steps += 1
+    what = "synthetic N(0,1)" if data is None else f"sce1 data ({data.shape[0]} rows, shuffled batches)"
+    return {"value": round(rows / t_tot, 1), "unit": "trajectories/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(),
+            "sample": f"{steps} steps of the oracle step (Training_VAE.py:345-363 body, torch-CPU fp32, "
+                      f"B={B} S={S} D={D} Z={Z} H={H}, {n_enc}+{n_dec} layers, {what}), "
+                      f"{t_tot / steps * 1e3:.3f} ms/step mean"}
 
 
 def main():
@@ -121,17 +150,18 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=1024, help="per-GPU batch")
-    ap.add_argument("--seq-len", type=int, default=100)
-    ap.add_argument("--dim", type=int, default=6)
-    ap.add_argument("--latent", type=int, default=8)
-    ap.add_argument("--hidden", type=int, default=128)
-    ap.add_argument("--n-enc", type=int, default=4)
-    ap.add_argument("--n-dec", type=int, default=4)
-    ap.add_argument("--workload", default="cfg2", choices=["cfg2", "wide"],
-                    help="cfg2: the headline (S=100, Z=8, 4+4 layers); wide: BASELINE cfg5's shape "
-                         "(S=200, Z=512, 8+8 layers; bf16 operands, the fp8 variant is not built)")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp8"])
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (cfg2/wide: 1024, cfg1: 32)")
+    ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg1", "wide"],
+                    help="cfg2: the headline (S=100, Z=8, 4+4 layers, synthetic); cfg1: the reference's sce1 "
+                         "data at B=32, fp32; wide: BASELINE cfg5's shape (S=200, Z=512, 8+8 layers)")
+    ap.add_argument("--dtype", default=None, choices=["bf16", "fp32", "fp8"],
+                    help="operand dtype (default: bf16; cfg1: fp32)")
+    ap.add_argument("--dp", action="store_true",
+                    help="data-parallel split step even at N=1: fwd/bwd → RCCL all-reduce → Adam")
+    ap.add_argument("--buckets", type=int, default=1, choices=[1, 2],
+                    help="split step: 2 = decoder-gradient all-reduce overlapped with the rest of dW")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture one step into a hipGraph and replay it (device step counters)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-b2b", action="store_true",
@@ -143,36 +173,79 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 or args.dp:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1:
+            os.environ.setdefault("MASTER_PORT", "29533")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
     from cvae_amd import ConditionalTrajectoryVAE
-    from cvae_amd.dist import DataParallelStep
+    from cvae_amd.dist import DataParallelStep, GraphedStep
 
-    if args.workload == "wide":
-        args.seq_len, args.latent, args.n_enc, args.n_dec = 200, 512, 8, 8
-    B, S, D, Z, H = args.batch, args.seq_len, args.dim, args.latent, args.hidden
-    NE, ND = args.n_enc, args.n_dec
+    wl = args.workload
+    S, D, Z, H, NE, ND = 100, 6, 8, 128, 4, 4
+    if wl == "wide":
+        S, Z, NE, ND = 200, 512, 8, 8
+    if wl == "cfg1":
+        S, D = 10, 3
+    dtype = args.dtype or ("fp32" if wl == "cfg1" else "bf16")
+    B = args.batch or (32 if wl == "cfg1" else 1024)
     torch.manual_seed(0)
     model = ConditionalTrajectoryVAE(S, D, Z, H, NE, ND)
-    eng = model.attach(dtype=args.dtype, max_batch=B, device=dev, seed=4321 + rank)
-    x = torch.randn(B, S, D, generator=torch.Generator().manual_seed(1234 + rank))
-    x = eng.as_input(x)  # resident in HBM, operand dtype
-    dp = DataParallelStep(eng)  # N=1: fused train_step; N>1: fwd/bwd → RCCL all-reduce → Adam
+    eng = model.attach(dtype=dtype, max_batch=B, device=dev, seed=4321)
+    dp = DataParallelStep(eng, force_split=args.dp, buckets=args.buckets)
     dp.broadcast_params()
 
-    def run(k):
-        """k training steps: on one GPU one cvae_train_steps call (no host work per step); under
-        data parallelism fwd/bwd → RCCL all-reduce → Adam per step."""
-        if world == 1:
-            eng.train_steps(x, k, batch=B)
-        else:
+    if wl == "cfg1":
+        import numpy as np
+        sce1 = np.load(os.path.join(ROOT, "tests", "golden", "sce_fixed.npz"))["sce1_x"]
+        data_cpu = torch.from_numpy(np.ascontiguousarray(sce1, dtype=np.float32))
+        n_rows = data_cpu.shape[0]
+        eng.keep_f32 = True
+        x = eng.as_input(data_cpu, keep_f32=True)
+        idx_dev = torch.empty(n_rows, device=dev, dtype=torch.int64)
+        sizes = [min(B, n_rows - s) for s in range(0, n_rows, B)]
+        gen = torch.Generator().manual_seed(0)
+        state = {"k": len(sizes)}
+
+        def run(k):
+            """k batches of the reference loop: a fresh permutation each epoch (host, DataLoader
+            shuffle), uploaded once per epoch; host eps per batch (randn_like on the CPU, :205)."""
             for _ in range(k):
-                dp.step(x, batch=B, global_batch=B * world)
+                if state["k"] == len(sizes):
+                    idx_dev.copy_(torch.randperm(n_rows, generator=gen), non_blocking=True)
+                    state["k"] = 0
+                j = state["k"]
+                lo = sum(sizes[:j])
+                eps = torch.randn(sizes[j], Z, generator=gen)
+                dp.step(x, idx=idx_dev[lo:lo + sizes[j]], eps=eps, batch=sizes[j],
+                        global_batch=sizes[j] * world)
+                state["k"] += 1
+        rows_per_step = n_rows / len(sizes)
+    else:
+        x = torch.randn(B, S, D, generator=torch.Generator().manual_seed(1234 + rank))
+        x = eng.as_input(x)  # resident in HBM, operand dtype
+        rows_per_step = B
+        graphed = None
+        if args.graph:
+            graphed = GraphedStep(eng, lambda: dp.step(x, batch=B, global_batch=B * world), n=1, warmup=2)
+
+        def run(k):
+            """k training steps: on one GPU one cvae_train_steps call (no host work per step); split
+            (data-parallel) path: fwd/bwd → RCCL all-reduce → Adam per step; --graph: replays."""
+            if graphed is not None:
+                for _ in range(k):
+                    graphed.replay()
+            elif not dp.split:
+                eng.train_steps(x, k, batch=B)
+            else:
+                for _ in range(k):
+                    dp.step(x, batch=B, global_batch=B * world)
 
     run(args.warmup)
     torch.cuda.synchronize(dev)
@@ -186,15 +259,22 @@ def main():
         dist.barrier()
     t = time.perf_counter() - t0
     # kernel durations for the roofline: the same K steps again with HIP events recorded on the
-    # launch stream between kernels (events inside the timed pass would add ~10 us per step)
+    # launch stream between kernels (events inside the timed pass would add ~10 us per step;
+    # graph replays record none, so this pass runs eagerly)
     eng.set_timing(True)
-    run(args.steps)
+    if args.graph and wl != "cfg1":
+        for _ in range(args.steps):
+            dp.step(x, batch=B, global_batch=B * world)
+    else:
+        run(args.steps)
     torch.cuda.synchronize(dev)
     kt = eng.kernel_times()
     eng.set_timing(False)
     # each kernel alone, launched back-to-back (cvae_bench_kernels): the step's kernels without
     # their neighbours' cache/instruction-cache effects
-    b2b = None if args.no_b2b else eng.bench_kernels(x, max(args.steps, 20), batch=B)
+    b2b = None
+    if not args.no_b2b and wl != "cfg1":
+        b2b = eng.bench_kernels(x, max(args.steps, 20), batch=B)
     if world > 1:
         tt = torch.tensor([t], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -204,41 +284,54 @@ def main():
 
     if rank == 0:
         fl = flops_per_traj(S, D, Z, H, n_enc=NE, n_dec=ND)
-        tsize = 4 if args.dtype == "fp32" else 2  # fp8: bf16 activations
+        tsize = 4 if dtype == "fp32" else 2  # fp8: bf16 activations
         bt = bytes_per_traj(S, D, Z, H, tsize, n_enc=NE, n_dec=ND)
         n_par = eng.n_params
-        flop = {"rowchain": fl["rowchain"] * B, "wgrad": fl["wgrad"] * B, "wgrad_adam": fl["wgrad"] * B}
-        nbytes = {"rowchain": bt["rowchain"] * B, "wgrad": bt["wgrad"] * B + 4 * n_par,
-                  "wgrad_adam": bt["wgrad"] * B + ADAM_BYTES_PER_PARAM * n_par}
-        # the fused launch (one kernel per step: row chain + dW ⊕ Adam tiles)
+        rows_launch = rows_per_step if wl == "cfg1" else B
+        flop = {k: fl["rowchain" if k.startswith("rowchain") else "wgrad"] * rows_launch
+                for k in ("rowchain", "wgrad", "wgrad_adam", "wgrad_dec", "wgrad_rest")}
+        nbytes = {"rowchain": bt["rowchain"] * rows_launch, "wgrad": bt["wgrad"] * rows_launch + 4 * n_par,
+                  "wgrad_adam": bt["wgrad"] * rows_launch + ADAM_BYTES_PER_PARAM * n_par,
+                  "wgrad_dec": bt["wgrad"] * rows_launch, "wgrad_rest": bt["wgrad"] * rows_launch}
         flop["fused_step"] = flop["rowchain"] + flop["wgrad_adam"]
         nbytes["fused_step"] = nbytes["rowchain"] + nbytes["wgrad_adam"]
-        dom = max((k for k in kt if k in flop), key=lambda k: kt[k][0])
-        wide = (S, D, Z, H, NE, ND) != (100, 6, 8, 128, 4, 4)
-        traffic = None if wide else measured_traffic(args.traffic_file, dom, B, args.dtype)
-        roof = roofline(dom, kt[dom][0], flop[dom], nbytes[dom], args.dtype, traffic)
+        flop["adam"], nbytes["adam"] = 0, ADAM_BYTES_PER_PARAM * n_par
+        dom = max((k for k in kt if k in flop and flop[k] > 0), key=lambda k: kt[k][0])
+        std = (S, D, Z, H, NE, ND) == (100, 6, 8, 128, 4, 4)
+        traffic = measured_traffic(args.traffic_file, dom, B, dtype) if std else None
+        roof = roofline(dom, kt[dom][0], flop[dom], nbytes[dom], dtype, traffic)
         roof["kernels_ms"] = {k: round(v[0], 5) for k, v in kt.items()}
         if b2b:
             roof["kernels_back_to_back_ms"] = {k: round(v, 5) for k, v in b2b.items()}
-        value = world * B * args.steps / t
-        metric = ("trajectories/sec per ELBO step, batch=1024 seq_len=100; 1/2/4/8 MI355X" if not wide else
-                  f"trajectories/sec per ELBO step, batch={B} seq_len={S} (BASELINE cfg5 shape, bf16 not fp8)")
+        value = world * rows_per_step * args.steps / t
+        if wl == "cfg2":
+            metric = "trajectories/sec per ELBO step, batch=1024 seq_len=100; 1/2/4/8 MI355X"
+            data = "synthetic x~N(0,1) (seeded), random-init weights (torch.manual_seed(0))"
+        elif wl == "cfg1":
+            metric = (f"trajectories/sec per ELBO step, sce1 StaticBlindTown05 data, batch={B} seq_len=10 "
+                      f"(BASELINE configs[0])")
+            data = "the reference's trajectory_sce1_cond.npy rows (38x10x3, committed fixture), host eps"
+        else:
+            metric = f"trajectories/sec per ELBO step, batch={B} seq_len={S} (BASELINE cfg5 shape)"
+            data = "synthetic x~N(0,1) (seeded), random-init weights (torch.manual_seed(0))"
+        path = "graph" if args.graph else ("split" if dp.split else "fused")
         res = {"metric": metric,
                "value": round(value, 1), "unit": "trajectories/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(t / args.steps * 1e3, 5), "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
-               "data": "synthetic x~N(0,1) (seeded), random-init weights (torch.manual_seed(0))",
-               "config": {"workload": f"Training_VAE step, B_local={B} S={S} D={D} Z={Z} H={H}, "
-                                      f"{NE}+{ND} layers, {args.dtype} operands / fp32 master+Adam",
+               "scaling": "weak", "vs_baseline": None, "dtype": dtype, "data": data,
+               "config": {"workload": f"{wl}: Training_VAE step, B_local={B} S={S} D={D} Z={Z} H={H}, "
+                                      f"{NE}+{ND} layers, {dtype} operands / fp32 master+Adam, {path} step"
+                                      + (f", {args.buckets} buckets" if dp.split else ""),
                           "global_batch": B * world, "seq_len": S, "state_dim": D, "latent_dim": Z,
                           "hidden_dim": H, "parallelism": f"dp{world}"},
                "roofline": roof,
                "flop_per_traj": fl["total"]}
         if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(B, S, D, Z, H, args.cpu_seconds, NE, ND)
+            res["cpu_baseline"] = cpu_baseline(B, S, D, Z, H, args.cpu_seconds, NE, ND,
+                                               data=data_cpu if wl == "cfg1" else None)
             res["speedup_vs_cpu"] = round(value / res["cpu_baseline"]["value"], 1)
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

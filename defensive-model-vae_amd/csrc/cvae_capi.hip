@@ -53,6 +53,10 @@ struct cvae_handle {
   int64_t nparams = 0;
   std::vector<TileDesc> tiles;
   TileDesc* d_tiles = nullptr;
+  // the two dW buckets (CVAE_PART_DW_DEC / CVAE_PART_DW_REST): tiles of the decoder layers and of the rest
+  std::vector<TileDesc> tiles_part[2];
+  TileDesc* d_tiles_part[2] = {nullptr, nullptr};
+  int64_t bucket_split = 0;   // flat index of decoder.0.weight
   char* arena = nullptr;    // weight copies + activations
   unsigned* d_sync = nullptr;  // fused launch hand-off words (fchain::FusedArgs::sync), zero between launches
   bool fused = false;          // training steps run as one fused_step_kernel launch
@@ -178,13 +182,22 @@ int build_plan(cvae_handle* h) {
         for (int i = 0; i < L.Kp; i += 32) seq.push_back({l, o, i, 0});
     }
   }
-  const int nt = (int)seq.size(), q = nt / 8, r = nt % 8;
-  h->tiles.assign(nt, TileDesc{});
-  for (int b = 0; b < nt; ++b) {
-    const int x = b % 8, j = b / 8;
-    const int start = x * q + (x < r ? x : r);  // chunk x = seq[start, start + q + (x < r))
-    h->tiles[b] = seq[start + j];
-  }
+  auto xcd_order = [](const std::vector<TileDesc>& list) {
+    const int nt = (int)list.size(), q = nt / 8, r = nt % 8;
+    std::vector<TileDesc> out(nt);
+    for (int b = 0; b < nt; ++b) {
+      const int x = b % 8, j = b / 8;
+      const int start = x * q + (x < r ? x : r);  // chunk x = list[start, start + q + (x < r))
+      out[b] = list[start + j];
+    }
+    return out;
+  };
+  h->tiles = xcd_order(seq);
+  std::vector<TileDesc> dec, rest;
+  for (const TileDesc& t : seq) (t.layer >= lD(n, 0) ? dec : rest).push_back(t);
+  h->tiles_part[0] = xcd_order(dec);
+  h->tiles_part[1] = xcd_order(rest);
+  h->bucket_split = n.L[lD(n, 0)].pw[0];
   return CVAE_OK;
 }
 
@@ -322,6 +335,8 @@ int alloc_arena(cvae_handle* h) {
   const int64_t part_off = take((int64_t)h->max_row_tiles * 8 * 4);
   const int64_t sync_off = take(256);
   const int64_t tile_off = take((int64_t)h->tiles.size() * sizeof(TileDesc));
+  const int64_t tp_off0 = take((int64_t)h->tiles_part[0].size() * sizeof(TileDesc));
+  const int64_t tp_off1 = take((int64_t)h->tiles_part[1].size() * sizeof(TileDesc));
   int64_t step_off[cvae_handle::ST_N];
   for (int m = 0; m < cvae_handle::ST_N; ++m) step_off[m] = take(64 * (int64_t)sizeof(StepDesc));
   HIPCK(hipMalloc(&h->arena, total));
@@ -341,6 +356,12 @@ int alloc_arena(cvae_handle* h) {
   h->d_sync = (unsigned*)(h->arena + sync_off);
   h->d_tiles = (TileDesc*)(h->arena + tile_off);
   HIPCK(hipMemcpy(h->d_tiles, h->tiles.data(), h->tiles.size() * sizeof(TileDesc), hipMemcpyHostToDevice));
+  const int64_t tp_off[2] = {tp_off0, tp_off1};
+  for (int k = 0; k < 2; ++k) {
+    h->d_tiles_part[k] = (TileDesc*)(h->arena + tp_off[k]);
+    HIPCK(hipMemcpy(h->d_tiles_part[k], h->tiles_part[k].data(), h->tiles_part[k].size() * sizeof(TileDesc),
+                    hipMemcpyHostToDevice));
+  }
   for (int m = 0; m < cvae_handle::ST_N; ++m) {
     const std::vector<StepSpec> spec = build_steps(n, m);
     std::vector<StepDesc> st;
@@ -457,20 +478,25 @@ int check_batch(cvae_handle* h, int batch) {
   return CVAE_OK;
 }
 
-AdamArgs make_adam(float* params, float* grads, float* m, float* v, int step, float lr, float b1, float b2,
-                   float eps, float grad_scale) {
+AdamArgs make_adam(float* params, float* grads, float* m, float* v, int64_t step, const cvae_adam_config& c,
+                   float grad_scale, const uint64_t* ctr) {
   AdamArgs a{};
   a.params = params; a.grads = grads; a.m = m; a.v = v;
   a.grad_scale = grad_scale;
-  // torch computes these python scalars in double, then the CPU kernels see them as float
-  const double bc1 = 1.0 - std::pow((double)b1, (double)step);
-  const double bc2 = 1.0 - std::pow((double)b2, (double)step);
-  a.lr_neg_step = (float)(-((double)lr / bc1));
-  a.bc2_sqrt = (float)std::sqrt(bc2);
-  a.beta1_w = (float)(1.0 - (double)b1);
-  a.beta2 = b2;
-  a.one_m_beta2 = (float)(1.0 - (double)b2);
-  a.eps = eps;
+  // torch computes these in Python doubles, then the tensor ops take them as float
+  // (torch/optim/adam.py _single_tensor_adam): step_size = lr / (1 - beta1**step), bias_correction2**0.5
+  if (!ctr) {
+    const double bc1 = 1.0 - std::pow(c.beta1, (double)step);
+    const double bc2 = 1.0 - std::pow(c.beta2, (double)step);
+    a.lr_neg_step = (float)(-(c.lr / bc1));
+    a.bc2_sqrt = (float)std::pow(bc2, 0.5);
+  }
+  a.beta1_w = (float)(1.0 - c.beta1);   // exp_avg.lerp_(grad, 1 - beta1)
+  a.beta2 = (float)c.beta2;             // exp_avg_sq.mul_(beta2)
+  a.one_m_beta2 = (float)(1.0 - c.beta2);  // .addcmul_(grad, grad, value=1 - beta2)
+  a.eps = (float)c.eps;
+  a.ctr = ctr;
+  a.lr = c.lr; a.beta1d = c.beta1; a.beta2d = c.beta2;
   return a;
 }
 
@@ -546,43 +572,79 @@ int plan_fast(cvae_handle* h) {
   return CVAE_OK;
 }
 
-template <typename T>
-int train_fwd_bwd_impl(cvae_handle* h, const void* x, const int64_t* idx, int batch, const float* eps,
-                       uint64_t seed, uint64_t offset, const cvae_loss_weights* w, hipStream_t s,
-                       RowArgs& ra) {
-  ra = RowArgs{};
-  ra.x = x; ra.idx = idx; ra.batch = batch; ra.eps = eps; ra.seed = seed; ra.offset = offset;
-  ra.w_recon = w ? w->recon : 0.1f; ra.w_kld = w ? w->kld : 0.1f;
-  ra.w_start = w ? w->start : 1.0f; ra.w_time = w ? w->time : 1.0f;
+// What every training / inference call hands the row chain.
+struct CallX {
+  const void* x;
+  const int64_t* idx;
+  int batch;
+  int xflags;
+  const float* eps;
+  uint64_t seed, offset;
+  int64_t eps_row0;
+  const cvae_loss_weights* w;
+  uint64_t* ctr;
+};
+
+RowArgs row_args(cvae_handle* h, const CallX& c) {
+  RowArgs ra{};
+  ra.x = c.x; ra.idx = c.idx; ra.batch = c.batch; ra.eps = c.eps; ra.seed = c.seed; ra.offset = c.offset;
+  ra.eps_row0 = c.eps_row0;
+  ra.x_f32 = (c.xflags & CVAE_X_F32) && is16(h) ? 1 : 0;
+  ra.ctr = c.ctr;
+  ra.w_recon = c.w ? c.w->recon : 0.1f; ra.w_kld = c.w ? c.w->kld : 0.1f;
+  ra.w_start = c.w ? c.w->start : 1.0f; ra.w_time = c.w ? c.w->time : 1.0f;
   ra.partials = h->d_partials;
+  return ra;
+}
+
+bool fast_ok(const cvae_handle* h, const RowArgs& ra) {
+  return h->fast_nki > 0 && (((uintptr_t)ra.x) & 15) == 0 && !ra.x_f32 && !ra.ext && !ra.x_relative;
+}
+
+// the training row chain (forward + loss + every dX): the specialised bf16 chain where it applies
+template <typename T>
+int launch_train_chain(cvae_handle* h, RowArgs ra, hipStream_t s) {
   int rc = tmark(h, s, "rowchain");
   if (rc) return rc;
-  if (std::is_same<T, __bf16>::value && h->fast_nki > 0 && (((uintptr_t)x) & 15) == 0) {
+  if (std::is_same<T, __bf16>::value && fast_ok(h, ra)) {
     ra.steps = h->d_steps[cvae_handle::ST_TRAIN];
     ra.nsteps = h->n_steps[cvae_handle::ST_TRAIN];
     ra.stamps = h->d_stamps;
-    const int grid = rup_i(batch, 32) / fchain::R;
-    return klaunch(h, fchain::fastchain_kernel<19>, dim3(grid), dim3(fchain::NT), h->fast_lds, s, h->arena, x, idx,
-                   h->net.Bp, batch, h->net.S, h->net.D, h->net.I, ra);
+    const int grid = rup_i(ra.batch, 32) / fchain::R;
+    return klaunch(h, fchain::fastchain_kernel<19>, dim3(grid), dim3(fchain::NT), h->fast_lds, s, h->arena, ra.x,
+                   ra.idx, h->net.Bp, ra.batch, h->net.S, h->net.D, h->net.I, ra);
   }
   return launch_rowchain<T, RC_TRAIN>(h, ra, s);
 }
 
-LossArgs make_loss(cvae_handle* h, const RowArgs& ra, float* loss_out, float* loss_accum) {
+LossArgs make_loss(cvae_handle* h, const RowArgs& ra, float* loss_out, double* loss_accum) {
   LossArgs la{};
   la.partials = h->d_partials;
   la.ntiles = rup_i(ra.batch, 32) / h->R;
   la.batch = ra.batch;
   la.w_recon = ra.w_recon; la.w_kld = ra.w_kld; la.w_start = ra.w_start; la.w_time = ra.w_time;
   la.loss_out = loss_out; la.loss_accum = loss_accum;
+  la.ctr = ra.ctr;
   return la;
 }
 
 int bk_of(cvae_handle*, int batch) { return rup_i(batch, 32); }
 
-// the dW (⊕ Adam) launch of a training step: the fast kernel for the fast configuration
+// the dW (⊕ Adam) launch of a training step: the fast kernel for the fast configuration, the
+// generic kernel over a bucket's tile list for a split (two-bucket) step
 template <int MODE>
-int launch_wgrad(cvae_handle* h, int batch, const AdamArgs& aa, const LossArgs& la, hipStream_t s) {
+int launch_wgrad(cvae_handle* h, int batch, const AdamArgs& aa, const LossArgs& la, hipStream_t s,
+                 int parts = CVAE_PART_DW_DEC | CVAE_PART_DW_REST) {
+  const int dw = parts & (CVAE_PART_DW_DEC | CVAE_PART_DW_REST);
+  if (dw != (CVAE_PART_DW_DEC | CVAE_PART_DW_REST)) {
+    const int k = dw == CVAE_PART_DW_DEC ? 0 : 1;
+    const int nt = (int)h->tiles_part[k].size();
+    if (is16(h))
+      return klaunch(h, wgrad_kernel<__bf16, MODE>, dim3(nt), dim3(WG_THREADS), 0, s, h->net,
+                     (const TileDesc*)h->d_tiles_part[k], bk_of(h, batch), aa, la);
+    return klaunch(h, wgrad_kernel<float, MODE>, dim3(nt), dim3(WG_THREADS), 0, s, h->net,
+                   (const TileDesc*)h->d_tiles_part[k], bk_of(h, batch), aa, la);
+  }
   const int nt = (int)h->tiles.size();
   if (h->fast_nki == 19)
     return klaunch(h, fchain::fastwgrad_kernel<19, MODE>, dim3(fchain::Tiles<19>::total() + 1), dim3(WG_THREADS),
@@ -595,31 +657,74 @@ int launch_wgrad(cvae_handle* h, int batch, const AdamArgs& aa, const LossArgs& 
                  (const TileDesc*)h->d_tiles, bk_of(h, batch), aa, la);
 }
 
+// device counters, fused launch: its chain blocks do not bump the step (its dW tiles read it in the
+// same launch), so the step begins with this one-lane kernel; the loss tile advances the offset
+// after every chain block has published (read) it
+__global__ void counter_bump_kernel(uint64_t* c) { c[0] = c[0] + 1; }
+
 // one training step as a single fused_step_kernel launch (fast configuration, 16-B aligned x)
-int launch_fused(cvae_handle* h, const void* x, const int64_t* idx, int batch, const float* eps, uint64_t seed,
-                 uint64_t offset, const cvae_loss_weights* w, const AdamArgs& aa, float* loss_out,
-                 float* loss_accum, hipStream_t s) {
-  RowArgs ra{};
-  ra.x = x; ra.idx = idx; ra.batch = batch; ra.eps = eps; ra.seed = seed; ra.offset = offset;
-  ra.w_recon = w ? w->recon : 0.1f; ra.w_kld = w ? w->kld : 0.1f;
-  ra.w_start = w ? w->start : 1.0f; ra.w_time = w ? w->time : 1.0f;
-  ra.partials = h->d_partials;
+int launch_fused(cvae_handle* h, RowArgs ra, const AdamArgs& aa, float* loss_out, double* loss_accum,
+                 hipStream_t s) {
   ra.stamps = h->d_stamps;
   fchain::FusedArgs f{};
   f.aa = aa;
   f.la = make_loss(h, ra, loss_out, loss_accum);
   f.sync = h->d_sync;
-  f.Bk = bk_of(h, batch);
-  f.nchain = rup_i(batch, 32) / fchain::R;
+  f.Bk = bk_of(h, ra.batch);
+  f.nchain = rup_i(ra.batch, 32) / fchain::R;
   const int nt = fchain::Tiles<19>::total();
+  // the group counters start every launch at zero (stream-ordered; the sticky time-out flag stays)
+  HIPCK(hipMemsetAsync(h->d_sync, 0, 4 * sizeof(unsigned), s));
+  if (ra.ctr) {
+    hipLaunchKernelGGL(counter_bump_kernel, dim3(1), dim3(1), 0, s, ra.ctr + 1);
+    HIPCK(hipGetLastError());
+  }
   int rc = tmark(h, s, "fused_step");
   if (rc) return rc;
   return klaunch(h, fchain::fused_step_kernel<19>, dim3(f.nchain + nt), dim3(fchain::NT), h->fast_lds, s,
                  fchain::FastNet{h->arena, h->net.Bp, h->net.S, h->net.D, h->net.I}, ra, f);
 }
 
-bool use_fused(const cvae_handle* h, const void* x) {
-  return h->fused && h->fast_nki == 19 && (((uintptr_t)x) & 15) == 0;
+bool use_fused(const cvae_handle* h, const RowArgs& ra) {
+  return h->fused && h->fast_nki == 19 && fast_ok(h, ra);
+}
+
+int check_adam(const cvae_adam_config* adam) {
+  if (!adam) return fail(CVAE_E_INVALID, "null adam config");
+  if (!(adam->beta1 >= 0.0 && adam->beta1 < 1.0 && adam->beta2 >= 0.0 && adam->beta2 < 1.0))
+    return fail(CVAE_E_INVALID, "betas must lie in [0, 1)");
+  return CVAE_OK;
+}
+
+int fwd_bwd_impl(cvae_handle* h, const CallX& c, float* grads, float* loss_out, double* loss_accum, int parts,
+                 hipStream_t s) {
+  tbegin(h);
+  const RowArgs ra = row_args(h, c);
+  int rc = CVAE_OK;
+  if (parts & CVAE_PART_CHAIN)
+    rc = is16(h) ? launch_train_chain<__bf16>(h, ra, s) : launch_train_chain<float>(h, ra, s);
+  if (rc) return rc;
+  AdamArgs aa{};
+  aa.grads = grads;
+  LossArgs la{};
+  if (parts & CVAE_PART_CHAIN) la = make_loss(h, ra, loss_out, loss_accum);  // the loss belongs to the chain's call
+  const int dw = parts & (CVAE_PART_DW_DEC | CVAE_PART_DW_REST);
+  if ((rc = tmark(h, s, dw == CVAE_PART_DW_DEC ? "wgrad_dec" : dw == CVAE_PART_DW_REST ? "wgrad_rest" : "wgrad")))
+    return rc;
+  return launch_wgrad<PM_GRAD>(h, c.batch, aa, la, s, parts);
+}
+
+int train_step_impl(cvae_handle* h, const CallX& c, float* params, float* m, float* v, int64_t step,
+                    const cvae_adam_config* adam, float* loss_out, double* loss_accum, hipStream_t s) {
+  tbegin(h);
+  AdamArgs aa = make_adam(params, nullptr, m, v, step, *adam, 1.f, c.ctr);
+  const RowArgs ra = row_args(h, c);
+  if (use_fused(h, ra)) return launch_fused(h, ra, aa, loss_out, loss_accum, s);
+  int rc = is16(h) ? launch_train_chain<__bf16>(h, ra, s) : launch_train_chain<float>(h, ra, s);
+  if (rc) return rc;
+  const LossArgs la = make_loss(h, ra, loss_out, loss_accum);
+  if ((rc = tmark(h, s, "wgrad_adam"))) return rc;
+  return launch_wgrad<PM_ADAM>(h, c.batch, aa, la, s);
 }
 
 }  // namespace
@@ -692,6 +797,12 @@ int cvae_workspace_bytes(const cvae_handle* h, int64_t* bytes) {
   return CVAE_OK;
 }
 
+int cvae_bucket_split(const cvae_handle* h, int64_t* split) {
+  if (!h || !split) return fail(CVAE_E_INVALID, "null argument");
+  *split = h->bucket_split;
+  return CVAE_OK;
+}
+
 int cvae_pack_weights(cvae_handle* h, const float* params, void* stream) {
   if (!h || !params) return fail(CVAE_E_INVALID, "null argument");
   hipStream_t s = (hipStream_t)stream;
@@ -708,16 +819,15 @@ int cvae_pack_weights(cvae_handle* h, const float* params, void* stream) {
   return CVAE_OK;
 }
 
-int cvae_forward(cvae_handle* h, const void* x, const int64_t* idx, int batch, const float* start, const float* eps,
-                 uint64_t seed, uint64_t offset, float* recon, float* mu, float* logvar, float* hc, void* stream) {
+int cvae_forward(cvae_handle* h, const void* x, const int64_t* idx, int batch, int xflags, const float* start,
+                 const float* eps, uint64_t seed, uint64_t offset, int64_t eps_row0, float* recon, float* mu,
+                 float* logvar, float* hc, float* eps_out, void* stream) {
   if (!h || !x) return fail(CVAE_E_INVALID, "null argument");
   int rc = check_batch(h, batch);
   if (rc) return rc;
-  RowArgs a{};
-  a.x = x; a.idx = idx; a.batch = batch; a.eps = eps; a.seed = seed; a.offset = offset;
+  RowArgs a = row_args(h, CallX{x, idx, batch, xflags, eps, seed, offset, eps_row0, nullptr, nullptr});
   a.start_in = start; a.x_relative = start ? 1 : 0;
-  a.recon_out = recon; a.mu_out = mu; a.lv_out = logvar; a.hc_out = hc;
-  a.partials = h->d_partials;
+  a.recon_out = recon; a.mu_out = mu; a.lv_out = logvar; a.hc_out = hc; a.eps_out = eps_out;
   hipStream_t s = (hipStream_t)stream;
   return is16(h) ? launch_rowchain<__bf16, RC_FWD>(h, a, s) : launch_rowchain<float, RC_FWD>(h, a, s);
 }
@@ -747,34 +857,49 @@ int cvae_decode(cvae_handle* h, const float* z, const float* start, const float*
                                    : launch_rowchain<float, RC_DECODE>(h, a, s);
 }
 
-int cvae_train_fwd_bwd(cvae_handle* h, const void* x, const int64_t* idx, int batch, const float* eps,
-                       uint64_t seed, uint64_t offset, const cvae_loss_weights* w, float* grads,
-                       float* loss_out, float* loss_accum, void* stream) {
+int cvae_train_fwd_bwd(cvae_handle* h, const void* x, const int64_t* idx, int batch, int xflags, const float* eps,
+                       uint64_t seed, uint64_t offset, int64_t eps_row0, const cvae_loss_weights* w, float* grads,
+                       float* loss_out, double* loss_accum, uint64_t* counters, int parts, void* stream) {
+  if (!h || !grads || ((parts & CVAE_PART_CHAIN) && !x)) return fail(CVAE_E_INVALID, "null argument");
+  if (parts != CVAE_PART_ALL && parts != (CVAE_PART_CHAIN | CVAE_PART_DW_DEC) && parts != CVAE_PART_DW_REST)
+    return fail(CVAE_E_INVALID, "parts must be CVAE_PART_ALL, CHAIN|DW_DEC, or DW_REST");
+  int rc = check_batch(h, batch);
+  if (rc) return rc;
+  return fwd_bwd_impl(h, CallX{x, idx, batch, xflags, eps, seed, offset, eps_row0, w, counters}, grads, loss_out,
+                      loss_accum, parts, (hipStream_t)stream);
+}
+
+int cvae_backward(cvae_handle* h, const void* x, const int64_t* idx, int batch, int xflags, const float* start,
+                  const float* eps, uint64_t seed, uint64_t offset, int64_t eps_row0, const float* d_recon,
+                  const float* d_mu, const float* d_logvar, const float* d_hc, float* grads, void* stream) {
   if (!h || !x || !grads) return fail(CVAE_E_INVALID, "null argument");
   int rc = check_batch(h, batch);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   tbegin(h);
-  RowArgs ra;
-  rc = is16(h) ? train_fwd_bwd_impl<__bf16>(h, x, idx, batch, eps, seed, offset, w, s, ra)
-                                 : train_fwd_bwd_impl<float>(h, x, idx, batch, eps, seed, offset, w, s, ra);
+  RowArgs ra = row_args(h, CallX{x, idx, batch, xflags, eps, seed, offset, eps_row0, nullptr, nullptr});
+  ra.start_in = start; ra.x_relative = start ? 1 : 0;
+  ra.ext = 1;
+  ra.d_recon = d_recon; ra.d_mu = d_mu; ra.d_lv = d_logvar; ra.d_hc = d_hc;
+  if ((rc = tmark(h, s, "rowchain_bwd"))) return rc;
+  rc = is16(h) ? launch_rowchain<__bf16, RC_TRAIN>(h, ra, s) : launch_rowchain<float, RC_TRAIN>(h, ra, s);
   if (rc) return rc;
   AdamArgs aa{};
   aa.grads = grads;
-  const LossArgs la = make_loss(h, ra, loss_out, loss_accum);
   if ((rc = tmark(h, s, "wgrad"))) return rc;
-  return launch_wgrad<PM_GRAD>(h, batch, aa, la, s);
+  return launch_wgrad<PM_GRAD>(h, batch, aa, LossArgs{}, s);
 }
 
-int cvae_adam(cvae_handle* h, float* params, const float* grads, float* m, float* v, int step, float lr,
-              float beta1, float beta2, float eps, float grad_scale, void* stream) {
+int cvae_adam(cvae_handle* h, float* params, const float* grads, float* m, float* v, int64_t step,
+              const cvae_adam_config* adam, float grad_scale, const uint64_t* counters, void* stream) {
   if (!h || !params || !grads || !m || !v) return fail(CVAE_E_INVALID, "null argument");
-  if (step < 1) return fail(CVAE_E_INVALID, "step must be >= 1");
-  hipStream_t s = (hipStream_t)stream;
-  AdamArgs aa = make_adam(params, (float*)grads, m, v, step, lr, beta1, beta2, eps, grad_scale);
-  const int nt = (int)h->tiles.size();
-  int rc = tmark(h, s, "adam");
+  if (!counters && step < 1) return fail(CVAE_E_INVALID, "step must be >= 1");
+  int rc = check_adam(adam);
   if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  AdamArgs aa = make_adam(params, (float*)grads, m, v, step, *adam, grad_scale, counters);
+  const int nt = (int)h->tiles.size();
+  if ((rc = tmark(h, s, "adam"))) return rc;
   if (is16(h))
     return klaunch(h, param_kernel<__bf16, PM_ADAM>, dim3(nt), dim3(CVAE_THREADS), 0, s, h->net,
                    (const TileDesc*)h->d_tiles, aa);
@@ -782,45 +907,38 @@ int cvae_adam(cvae_handle* h, float* params, const float* grads, float* m, float
                  (const TileDesc*)h->d_tiles, aa);
 }
 
-int cvae_train_step(cvae_handle* h, const void* x, const int64_t* idx, int batch, const float* eps, uint64_t seed,
-                    uint64_t offset, const cvae_loss_weights* w, float* params, float* m, float* v, int step,
-                    float lr, float beta1, float beta2, float adam_eps, float* loss_out, float* loss_accum,
-                    void* stream) {
+int cvae_train_step(cvae_handle* h, const void* x, const int64_t* idx, int batch, int xflags, const float* eps,
+                    uint64_t seed, uint64_t offset, int64_t eps_row0, const cvae_loss_weights* w, float* params,
+                    float* m, float* v, int64_t step, const cvae_adam_config* adam, float* loss_out,
+                    double* loss_accum, uint64_t* counters, void* stream) {
   if (!h || !x || !params || !m || !v) return fail(CVAE_E_INVALID, "null argument");
-  if (step < 1) return fail(CVAE_E_INVALID, "step must be >= 1");
+  if (!counters && step < 1) return fail(CVAE_E_INVALID, "step must be >= 1");
   int rc = check_batch(h, batch);
+  if (!rc) rc = check_adam(adam);
   if (rc) return rc;
-  hipStream_t s = (hipStream_t)stream;
-  tbegin(h);
-  AdamArgs aa = make_adam(params, nullptr, m, v, step, lr, beta1, beta2, adam_eps, 1.f);
-  if (use_fused(h, x)) return launch_fused(h, x, idx, batch, eps, seed, offset, w, aa, loss_out, loss_accum, s);
-  RowArgs ra;
-  rc = is16(h) ? train_fwd_bwd_impl<__bf16>(h, x, idx, batch, eps, seed, offset, w, s, ra)
-                                 : train_fwd_bwd_impl<float>(h, x, idx, batch, eps, seed, offset, w, s, ra);
-  if (rc) return rc;
-  const LossArgs la = make_loss(h, ra, loss_out, loss_accum);
-  if ((rc = tmark(h, s, "wgrad_adam"))) return rc;
-  return launch_wgrad<PM_ADAM>(h, batch, aa, la, s);
+  return train_step_impl(h, CallX{x, idx, batch, xflags, eps, seed, offset, eps_row0, w, counters}, params, m, v,
+                         step, adam, loss_out, loss_accum, (hipStream_t)stream);
 }
 
-int cvae_train_steps(cvae_handle* h, const void* x, const int64_t* idx, int batch, int n_steps, const float* eps,
-                     uint64_t seed, uint64_t offset, const cvae_loss_weights* w, float* params, float* m, float* v,
-                     int step0, float lr, float beta1, float beta2, float adam_eps, float* loss_out,
-                     float* loss_accum, void* stream) {
+int cvae_train_steps(cvae_handle* h, const void* x, const int64_t* idx, int batch, int n_steps, int xflags,
+                     const float* eps, uint64_t seed, uint64_t offset, int64_t eps_row0,
+                     const cvae_loss_weights* w, float* params, float* m, float* v, int64_t step0,
+                     const cvae_adam_config* adam, float* loss_out, double* loss_accum, uint64_t* counters,
+                     void* stream) {
   if (!h) return fail(CVAE_E_INVALID, "null handle");
   if (n_steps < 0) return fail(CVAE_E_INVALID, "n_steps must be >= 0");
   const int Z = h->cfg.latent_dim;
   for (int i = 0; i < n_steps; ++i) {
-    const int rc = cvae_train_step(h, x, idx ? idx + (size_t)i * batch : nullptr, batch,
-                                   eps ? eps + (size_t)i * batch * Z : nullptr, seed, offset + (uint64_t)i, w, params,
-                                   m, v, step0 + i, lr, beta1, beta2, adam_eps, loss_out, loss_accum, stream);
+    const int rc = cvae_train_step(h, x, idx ? idx + (size_t)i * batch : nullptr, batch, xflags,
+                                   eps ? eps + (size_t)i * batch * Z : nullptr, seed, offset + (uint64_t)i, eps_row0,
+                                   w, params, m, v, step0 + i, adam, loss_out, loss_accum, counters, stream);
     if (rc) return rc;
   }
   return CVAE_OK;
 }
 
 int cvae_bench_kernels(cvae_handle* h, const void* x, const int64_t* idx, int batch, int reps, float* params,
-                       float* m, float* v, int step0, float* ms, void* stream) {
+                       float* m, float* v, int64_t step0, float* ms, void* stream) {
   if (!h || !x || !params || !m || !v || !ms || reps < 1) return fail(CVAE_E_INVALID, "bad argument");
   int rc = check_batch(h, batch);
   if (rc) return rc;
@@ -831,21 +949,19 @@ int cvae_bench_kernels(cvae_handle* h, const void* x, const int64_t* idx, int ba
   HIPCK(hipEventCreate(&e0));
   HIPCK(hipEventCreate(&e1));
   const cvae_loss_weights w{0.1f, 0.1f, 1.0f, 1.0f};
-  const float lr = 1e-3f, b1 = 0.9f, b2 = 0.999f, ae = 1e-8f;
+  const cvae_adam_config ac{1e-3, 0.9, 0.999, 1e-8};
   auto timed = [&](int which, float* out) -> int {
     HIPCK(hipEventRecord(e0, s));
     for (int r = 0; r < reps; ++r) {
       int rc2 = CVAE_OK;
-      RowArgs ra;
+      const CallX c{x, idx, batch, 0, nullptr, 1, (uint64_t)r, 0, &w, nullptr};
       if (which == 0) {
-        rc2 = is16(h) ? train_fwd_bwd_impl<__bf16>(h, x, idx, batch, nullptr, 1, r, &w, s, ra)
-                                        : train_fwd_bwd_impl<float>(h, x, idx, batch, nullptr, 1, r, &w, s, ra);
+        rc2 = is16(h) ? launch_train_chain<__bf16>(h, row_args(h, c), s) : launch_train_chain<float>(h, row_args(h, c), s);
       } else if (which == 1) {
-        AdamArgs aa = make_adam(params, nullptr, m, v, step0 + r, lr, b1, b2, ae, 1.f);
+        AdamArgs aa = make_adam(params, nullptr, m, v, step0 + r, ac, 1.f, nullptr);
         rc2 = launch_wgrad<PM_ADAM>(h, batch, aa, LossArgs{}, s);
       } else {
-        rc2 = cvae_train_step(h, x, idx, batch, nullptr, 1, r, &w, params, m, v, step0 + r, lr, b1, b2, ae, nullptr,
-                              nullptr, stream);
+        rc2 = train_step_impl(h, c, params, m, v, step0 + r, &ac, nullptr, nullptr, s);
       }
       if (rc2) return rc2;
     }
@@ -885,6 +1001,31 @@ int cvae_loss(const float* recon, const float* x, const float* mu, const float* 
   la.w_recon = w->recon; la.w_kld = w->kld; la.w_start = w->start; la.w_time = w->time;
   la.loss_out = loss_out;
   hipLaunchKernelGGL(loss_finish_kernel, dim3(1), dim3(64), 0, s, la, seq_len, dim, latent_dim);
+  HIPCK(hipGetLastError());
+  return CVAE_OK;
+}
+
+int cvae_loss_backward(const float* recon, const float* x, const float* mu, const float* logvar, int batch,
+                       int seq_len, int dim, int latent_dim, const cvae_loss_weights* w, const float* g_out,
+                       float* d_recon, float* d_mu, float* d_logvar, void* stream) {
+  if (!recon || !x || !mu || !logvar || !w || !g_out || !d_recon || !d_mu || !d_logvar)
+    return fail(CVAE_E_INVALID, "null argument");
+  if (batch < 1 || seq_len < 1 || dim < 3 || latent_dim < 1) return fail(CVAE_E_INVALID, "bad shape");
+  const int64_t n = (int64_t)batch * (seq_len * dim + latent_dim);
+  const int grid = (int)std::min<int64_t>((n + CVAE_THREADS - 1) / CVAE_THREADS, 4096);
+  hipLaunchKernelGGL(loss_backward_kernel, dim3(grid), dim3(CVAE_THREADS), 0, (hipStream_t)stream, recon, x, mu,
+                     logvar, batch, seq_len, dim, latent_dim, *w, g_out, d_recon, d_mu, d_logvar);
+  HIPCK(hipGetLastError());
+  return CVAE_OK;
+}
+
+int cvae_adam_scalars(const cvae_adam_config* adam, int64_t n, float* out, void* stream) {
+  int rc = check_adam(adam);
+  if (rc) return rc;
+  if (!out || n < 1) return fail(CVAE_E_INVALID, "bad argument");
+  const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(adam_scalars_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, adam->lr, adam->beta1,
+                     adam->beta2, n, out);
   HIPCK(hipGetLastError());
   return CVAE_OK;
 }

@@ -325,9 +325,9 @@ __device__ __forceinline__ void chain_body(const FastNet& net, const RowArgs& a,
     if (tid >= NT - 2 * R) {
       const int k = tid - (NT - 2 * R), row = k >> 1, j0 = (k & 1) * 4;
       f32x4 e = {0.f, 0.f, 0.f, 0.f};
-      if (row < nrows)
+      if (row < nrows)  // Philox keyed by the global row (data parallelism: eps_row0 = the rank's first row)
         e = a.eps ? gld<f32x4>(a.eps + (size_t)(b0 + row) * Z + j0)
-                  : philox_normal4(a.seed, a.offset, (uint32_t)(b0 + row), (uint32_t)j0);
+                  : philox_normal4(a.seed, rng_offset(a), (uint32_t)(a.eps_row0 + b0 + row), (uint32_t)j0);
 #pragma unroll
       for (int k = 0; k < 4; ++k) EPS[(j0 + k) * R + row] = e[k];
     }
@@ -734,6 +734,8 @@ __device__ __forceinline__ void chain_body(const FastNet& net, const RowArgs& a,
     lbar();
     if (tid == 0) __hip_atomic_fetch_add(pub + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  // device counters: this launch begins optimizer step ctr[1] + 1 (the Adam kernel behind it reads it)
+  if (a.ctr && blk == 0 && tid == 0 && !pub) a.ctr[1] = a.ctr[1] + 1;
   if (CVAE_DIAG_STAMPS && a.stamps && tid < 64) {
     stamp();
     gst<unsigned long long>(a.stamps + blk * 64 + tid, tid < stamp_i ? STAMPS[tid] : 0ull);

@@ -165,8 +165,8 @@ __global__ __launch_bounds__(WG_THREADS) void fastwgrad_kernel(char* arena, floa
 // block polls its group's counter (one lane, relaxed sc1 loads, bounded), joins a workgroup
 // barrier, then reads the rows with sc1 loads only.  Deadlock-free: tiles wait only on chain
 // blocks, which have the lowest indices and are dispatched first; the spin gives up after ~0.5 s
-// (flag sync[4]) rather than hang.  The last tile block to finish zeroes the counters for the next
-// launch (stream order makes that visible to it).
+// (flag sync[4]; the tile then skips its update) rather than hang.  The host zeroes the counters
+// before every launch (stream-ordered memset).
 __host__ __device__ constexpr int ready_layer(int k) {
   return k == 0 ? LD0 : k == 1 ? LD1 : k == 2 ? LD2 : k == 3 ? LD3 : k == 4 ? LFC : k == 5 ? LE3
        : k == 6 ? LC1 : k == 7 ? LE2 : k == 8 ? LE1 : k == 9 ? LE0 : LC0;
@@ -209,7 +209,7 @@ struct ReadyTiles {
 struct FusedArgs {
   AdamArgs aa;
   LossArgs la;
-  unsigned* sync;  // [0..2] group counters, [3] finished tiles, [4] spin time-out flag
+  unsigned* sync;  // [0..2] group counters (zeroed by the host before the launch), [3] unused, [4] sticky spin time-out flag
   int Bk;          // batch rows rounded to the dW K chunk
   int nchain;      // row-chain blocks
 };
@@ -230,18 +230,26 @@ __global__ __launch_bounds__(NT) void fused_step_kernel(FastNet fn, RowArgs a, F
 #ifdef FUSED_DIAG  // diagnostic builds: 1 = tiles exit at once, 2 = tiles exit after their wait
   if (FUSED_DIAG == 1) return;
 #endif
+  // one lane polls its group's counter (bounded); on a time-out the tile sets the sticky flag
+  // sync[4] and SKIPS its update (reading unfinished rows would corrupt params, m and v), so a
+  // failed step leaves the old parameters of its tiles and cvae_sync_words reports it
+  __shared__ int timed_out;
   if (threadIdx.x == 0) {
     unsigned* cnt = f.sync + ready_group(td.layer);
+    int to = 0;
     for (unsigned spins = 0;
          __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)f.nchain;) {
       __builtin_amdgcn_s_sleep(FUSED_SLEEP);  // ~FUSED_SLEEP·64 cycles: ~200 pollers must not load the fabric
       if (++spins == (1u << 24) / FUSED_SLEEP) {
         __hip_atomic_store(f.sync + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        to = 1;
         break;
       }
     }
+    timed_out = to;
   }
   __syncthreads();
+  if (timed_out) return;
 #ifdef FUSED_DIAG
   if (FUSED_DIAG == 2) return;
 #endif
@@ -251,11 +259,8 @@ __global__ __launch_bounds__(NT) void fused_step_kernel(FastNet fn, RowArgs a, F
     wgrad_body<__bf16, PM_ADAM, true, 2>(L, td, f.Bk, f.aa, f.la, tb == NTL - 1, fn.S, fn.D, Z, sh.red, sh.dbp);
   else
     wgrad_body<__bf16, PM_ADAM, true, 1>(L, td, f.Bk, f.aa, f.la, tb == NTL - 1, fn.S, fn.D, Z, sh.red, sh.dbp);
-  if (threadIdx.x == 0 &&
-      __hip_atomic_fetch_add(f.sync + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == NTL - 1) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) __hip_atomic_store(f.sync + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  // the group counters are zeroed by the host before every fused launch (hipMemsetAsync on the
+  // same stream), never inside the kernel: a reset here could race chain blocks still adding
 }
 
 }  // namespace fchain

@@ -162,7 +162,7 @@ inline StepDesc encode_step(const StepSpec& s) {
 }
 
 struct RowArgs {
-  const void* x;          // (N_total, S, D) operand dtype
+  const void* x;          // (N_total, S, D) operand dtype (fp32 with x_f32)
   const int64_t* idx;     // optional row gather
   int batch;
   int nsteps;
@@ -180,8 +180,20 @@ struct RowArgs {
   const float* hc_in;     // DECODE: given condition features (skips the condition encoder)
   unsigned long long* stamps;  // diagnostic builds only
   int x_relative;         // 1: x is relative, condition = start_in (no transform)
-  int pad_;
+  int x_f32;              // 1: x is fp32 whatever T (relative transform in fp32, one rounding)
+  int64_t eps_row0;       // Philox rows are keyed by the GLOBAL row eps_row0 + b (data parallelism)
+  uint64_t* ctr;          // device step counters (cvae.h): offset = ctr[0]; block 0 adds 1 to ctr[1]
+  float* eps_out;         // FWD: the eps each row used (fp32 (batch, Z), nullable)
+  // external-gradient backward (cvae_backward): the loss gradient is given, not computed
+  int ext;
+  const float* d_recon;   // (batch, S, D) fp32, nullable = 0
+  const float* d_mu;      // (batch, Z)
+  const float* d_lv;      // (batch, Z)
+  const float* d_hc;      // (batch, H)
 };
+
+// Philox offset of this launch's eps draws: the device counter when given (a replayable step)
+__device__ __forceinline__ uint64_t rng_offset(const RowArgs& a) { return a.ctr ? gld<uint64_t>(a.ctr) : a.offset; }
 
 struct LdsPlan {
   int sx, sp, shc, sdec, scin;   // row strides (elements of T)
@@ -571,6 +583,8 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
   };
 
   float s_recon = 0.f, s_kl = 0.f, s_start = 0.f, s_t0 = 0.f, s_relu = 0.f;
+  const uint64_t rng_off = rng_offset(a);
+  const uint32_t erow0 = (uint32_t)a.eps_row0;
 
   // the weight stream starts before anything else: first block of the first step
   WBlock<T> pre;
@@ -601,7 +615,8 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
   // tile, and stores the feature-major arena copy of the tile as quad-transposed 8/16-B stores.
   constexpr int EPL = Op<T>::EPL, U = 5;
   const int VPR = I / EPL, NV = R * VPR;
-  const bool vec = MODE != RC_DECODE && (I % EPL) == 0 && (((uintptr_t)xg) & 15) == 0;
+  const bool vec = MODE != RC_DECODE && (I % EPL) == 0 && (((uintptr_t)xg) & 15) == 0 &&
+                   (sizeof(T) == 4 || !a.x_f32);
   const bool fast = vec && !a.x_relative && NV <= U * RC_THREADS;
   if (fast) {
     const float inv_VPR = 1.f / (float)VPR, inv_Dd = 1.f / (float)D;
@@ -687,8 +702,9 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
             s1 = gld<float>(a.start_in + (size_t)(b0 + r) * 2 + 1);
           }
         } else {
-          s0 = to_f(gld<T>(xg + g * I + 1));  // x[:,0,1:3]  (Training_VAE.py:345)
-          s1 = to_f(gld<T>(xg + g * I + 2));
+          // x[:,0,1:3]  (Training_VAE.py:345)
+          s0 = a.x_f32 ? gld<float>((const float*)a.x + g * I + 1) : to_f(gld<T>(xg + g * I + 1));
+          s1 = a.x_f32 ? gld<float>((const float*)a.x + g * I + 2) : to_f(gld<T>(xg + g * I + 2));
         }
       }
       Start[r * 2 + 0] = s0;
@@ -706,7 +722,7 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
         float v = 0.f;
         if (r < nrows && c < I) {
           const int d = c % D;
-          v = to_f(gld<T>(xg + RowG[r] * I + c));
+          v = a.x_f32 ? gld<float>((const float*)a.x + RowG[r] * I + c) : to_f(gld<T>(xg + RowG[r] * I + c));
           if (!a.x_relative) v -= (d == 1 ? Start[r * 2 + 0] : 0.f) + (d == 2 ? Start[r * 2 + 1] : 0.f);
         }
         Xin[r * P.sx + c] = to_t<T>(v);
@@ -752,7 +768,8 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
   const float inv_B = 1.f / Bf;
   const float inv_BS1 = S > 1 ? 1.f / (Bf * (float)(S - 1)) : 0.f;
   const float inv_BZ = 1.f / (Bf * (float)Z);
-  const bool use_start = a.w_start > 0.f, use_time = a.w_time > 0.f;  // Training_VAE.py:247, :256
+  // Training_VAE.py:247, :256; the external-gradient backward takes dL/drecon as given
+  const bool use_start = !a.ext && a.w_start > 0.f, use_time = !a.ext && a.w_time > 0.f;
   const bool prim = R >= 16 || (lane & 15) < R;  // this lane's row is not a duplicate (R < 16)
   const float inv_D = 1.f / (float)D, inv_S = 1.f / (float)S, inv_Z = 1.f / (float)Z;
   const float inv_Zp2 = 1.f / (float)net.Zp2;
@@ -882,7 +899,10 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         float gi = 0.f;
-        if (live && f0 + i < I) {
+        if (live && f0 + i < I && a.ext) {  // cvae_backward: dL/drecon given
+          gi = a.d_recon ? gld<float>(a.d_recon + (size_t)(b0 + row) * I + f0 + i) : 0.f;
+          if (d == 0) Gd0[row * S + s] = gi;
+        } else if (live && f0 + i < I) {
           const float r = v[i] + b4[i];
           const float diff = r - xr[i];
           s_recon += prim ? diff * diff : 0.f;
@@ -917,8 +937,13 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
     // decoder L0 backward: dz and the decoder's share of dh_c (Z, H multiples of 4: no straddle)
     auto epi_d0b = [&](int row, int f0, f32x4 v, f32x4) {
       if (CVAE_DIAG_NOEPI) return;
-      if (f0 < Z) *(f32x4*)(Dz + row * Z + f0) = v;
-      else if (f0 < Z + H) *(f32x4*)(Dhc2 + row * H + f0 - Z) = v;
+      if (f0 < Z) {
+        *(f32x4*)(Dz + row * Z + f0) = v;
+      } else if (f0 < Z + H) {
+        f32x4 y = v;
+        if (a.ext && a.d_hc && row < nrows) y += gld<f32x4>(a.d_hc + (size_t)(b0 + row) * H + f0 - Z);  // H % 4 == 0
+        *(f32x4*)(Dhc2 + row * H + f0 - Z) = y;
+      }
     };
     // dh = G_fc·W_fc → [dh_traj ‖ dh_c(fc share)]   (H % 4 == 0: no straddle)
     auto epi_fcb = [&](int row, int f0, f32x4 v, f32x4) {
@@ -965,9 +990,10 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
           const float mu = MuLv[r * net.Zp2 + j], lv = MuLv[r * net.Zp2 + Z + j];
           sd = expf(0.5f * lv);
           ep = a.eps ? gld<float>(a.eps + (size_t)(b0 + r) * Z + j)
-                     : philox_normal(a.seed, a.offset, (uint32_t)(b0 + r), (uint32_t)j);
+                     : philox_normal(a.seed, rng_off, erow0 + (uint32_t)(b0 + r), (uint32_t)j);
           z = mu + ep * sd;
           s_kl += 1.f + lv - mu * mu - expf(lv);
+          if (MODE == RC_FWD && a.eps_out) gst<float>(a.eps_out + (size_t)(b0 + r) * Z + j, ep);
         }
         Dec[r * P.sdec + j] = to_t<T>(z);
         if (TRAIN && !CVAE_DIAG_NOSTORE) gst<T>(xd0 + aoff(j, b0 + r, net.L[lD(net, 0)].Kp), to_t<T>(z));
@@ -1008,7 +1034,19 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
         if (r < nrows && c < 2 * Z) {
           const int j = c < Z ? c : c - Z;
           const float dz = Dz[r * Z + j];
-          if (c < Z) {
+          if (a.ext) {  // cvae_backward: dL/dmu, dL/dlogvar given (+ the reparameterisation path)
+            const float gin = c < Z ? (a.d_mu ? gld<float>(a.d_mu + (size_t)(b0 + r) * Z + j) : 0.f)
+                                    : (a.d_lv ? gld<float>(a.d_lv + (size_t)(b0 + r) * Z + j) : 0.f);
+            if (c < Z) {
+              g = gin + dz;
+            } else {
+              const float lv = MuLv[r * net.Zp2 + Z + j];
+              const float sd = expf(0.5f * lv);
+              const float ep = a.eps ? gld<float>(a.eps + (size_t)(b0 + r) * Z + j)
+                                     : philox_normal(a.seed, rng_off, erow0 + (uint32_t)(b0 + r), (uint32_t)j);
+              g = gin + dz * ep * 0.5f * sd;
+            }
+          } else if (c < Z) {
             g = a.w_kld * MuLv[r * net.Zp2 + j] * inv_BZ + dz;
           } else {
             // eps and std are recomputed (same draw, same expf) rather than kept in LDS: at
@@ -1016,7 +1054,7 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
             const float lv = MuLv[r * net.Zp2 + Z + j];
             const float sd = expf(0.5f * lv);
             const float ep = a.eps ? gld<float>(a.eps + (size_t)(b0 + r) * Z + j)
-                                   : philox_normal(a.seed, a.offset, (uint32_t)(b0 + r), (uint32_t)j);
+                                   : philox_normal(a.seed, rng_off, erow0 + (uint32_t)(b0 + r), (uint32_t)j);
             g = a.w_kld * 0.5f * (expf(lv) - 1.f) * inv_BZ + dz * ep * 0.5f * sd;
           }
         }
@@ -1036,6 +1074,8 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
     stamp();
   }
   if (!TRAIN) return;
+  // device counters: this launch begins optimizer step ctr[1] + 1 (the Adam kernel behind it reads it)
+  if (a.ctr && blockIdx.x == 0 && tid == 0) a.ctr[1] = a.ctr[1] + 1;
 
   // ---------------------------------------------------------------- loss partial sums (deterministic order)
   s_recon = wave_sum(s_recon);

@@ -52,14 +52,34 @@ struct AdamArgs {
   float* v;
   float* grads;       // PM_GRAD: output; param_kernel PM_ADAM: input
   float grad_scale;
-  float lr_neg_step;  // -lr / (1 - beta1^t)
+  float lr_neg_step;  // -lr / (1 - beta1^t)        (host path; device path: adam_resolve)
   float bc2_sqrt;     // sqrt(1 - beta2^t)
   float beta1_w;      // 1 - beta1  (lerp weight)
   float beta2;
   float one_m_beta2;
   float eps;
   int pad_;
+  const uint64_t* ctr;  // device step counters (cvae.h): t = ctr[1]; NULL = the two scalars above
+  double lr, beta1d, beta2d;
 };
+
+// torch's two per-step Adam scalars from the step count t, in doubles as Python forms them
+// (torch/optim/adam.py: bias_correction1 = 1 - beta1 ** step, step_size = lr / bias_correction1,
+// bias_correction2_sqrt = bias_correction2 ** 0.5), rounded to fp32 where the tensor op takes them
+__device__ __forceinline__ void adam_scalars(double lr, double b1, double b2, double t, float& lr_neg_step,
+                                             float& bc2_sqrt) {
+  const double bc1 = 1.0 - pow(b1, t);
+  const double bc2 = 1.0 - pow(b2, t);
+  lr_neg_step = (float)(-(lr / bc1));
+  bc2_sqrt = (float)sqrt(bc2);
+}
+// device-counter path: the scalars of step t = ctr[1] (every thread; wave-uniform).  Split in two
+// so a kernel can issue the counter load first and do the double arithmetic once its operand loads
+// are in flight (vmcnt retires in order: a load issued after them would wait for all of them).
+__device__ __forceinline__ uint64_t adam_step_load(const AdamArgs& a) { return a.ctr ? gld<uint64_t>(a.ctr + 1) : 0; }
+__device__ __forceinline__ void adam_resolve(AdamArgs& a, uint64_t t) {
+  if (a.ctr) adam_scalars(a.lr, a.beta1d, a.beta2d, (double)t, a.lr_neg_step, a.bc2_sqrt);
+}
 
 struct LossArgs {
   const float* partials;  // [ntiles][8]
@@ -67,7 +87,8 @@ struct LossArgs {
   int batch;
   float w_recon, w_kld, w_start, w_time;
   float* loss_out;        // [5] nullable
-  float* loss_accum;      // [5] nullable, += loss * batch
+  double* loss_accum;     // [5] nullable, += (double)loss * batch (Training_VAE.py:366-370 in doubles)
+  uint64_t* ctr;          // device step counters: the loss finisher advances ctr[0] (Philox offset)
 };
 
 #ifndef CVAE_DIAG_NOADAM
@@ -321,8 +342,10 @@ __device__ void finish_loss(const LossArgs& l, int S, int D, int Z) {
   const float v[5] = {total, recon, kld, start, time};
   for (int k = 0; k < 5; ++k) {
     if (l.loss_out) l.loss_out[k] = v[k];
-    if (l.loss_accum) l.loss_accum[k] += v[k] * B;
+    if (l.loss_accum) l.loss_accum[k] += (double)v[k] * (double)l.batch;
   }
+  // the step's row chain has read the Philox offset (previous launch): advance it for the next step
+  if (l.ctr) l.ctr[0] = l.ctr[0] + 1;
 }
 
 // 8 waves per tile: the batch (K) is cut into 8 wave slices whose loads are all in flight at once
@@ -340,7 +363,7 @@ struct WgradLds {
 // SC1: the arena rows were handed over inside the launch (fused_step_kernel): every load of them
 // is an sc1 buffer load.
 template <typename T, int MODE, bool SC1 = false, int NI = 1>
-__device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td, int Bk, const AdamArgs& aa,
+__device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td, int Bk, AdamArgs aa,
                                            const LossArgs& la, bool loss_block, int S, int D, int Z,
                                            float* red, float* dbp) {
   using V = typename Op<T>::V;
@@ -358,6 +381,7 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
   const int o = tid / TPR, iv = (tid % TPR) * EPT;
 
   WSTAMP(0);
+  const uint64_t t_step = MODE == PM_ADAM ? adam_step_load(aa) : 0;
   f32x4 acc[2][NX];
 #pragma unroll
   for (int m = 0; m < 2; ++m)
@@ -409,6 +433,8 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
   if (bias_tile && tid < 32) sb = loadb<MODE>(L, td.o0 + tid, aa);
 #pragma unroll
   for (int u = 0; u < PF; ++u) load(u, u);
+  // device-counter path: this step's Adam scalars (double pow), computed while the operands load
+  if (MODE == PM_ADAM) adam_resolve(aa, t_step);
   if (loss_block && wave == WG_NW - 1 && la.partials) finish_loss<SC1>(la, S, D, Z);
   for (int j0 = 0; j0 < nmine; j0 += PF) {
 #pragma unroll
@@ -477,8 +503,9 @@ __global__ __launch_bounds__(WG_THREADS) void wgrad_kernel(NetDev net, const Til
 
 // Adam from a (reduced) gradient buffer, or repack of the operand copies.
 template <typename T, int MODE>
-__device__ __forceinline__ void param_body(const LayerDev& L, const TileDesc& td, const AdamArgs& aa, float* wt) {
+__device__ __forceinline__ void param_body(const LayerDev& L, const TileDesc& td, AdamArgs aa, float* wt) {
   const int tid = threadIdx.x;
+  if (MODE == PM_ADAM) adam_resolve(aa, adam_step_load(aa));
   const PreN<4> st = loadn<MODE, 4>(L, td.o0 + (tid >> 3), td.i0 + (tid & 7) * 4, aa);
   PreB sb = {0.f, 0.f, 0.f, -1};
   if (td.i0 == 0 && tid < 32) sb = loadb<MODE>(L, td.o0 + tid, aa);

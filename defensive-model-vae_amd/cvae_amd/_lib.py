@@ -23,43 +23,52 @@ class CvaeLossWeights(C.Structure):
     _fields_ = [("recon", C.c_float), ("kld", C.c_float), ("start", C.c_float), ("time", C.c_float)]
 
 
-CVAE_F32, CVAE_BF16, CVAE_FP8 = 0, 1, 2
+class CvaeAdamConfig(C.Structure):
+    _fields_ = [("lr", C.c_double), ("beta1", C.c_double), ("beta2", C.c_double), ("eps", C.c_double)]
 
+
+CVAE_F32, CVAE_BF16, CVAE_FP8 = 0, 1, 2
+CVAE_X_OPERAND, CVAE_X_F32 = 0, 1
+CVAE_PART_CHAIN, CVAE_PART_DW_DEC, CVAE_PART_DW_REST, CVAE_PART_ALL = 1, 2, 4, 7
+
+_v, _i, _u64, _i64, _f, _d = C.c_void_p, C.c_int, C.c_uint64, C.c_int64, C.c_float, C.c_double
+_W = C.POINTER(CvaeLossWeights)
+_A = C.POINTER(CvaeAdamConfig)
 _SIGS = {
-    "cvae_create": (C.c_int, [C.POINTER(CvaeConfig), C.c_int, C.POINTER(C.c_void_p)]),
-    "cvae_destroy": (C.c_int, [C.c_void_p]),
-    "cvae_num_params": (C.c_int, [C.c_void_p, c_i64p, C.POINTER(C.c_int)]),
-    "cvae_param_info": (C.c_int, [C.c_void_p, C.c_int, c_i64p, c_i64p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
-    "cvae_config_info": (C.c_int, [C.POINTER(CvaeConfig), c_i64p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
-    "cvae_workspace_bytes": (C.c_int, [C.c_void_p, c_i64p]),
-    "cvae_pack_weights": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
-    "cvae_forward": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64,
-                               C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
-    "cvae_condition": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
-    "cvae_decode": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
-    "cvae_train_fwd_bwd": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_uint64,
-                                     C.c_uint64, C.POINTER(CvaeLossWeights), C.c_void_p, C.c_void_p, C.c_void_p,
-                                     C.c_void_p]),
-    "cvae_adam": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_float,
-                            C.c_float, C.c_float, C.c_float, C.c_float, C.c_void_p]),
-    "cvae_train_step": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_uint64, C.c_uint64,
-                                  C.POINTER(CvaeLossWeights), C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
-                                  C.c_float, C.c_float, C.c_float, C.c_float, C.c_void_p, C.c_void_p,
-                                  C.c_void_p]),
-    "cvae_train_steps": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_uint64,
-                                   C.c_uint64, C.POINTER(CvaeLossWeights), C.c_void_p, C.c_void_p, C.c_void_p,
-                                   C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, C.c_void_p, C.c_void_p,
-                                   C.c_void_p]),
-    "cvae_bench_kernels": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
-                                     C.c_void_p, C.c_int, C.POINTER(C.c_float), C.c_void_p]),
-    "cvae_sync_words": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint)]),
-    "cvae_loss": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
-                            C.POINTER(CvaeLossWeights), C.c_void_p, C.c_void_p, C.c_void_p]),
-    "cvae_set_timing": (C.c_int, [C.c_void_p, C.c_int]),
-    "cvae_kernel_times": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int, C.POINTER(C.c_float), C.c_int]),
+    "cvae_create": (_i, [C.POINTER(CvaeConfig), _i, C.POINTER(_v)]),
+    "cvae_destroy": (_i, [_v]),
+    "cvae_num_params": (_i, [_v, c_i64p, C.POINTER(_i)]),
+    "cvae_param_info": (_i, [_v, _i, c_i64p, c_i64p, C.POINTER(_i), C.POINTER(_i)]),
+    "cvae_config_info": (_i, [C.POINTER(CvaeConfig), c_i64p, C.POINTER(_i), C.POINTER(_i)]),
+    "cvae_workspace_bytes": (_i, [_v, c_i64p]),
+    "cvae_bucket_split": (_i, [_v, c_i64p]),
+    "cvae_pack_weights": (_i, [_v, _v, _v]),
+    # h, x, idx, batch, xflags, start, eps, seed, offset, eps_row0, recon, mu, logvar, hc, eps_out, stream
+    "cvae_forward": (_i, [_v, _v, _v, _i, _i, _v, _v, _u64, _u64, _i64, _v, _v, _v, _v, _v, _v]),
+    "cvae_condition": (_i, [_v, _v, _i, _v, _v]),
+    "cvae_decode": (_i, [_v, _v, _v, _v, _i, _v, _v]),
+    # h, x, idx, batch, xflags, eps, seed, offset, eps_row0, w, grads, loss_out, loss_accum, counters, parts, stream
+    "cvae_train_fwd_bwd": (_i, [_v, _v, _v, _i, _i, _v, _u64, _u64, _i64, _W, _v, _v, _v, _v, _i, _v]),
+    # h, x, idx, batch, xflags, start, eps, seed, offset, eps_row0, d_recon, d_mu, d_logvar, d_hc, grads, stream
+    "cvae_backward": (_i, [_v, _v, _v, _i, _i, _v, _v, _u64, _u64, _i64, _v, _v, _v, _v, _v, _v]),
+    # h, params, grads, m, v, step, adam, grad_scale, counters, stream
+    "cvae_adam": (_i, [_v, _v, _v, _v, _v, _i64, _A, _f, _v, _v]),
+    # h, x, idx, batch, xflags, eps, seed, offset, eps_row0, w, params, m, v, step, adam, loss_out, loss_accum,
+    # counters, stream
+    "cvae_train_step": (_i, [_v, _v, _v, _i, _i, _v, _u64, _u64, _i64, _W, _v, _v, _v, _i64, _A, _v, _v, _v, _v]),
+    "cvae_train_steps": (_i, [_v, _v, _v, _i, _i, _i, _v, _u64, _u64, _i64, _W, _v, _v, _v, _i64, _A, _v, _v, _v,
+                              _v]),
+    "cvae_bench_kernels": (_i, [_v, _v, _v, _i, _i, _v, _v, _v, _i64, C.POINTER(_f), _v]),
+    "cvae_sync_words": (_i, [_v, C.POINTER(C.c_uint)]),
+    "cvae_loss": (_i, [_v, _v, _v, _v, _i, _i, _i, _i, _W, _v, _v, _v]),
+    "cvae_loss_backward": (_i, [_v, _v, _v, _v, _i, _i, _i, _i, _W, _v, _v, _v, _v, _v]),
+    "cvae_adam_scalars": (_i, [_A, _i64, _v, _v]),
+    "cvae_set_timing": (_i, [_v, _i]),
+    "cvae_kernel_times": (_i, [_v, C.c_char_p, _i, C.POINTER(_f), _i]),
     "cvae_last_error": (C.c_char_p, []),
-    "cvae_abi_version": (C.c_int, []),
+    "cvae_abi_version": (_i, []),
 }
+ABI_VERSION = 2
 
 _lib = None
 
@@ -74,6 +83,8 @@ def lib():
         for name, (res, args) in _SIGS.items():
             f = getattr(h, name)
             f.restype, f.argtypes = res, args
+        if h.cvae_abi_version() != ABI_VERSION:
+            raise RuntimeError(f"{LIB} has ABI {h.cvae_abi_version()}, this binding expects {ABI_VERSION} (rebuild)")
         _lib = h
     return _lib
 
@@ -82,6 +93,11 @@ def header_symbols(header_path: str):
     """Function names declared in include/cvae.h (used by the export test)."""
     txt = open(header_path).read()
     return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(cvae_\w+)\s*\(", txt, re.M)))
+
+
+def missing_signatures(header_path: str):
+    """Header functions without a ctypes signature here (the binding must cover the whole ABI)."""
+    return [n for n in header_symbols(header_path) if n not in _SIGS]
 
 
 class CvaeError(RuntimeError):

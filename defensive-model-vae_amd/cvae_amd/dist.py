@@ -4,14 +4,23 @@ The reference trains in one process (Training_VAE.py:326-370).  Every loss term 
 batch elements (:240-264), so the gradient of the global-batch mean is the batch-weighted mean
 of the per-rank gradients — one exchange per step:
 
-    rank r:  forward_backward(rows of global batch assigned to r)   → grads_r (mean over B_r)
+    rank r:  forward_backward(rows lo_r..hi_r of global batch)          → grads_r (mean over B_r)
              grads_r *= B_r / B_global      (skipped when every rank has the same B_r)
-             all_reduce(grads, SUM)                                 → global-mean gradient
-             adam_step(grad_scale = 1/world  or 1)                  → identical params on every rank
+             all_reduce(grads, SUM)                                    → global-mean gradient
+             adam_step(grad_scale = 1/world  or 1)                     → identical params on every rank
 
 Parameters and Adam moments are replicated (1.1 MB each at cfg2 — sharding them buys nothing);
-the only collective on the data path is the 1.1 MB fp32 gradient all-reduce, plus one 5-float
+the only collective on the data path is the 1.1 MB fp32 gradient all-reduce, plus one 5-double
 all-reduce per epoch for the loss log.
+
+eps: the in-kernel Philox draw is keyed by the GLOBAL row (``row0`` = lo_r, the rank's first row
+of the global batch) and every rank advances the same device offset, so the ranks of a global
+batch draw exactly the noise one process with that batch draws — not rank 0's noise B_r times.
+
+Two-bucket overlap (``buckets=2``): the dW launch is split into the decoder layers (a contiguous
+tail of the flat gradient, ready first) and the rest; the decoder bucket's all-reduce is issued
+asynchronously (RCCL runs it on the process group's stream) while the rest of the dW GEMMs run
+on the compute stream, then the second bucket follows.
 
 Row assignment (``shard_rows``): every rank draws the same global permutation, cuts it into
 global batches of ``batch_size * world`` and takes a contiguous slice of each, so a run over
@@ -56,14 +65,27 @@ def shard_rows(perm, batch_size, world_size, rank):
 
 
 class DataParallelStep:
-    """fwd+bwd → gradient all-reduce → Adam on every rank (the fused single-GPU step split in two)."""
+    """fwd+bwd → gradient all-reduce → Adam on every rank (the fused single-GPU step split in two).
 
-    def __init__(self, engine, group=None):
+    ``force_split``: run the split path (and its all-reduce) even at world 1 — the route every rank
+    of a multi-GPU run takes, measurable on one GPU (``bench.py --dp``).
+    ``buckets``: 1 = one all-reduce after the whole dW launch; 2 = decoder bucket overlapped with
+    the rest of the dW GEMMs (see the module docstring)."""
+
+    def __init__(self, engine, group=None, force_split=False, buckets=1):
         self.engine = engine
         self.group = group
         self.rank, self.world_size = world()
         if group is not None:
             self.rank, self.world_size = dist.get_rank(group), dist.get_world_size(group)
+        self.force_split = force_split
+        if buckets not in (1, 2):
+            raise ValueError("buckets must be 1 or 2")
+        self.buckets = buckets
+
+    @property
+    def split(self):
+        return self.world_size > 1 or self.force_split
 
     def broadcast_params(self, src=0):
         """Start every rank from rank ``src``'s parameters (call once after init / load)."""
@@ -71,36 +93,85 @@ class DataParallelStep:
             dist.broadcast(self.engine.params, src, group=self.group)
             self.engine.pack()
 
-    def step(self, x, idx=None, eps=None, batch=None, global_batch=None, weights=None):
-        """One data-parallel training step; ``batch`` = this rank's rows, ``global_batch`` = Σ over ranks."""
+    def step(self, x, idx=None, eps=None, batch=None, global_batch=None, weights=None, row0=None):
+        """One data-parallel training step; ``batch`` = this rank's rows, ``global_batch`` = Σ over
+        ranks, ``row0`` = this rank's first row in the global batch (default: rank · batch)."""
         eng = self.engine
         if batch is None:
             batch = idx.numel() if idx is not None else x.shape[0]
         batch = int(batch)
         if global_batch is None:
             global_batch = batch * self.world_size
-        if self.world_size == 1:
+        if row0 is None:
+            row0 = self.rank * batch
+        if not self.split:
             if batch > 0:
-                eng.train_step(x, idx=idx, eps=eps, batch=batch, weights=weights)
+                eng.train_step(x, idx=idx, eps=eps, batch=batch, weights=weights, row0=row0)
             return eng.loss
+        two = self.buckets == 2  # every rank issues the same collectives, empty shares included
         if batch > 0:
-            eng.forward_backward(x, idx=idx, eps=eps, batch=batch, weights=weights)
-            if batch * self.world_size != global_batch:
-                eng.grads.mul_(batch / global_batch)
-                scale = 1.0
-            else:
-                scale = 1.0 / self.world_size
-        else:  # an empty share of a ragged last batch still joins the collective
+            parts = 3 if two else 7  # CVAE_PART_CHAIN | DW_DEC, or CVAE_PART_ALL
+            eng.forward_backward(x, idx=idx, eps=eps, batch=batch, weights=weights, row0=row0, parts=parts)
+            ragged = batch * self.world_size != global_batch
+            scale = 1.0 if ragged else 1.0 / self.world_size
+        else:  # an empty share of a ragged last batch still joins the collectives
             eng.grads.zero_()
-            scale = 1.0
-        dist.all_reduce(eng.grads, op=dist.ReduceOp.SUM, group=self.group)
+            ragged, scale = True, 1.0
+        g = eng.grads
+        if two:
+            dec, rest = g[eng.bucket_split:], g[:eng.bucket_split]
+            if ragged:
+                dec.mul_(batch / global_batch)
+            w1 = dist.all_reduce(dec, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            if batch > 0:
+                eng.wgrad_rest(batch)  # beside the decoder bucket's all-reduce
+            if ragged:
+                rest.mul_(batch / global_batch)
+            w2 = dist.all_reduce(rest, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            w1.wait()
+            w2.wait()
+        else:
+            if ragged and batch > 0:
+                g.mul_(batch / global_batch)
+            dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group)
         eng.adam_step(grad_scale=scale)
         return eng.loss
 
     def epoch_loss_sums(self):
-        """Σ over ranks of the device Σ loss·batch accumulators (5 floats); resets them."""
+        """Σ over ranks of the device Σ loss·batch accumulators (5 doubles); resets them."""
         acc = self.engine.loss_accum.clone()
         if self.world_size > 1:
             dist.all_reduce(acc, op=dist.ReduceOp.SUM, group=self.group)
         self.engine.loss_accum.zero_()
         return acc
+
+
+class GraphedStep:
+    """A training step captured once into a hipGraph (torch.cuda.CUDAGraph) and replayed.
+
+    Replay is correct because every per-step quantity lives on the device: the Philox offset and
+    the Adam step are the engine's device counters, advanced by the kernels themselves; inputs
+    must sit in fixed device buffers (``x`` resident, ``idx`` a fixed tensor the caller refills).
+    ``fn`` is the step (e.g. ``lambda: dp.step(x, batch=B)``); ``n`` steps per replay.  Before the
+    capture ``warmup`` eager steps run on a side stream (torch's capture recipe); they are real
+    training steps.  The capture itself executes nothing."""
+
+    def __init__(self, engine, fn, n=1, warmup=1):
+        self.engine, self.fn, self.n = engine, fn, int(n)
+        s = torch.cuda.Stream(device=engine.device)
+        s.wait_stream(torch.cuda.current_stream(engine.device))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                fn()
+        torch.cuda.current_stream(engine.device).wait_stream(s)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            for _ in range(self.n):
+                fn()
+        # the capture launched nothing; the host mirrors counted the captured calls: undo that
+        self.engine.sync_counters()
+
+    def replay(self):
+        self.graph.replay()
+        self.engine._ctr[0] += self.n
+        self.engine._ctr[1] += self.n

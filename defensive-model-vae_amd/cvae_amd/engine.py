@@ -7,7 +7,12 @@ parameters, ``torch.optim.Adam`` state and autograd (Training_VAE.py:331-363):
 * ``m, v``    Adam moments (torch ``exp_avg``/``exp_avg_sq``), same layout
 * ``grads``   flat fp32 gradient (data-parallel path); bound ``p.grad`` are views
 * ``loss``    fp32[5] last step's (total, recon, kld, start, time)  — on device
-* ``loss_accum`` fp32[5] running Σ loss·batch for the epoch       — on device
+* ``loss_accum`` fp64[5] running Σ loss·batch for the epoch (Python-double sums of the
+  reference, Training_VAE.py:366-370)                             — on device
+* ``counters`` int64[2] device step counters (include/cvae.h): [0] the Philox offset of the
+  next training step, [1] optimizer steps begun.  Every training call reads and advances them
+  ON THE DEVICE, so a captured step (hipGraph) replays correctly; ``rng_offset`` /
+  ``step_count`` are host mirrors kept in step with every call the host issues.
 
 Every call enqueues HIP kernels on torch's current stream and returns without
 synchronising.  Nothing falls back to torch compute.
@@ -18,7 +23,9 @@ import ctypes as C
 
 import torch
 
-from ._lib import CVAE_BF16, CVAE_F32, CVAE_FP8, CvaeConfig, CvaeLossWeights, check, lib, ptr
+from ._lib import (CVAE_BF16, CVAE_F32, CVAE_FP8, CVAE_PART_ALL, CVAE_PART_CHAIN, CVAE_PART_DW_DEC,
+                   CVAE_PART_DW_REST, CVAE_X_F32, CVAE_X_OPERAND, CvaeAdamConfig, CvaeConfig, CvaeLossWeights,
+                   check, lib, ptr)
 
 # "fp8": bf16 activations with OCP e4m3 forward GEMM operands (BASELINE cfg5; cvae.h CVAE_FP8)
 DTYPES = {"fp32": (CVAE_F32, torch.float32), "bf16": (CVAE_BF16, torch.bfloat16),
@@ -63,19 +70,26 @@ class CVAEEngine:
             check(lib().cvae_param_info(h, i, C.byref(off), C.byref(numel), C.byref(rows), C.byref(cols)))
             shape = (rows.value, cols.value) if cols.value > 0 else (rows.value,)
             self.tensors.append((off.value, numel.value, shape))
+        split = C.c_int64()
+        check(lib().cvae_bucket_split(h, C.byref(split)))
+        self.bucket_split = split.value  # decoder.0.weight: grads[split:] is the decoder bucket
         kw = dict(device=self.device, dtype=torch.float32)
         self.params = torch.zeros(self.n_params, **kw)
         self.m = torch.zeros(self.n_params, **kw)
         self.v = torch.zeros(self.n_params, **kw)
         self.grads = torch.zeros(self.n_params, **kw)
         self.loss = torch.zeros(5, **kw)
-        self.loss_accum = torch.zeros(5, **kw)
-        self.step_count = 0
+        self.loss_accum = torch.zeros(5, device=self.device, dtype=torch.float64)
+        self.counters = torch.zeros(2, device=self.device, dtype=torch.int64)
+        self._ctr = [0, 0]  # host mirrors of counters
         self.seed = int(seed)
-        self.rng_offset = 0
         self.lr, self.betas, self.eps = 1e-3, (0.9, 0.999), 1e-8
         self.weights = DEFAULT_WEIGHTS
         self._module = None
+        self._packed_version = None
+        # fp32 trajectories handed to a bf16/fp8 engine: False = rounded to the operand dtype on upload
+        # (synthetic N(0,1) data), True = kept fp32, relative transform in fp32 (real data; train())
+        self.keep_f32 = False
 
     # ------------------------------------------------------------------ lifecycle
     def close(self):
@@ -111,25 +125,74 @@ class CVAEEngine:
         self.pack()
         return self
 
+    def _param_version(self):
+        m = self._module
+        return None if m is None else sum(p._version for p in m.parameters())
+
     def pack(self):
         """Refresh the device operand copies (W, Wᵀ, bias) after parameters were written."""
         check(lib().cvae_pack_weights(self._h, ptr(self.params), self._stream()), "cvae_pack_weights")
+        self._packed_version = self._param_version()
+
+    def ensure_packed(self):
+        """Repack if the bound parameters were modified in place since the last pack (an optimizer
+        outside this library, e.g. torch.optim.Adam over model.parameters())."""
+        if self._module is not None and self._param_version() != self._packed_version:
+            self.pack()
 
     def set_optimizer(self, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
         self.lr, self.betas, self.eps = float(lr), (float(betas[0]), float(betas[1])), float(eps)
+
+    def _adam(self):
+        return CvaeAdamConfig(self.lr, self.betas[0], self.betas[1], self.eps)
 
     def reset_optimizer(self):
         self.m.zero_()
         self.v.zero_()
         self.step_count = 0
 
+    # ------------------------------------------------------------------ step counters
+    @property
+    def rng_offset(self):
+        return self._ctr[0]
+
+    @rng_offset.setter
+    def rng_offset(self, v):
+        self._ctr[0] = int(v)
+        self.counters[0].fill_(int(v))
+
+    @property
+    def step_count(self):
+        return self._ctr[1]
+
+    @step_count.setter
+    def step_count(self, v):
+        self._ctr[1] = int(v)
+        self.counters[1].fill_(int(v))
+
+    def sync_counters(self):
+        """Host mirrors ← device counters (after graph replays the host did not count)."""
+        c = self.counters.cpu().tolist()
+        self._ctr = [int(c[0]), int(c[1])]
+        return tuple(self._ctr)
+
     # ------------------------------------------------------------------ inputs
-    def as_input(self, x):
-        """Trajectories in the operand dtype, contiguous on the device."""
+    def as_input(self, x, keep_f32=False):
+        """Trajectories on the device, contiguous: in the operand dtype, or — keep_f32 with an fp32
+        tensor — left fp32 so the kernels subtract the start point in fp32 before rounding (real
+        data with absolute coordinates, Training_VAE.py:345-348)."""
         x = torch.as_tensor(x)
-        if x.device != self.device or x.dtype != self.tdtype or not x.is_contiguous():
-            x = x.to(device=self.device, dtype=self.tdtype).contiguous()
+        want = torch.float32 if (keep_f32 and x.dtype in (torch.float32, torch.float64)) else self.tdtype
+        if x.device != self.device or x.dtype != want or not x.is_contiguous():
+            x = x.to(device=self.device, dtype=want).contiguous()
         return x
+
+    def _xflags(self, x):
+        if x.dtype == self.tdtype:
+            return CVAE_X_OPERAND
+        if x.dtype == torch.float32:
+            return CVAE_X_F32
+        raise ValueError(f"trajectories must be {self.tdtype} or float32, got {x.dtype}")
 
     def _check_rows(self, x, idx, batch):
         S, D = self.shape[0], self.shape[1]
@@ -137,13 +200,19 @@ class CVAEEngine:
             raise ValueError(f"expected (N,{S},{D}) trajectories, got {tuple(x.shape)}")
         if idx is None and batch > x.shape[0]:
             raise ValueError("batch larger than the trajectory tensor")
+        if idx is not None and idx.numel() < batch:
+            raise ValueError(f"idx holds {idx.numel()} rows, the batch needs {batch}")
         if batch > self.max_batch:
             raise ValueError(f"batch {batch} > max_batch {self.max_batch}")
 
-    def _idx(self, idx):
+    def _idx(self, idx, n_rows):
+        """int64 row indices on the device.  A host index tensor is range-checked before the upload
+        (the kernels gather x[idx[b]] without bounds checks); a device one is trusted."""
         if idx is None:
             return None
         idx = torch.as_tensor(idx)
+        if idx.device.type == "cpu" and idx.numel() and (int(idx.min()) < 0 or int(idx.max()) >= n_rows):
+            raise IndexError(f"row index out of range [0, {n_rows})")
         if idx.device != self.device or idx.dtype != torch.int64:
             idx = idx.to(device=self.device, dtype=torch.int64)
         return idx.contiguous()
@@ -160,33 +229,35 @@ class CVAEEngine:
         w = self.weights if weights is None else weights
         return CvaeLossWeights(*[float(v) for v in w])
 
-    def _next_offset(self):
-        o = self.rng_offset
-        self.rng_offset += 1
-        return o
+    def _prep(self, x, idx, batch):
+        x = self.as_input(x, keep_f32=self.keep_f32)
+        idx = self._idx(idx, x.shape[0])
+        B = int(batch if batch is not None else (idx.numel() if idx is not None else x.shape[0]))
+        self._check_rows(x, idx, B)
+        return x, idx, B
 
     # ------------------------------------------------------------------ training
-    def train_step(self, x, idx=None, eps=None, batch=None, weights=None, accumulate=True):
+    def train_step(self, x, idx=None, eps=None, batch=None, weights=None, accumulate=True, row0=0):
         """Fused step (fwd + loss + bwd + Adam) — Training_VAE.py:345-370 for one batch.
 
         ``x``: (B,S,D) absolute trajectories, or the whole dataset with ``idx`` the rows.
+        ``row0``: global row of this batch's first row (Philox eps keying under data parallelism).
         Returns the device loss tensor (total, recon, kld, start, time); no host sync.
         """
-        x = self.as_input(x)
-        idx = self._idx(idx)
-        B = int(batch if batch is not None else (idx.numel() if idx is not None else x.shape[0]))
-        self._check_rows(x, idx, B)
+        x, idx, B = self._prep(x, idx, batch)
         e = self._eps(eps, B)
-        self.step_count += 1
+        self.ensure_packed()
         w = self._weights(weights)
+        a = self._adam()
         check(lib().cvae_train_step(
-            self._h, ptr(x), ptr(idx), B, ptr(e), C.c_uint64(self.seed), C.c_uint64(self._next_offset()),
-            C.byref(w), ptr(self.params), ptr(self.m), ptr(self.v), self.step_count, self.lr, self.betas[0],
-            self.betas[1], self.eps, ptr(self.loss), ptr(self.loss_accum) if accumulate else None,
-            self._stream()), "cvae_train_step")
+            self._h, ptr(x), ptr(idx), B, self._xflags(x), ptr(e), self.seed, 0, int(row0), C.byref(w),
+            ptr(self.params), ptr(self.m), ptr(self.v), 0, C.byref(a), ptr(self.loss),
+            ptr(self.loss_accum) if accumulate else None, ptr(self.counters), self._stream()), "cvae_train_step")
+        self._ctr[0] += 1
+        self._ctr[1] += 1
         return self.loss
 
-    def train_steps(self, x, n_steps, idx=None, eps=None, batch=None, weights=None, accumulate=True):
+    def train_steps(self, x, n_steps, idx=None, eps=None, batch=None, weights=None, accumulate=True, row0=0):
         """``n_steps`` fused steps in one C call (cvae_train_steps): the loop body of
         Training_VAE.py:340-370 over a run of equal-size batches, with no host work per step.
 
@@ -194,13 +265,13 @@ class CVAEEngine:
         every step uses rows 0..batch-1.  ``eps``: (n_steps·batch, Z) or None (Philox).
         Returns the device loss tensor of the last step; no host sync.
         """
-        x = self.as_input(x)
-        idx = self._idx(idx)
+        x = self.as_input(x, keep_f32=self.keep_f32)
+        idx = self._idx(idx, x.shape[0])
         n_steps = int(n_steps)
         if batch is None:
             batch = idx.numel() // max(n_steps, 1) if idx is not None else x.shape[0]
         B = int(batch)
-        self._check_rows(x, idx, B)
+        self._check_rows(x, None if idx is None else idx[:B], B)
         if idx is not None and idx.numel() < n_steps * B:
             raise ValueError(f"idx holds {idx.numel()} rows, {n_steps} steps of {B} need {n_steps * B}")
         e = None
@@ -208,65 +279,109 @@ class CVAEEngine:
             e = torch.as_tensor(eps).to(device=self.device, dtype=torch.float32).contiguous()
             if e.shape != (n_steps * B, self.shape[2]):
                 raise ValueError(f"eps must be ({n_steps * B},{self.shape[2]})")
+        self.ensure_packed()
         w = self._weights(weights)
-        step0 = self.step_count + 1
-        offset = self.rng_offset
+        a = self._adam()
         check(lib().cvae_train_steps(
-            self._h, ptr(x), ptr(idx), B, n_steps, ptr(e), C.c_uint64(self.seed), C.c_uint64(offset), C.byref(w),
-            ptr(self.params), ptr(self.m), ptr(self.v), step0, self.lr, self.betas[0], self.betas[1], self.eps,
-            ptr(self.loss), ptr(self.loss_accum) if accumulate else None, self._stream()), "cvae_train_steps")
-        self.step_count += n_steps
-        self.rng_offset += n_steps
+            self._h, ptr(x), ptr(idx), B, n_steps, self._xflags(x), ptr(e), self.seed, 0, int(row0), C.byref(w),
+            ptr(self.params), ptr(self.m), ptr(self.v), 0, C.byref(a), ptr(self.loss),
+            ptr(self.loss_accum) if accumulate else None, ptr(self.counters), self._stream()), "cvae_train_steps")
+        self._ctr[0] += n_steps
+        self._ctr[1] += n_steps
         return self.loss
 
-    def forward_backward(self, x, idx=None, eps=None, batch=None, weights=None, accumulate=True):
-        """fwd + loss + bwd into ``self.grads`` (means over this batch) — the DP half-step."""
-        x = self.as_input(x)
-        idx = self._idx(idx)
-        B = int(batch if batch is not None else (idx.numel() if idx is not None else x.shape[0]))
-        self._check_rows(x, idx, B)
+    def forward_backward(self, x, idx=None, eps=None, batch=None, weights=None, accumulate=True, row0=0,
+                         parts=CVAE_PART_ALL):
+        """fwd + loss + bwd into ``self.grads`` (means over this batch) — the DP half-step.
+
+        ``parts``: CVAE_PART_ALL, or CHAIN|DW_DEC then (separately) ``wgrad_rest()`` — the two-bucket
+        split that lets the decoder bucket's all-reduce run beside the rest of the dW GEMMs."""
+        x, idx, B = self._prep(x, idx, batch)
         e = self._eps(eps, B)
+        self.ensure_packed()
         w = self._weights(weights)
         check(lib().cvae_train_fwd_bwd(
-            self._h, ptr(x), ptr(idx), B, ptr(e), C.c_uint64(self.seed), C.c_uint64(self._next_offset()),
-            C.byref(w), ptr(self.grads), ptr(self.loss), ptr(self.loss_accum) if accumulate else None,
-            self._stream()), "cvae_train_fwd_bwd")
+            self._h, ptr(x), ptr(idx), B, self._xflags(x), ptr(e), self.seed, 0, int(row0), C.byref(w),
+            ptr(self.grads), ptr(self.loss), ptr(self.loss_accum) if accumulate else None, ptr(self.counters),
+            int(parts), self._stream()), "cvae_train_fwd_bwd")
+        self._ctr[0] += 1
+        self._ctr[1] += 1
+        self._last_batch = B
         return self.loss
 
-    def adam_step(self, grad_scale=1.0):
-        """optimizer.step() on the flat buffers with g = grads * grad_scale (Training_VAE.py:363)."""
-        self.step_count += 1
-        check(lib().cvae_adam(self._h, ptr(self.params), ptr(self.grads), ptr(self.m), ptr(self.v),
-                              self.step_count, self.lr, self.betas[0], self.betas[1], self.eps,
-                              float(grad_scale), self._stream()), "cvae_adam")
+    def wgrad_rest(self, batch=None):
+        """The second dW bucket (condition encoder, encoder, fc) of the batch the last
+        ``forward_backward(parts=CHAIN|DW_DEC)`` ran."""
+        B = int(batch if batch is not None else self._last_batch)
+        check(lib().cvae_train_fwd_bwd(
+            self._h, None, None, B, 0, None, 0, 0, 0, None, ptr(self.grads), None, None, None, CVAE_PART_DW_REST,
+            self._stream()), "cvae_train_fwd_bwd(rest)")
 
-    # ------------------------------------------------------------------ inference
-    def forward(self, x, start=None, idx=None, eps=None, batch=None, outputs=("recon", "mu", "logvar", "hc")):
-        """Training_VAE.py:217-226.  start=None: x absolute (transform in-kernel); else x relative."""
+    def adam_step(self, grad_scale=1.0):
+        """optimizer.step() on the flat buffers with g = grads * grad_scale (Training_VAE.py:363);
+        the step number is the device counter the preceding forward_backward advanced."""
+        a = self._adam()
+        check(lib().cvae_adam(self._h, ptr(self.params), ptr(self.grads), ptr(self.m), ptr(self.v), 0,
+                              C.byref(a), float(grad_scale), ptr(self.counters), self._stream()), "cvae_adam")
+
+    def adam_host_step(self, step, grad_scale=1.0, grads=None):
+        """Adam with a host step number (no device counters): grads default ``self.grads``."""
+        a = self._adam()
+        g = self.grads if grads is None else grads
+        check(lib().cvae_adam(self._h, ptr(self.params), ptr(g), ptr(self.m), ptr(self.v), int(step),
+                              C.byref(a), float(grad_scale), None, self._stream()), "cvae_adam")
+
+    # ------------------------------------------------------------------ inference / autograd
+    def forward(self, x, start=None, idx=None, eps=None, batch=None, outputs=("recon", "mu", "logvar", "hc"),
+                row0=0, offset=None):
+        """Training_VAE.py:217-226.  start=None: x absolute (transform in-kernel); else x relative.
+        eps None: in-kernel Philox at ``offset`` (default: the next host offset, then advanced)."""
         S, D, Z, H = self.shape[:4]
-        x = self.as_input(x)
-        idx = self._idx(idx)
-        B = int(batch if batch is not None else (idx.numel() if idx is not None else x.shape[0]))
-        self._check_rows(x, idx, B)
+        x, idx, B = self._prep(x, idx, batch)
         e = self._eps(eps, B)
+        self.ensure_packed()
         st = None
         if start is not None:
             st = torch.as_tensor(start).to(device=self.device, dtype=torch.float32).contiguous()
+        if offset is None:
+            offset = self.rng_offset
+            self.rng_offset = offset + 1
         kw = dict(device=self.device, dtype=torch.float32)
         out = {"recon": torch.empty(B, S, D, **kw) if "recon" in outputs else None,
                "mu": torch.empty(B, Z, **kw) if "mu" in outputs else None,
                "logvar": torch.empty(B, Z, **kw) if "logvar" in outputs else None,
-               "hc": torch.empty(B, H, **kw) if "hc" in outputs else None}
-        check(lib().cvae_forward(self._h, ptr(x), ptr(idx), B, ptr(st), ptr(e), C.c_uint64(self.seed),
-                                 C.c_uint64(self._next_offset()), ptr(out["recon"]), ptr(out["mu"]),
-                                 ptr(out["logvar"]), ptr(out["hc"]), self._stream()), "cvae_forward")
+               "hc": torch.empty(B, H, **kw) if "hc" in outputs else None,
+               "eps": torch.empty(B, Z, **kw) if "eps" in outputs else None}
+        check(lib().cvae_forward(self._h, ptr(x), ptr(idx), B, self._xflags(x), ptr(st), ptr(e), self.seed,
+                                 int(offset), int(row0), ptr(out["recon"]), ptr(out["mu"]), ptr(out["logvar"]),
+                                 ptr(out["hc"]), ptr(out["eps"]), self._stream()), "cvae_forward")
+        if "eps" in outputs:
+            return out["recon"], out["mu"], out["logvar"], out["hc"], out["eps"]
         return out["recon"], out["mu"], out["logvar"], out["hc"]
+
+    def backward(self, x, start, eps, offset, d_recon, d_mu=None, d_logvar=None, d_hc=None, row0=0, grads=None):
+        """Gradient of the forward (x relative, start, eps / Philox offset) w.r.t. every parameter from
+        the output gradients (cvae_backward: recompute + backward).  Writes ``grads`` (default a
+        fresh flat buffer) and returns it."""
+        x, _, B = self._prep(x, None, None)
+        st = None if start is None else torch.as_tensor(start).to(device=self.device,
+                                                                    dtype=torch.float32).contiguous()
+        e = self._eps(eps, B)
+        f = lambda t: None if t is None else t.to(device=self.device, dtype=torch.float32).contiguous()  # noqa: E731
+        out = torch.empty(self.n_params, device=self.device, dtype=torch.float32) if grads is None else grads
+        self.ensure_packed()
+        dr, dm, dl, dh = f(d_recon), f(d_mu), f(d_logvar), f(d_hc)
+        check(lib().cvae_backward(self._h, ptr(x), None, B, self._xflags(x), ptr(st), ptr(e), self.seed, int(offset),
+                                  int(row0), ptr(dr), ptr(dm), ptr(dl), ptr(dh), ptr(out), self._stream()),
+              "cvae_backward")
+        return out
 
     def condition(self, start):
         """condition_encoder(start) — Training_VAE.py:132-137."""
         st = torch.as_tensor(start).to(device=self.device, dtype=torch.float32).contiguous()
         B = st.shape[0]
         hc = torch.empty(B, self.shape[3], device=self.device, dtype=torch.float32)
+        self.ensure_packed()
         check(lib().cvae_condition(self._h, ptr(st), B, ptr(hc), self._stream()), "cvae_condition")
         return hc
 
@@ -278,6 +393,7 @@ class CVAEEngine:
         st = None if start is None else torch.as_tensor(start).to(device=self.device, dtype=torch.float32).contiguous()
         h = None if hc is None else torch.as_tensor(hc).to(device=self.device, dtype=torch.float32).contiguous()
         out = torch.empty(B, S, D, device=self.device, dtype=torch.float32)
+        self.ensure_packed()
         check(lib().cvae_decode(self._h, ptr(z), ptr(st), ptr(h), B, ptr(out), self._stream()), "cvae_decode")
         return out
 
@@ -299,19 +415,16 @@ class CVAEEngine:
     def bench_kernels(self, x, reps, idx=None, batch=None):
         """{'rowchain', 'wgrad_adam', 'step'}: average device ms of ``reps`` back-to-back launches
         (cvae_bench_kernels; synchronises; updates params like training steps)."""
-        x = self.as_input(x)
-        idx = self._idx(idx)
-        B = int(batch if batch is not None else (idx.numel() if idx is not None else x.shape[0]))
-        self._check_rows(x, idx, B)
+        x, idx, B = self._prep(x, idx, batch)
         ms = (C.c_float * 3)()
         check(lib().cvae_bench_kernels(self._h, ptr(x), ptr(idx), B, int(reps), ptr(self.params), ptr(self.m),
                                        ptr(self.v), self.step_count + 1, ms, self._stream()), "cvae_bench_kernels")
-        self.step_count += 2 * int(reps)
+        self.step_count = self.step_count + 2 * int(reps)
         return {"rowchain": ms[0], "wgrad_adam": ms[1], "step": ms[2]}
 
     def sync_words(self):
-        """The fused launch's hand-off words (cvae_sync_words): [group0, group1, group2, finished
-        tiles, time-out flag], all 0 between launches."""
+        """The fused launch's hand-off words (cvae_sync_words): [group0, group1, group2, unused,
+        sticky time-out flag]; the counters are zeroed before every launch."""
         out = (C.c_uint * 5)()
         check(lib().cvae_sync_words(self._h, out), "cvae_sync_words")
         return list(out)
@@ -320,3 +433,17 @@ class CVAEEngine:
         b = C.c_int64()
         check(lib().cvae_workspace_bytes(self._h, C.byref(b)))
         return b.value
+
+
+def adam_scalars(n, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, device="cuda"):
+    """The device's (−lr/(1−β1^t), sqrt(1−β2^t)) for t = 1..n (cvae_adam_scalars), as an (n, 2)
+    fp32 tensor — the check of the device-counter Adam path against torch's Python doubles."""
+    out = torch.empty(n, 2, device=device, dtype=torch.float32)
+    a = CvaeAdamConfig(float(lr), float(betas[0]), float(betas[1]), float(eps))
+    check(lib().cvae_adam_scalars(C.byref(a), int(n), ptr(out),
+                                  C.c_void_p(torch.cuda.current_stream(out.device).cuda_stream)), "cvae_adam_scalars")
+    return out
+
+
+__all__ = ["CVAEEngine", "config_info", "adam_scalars", "DTYPES", "DEFAULT_WEIGHTS", "CVAE_PART_ALL",
+           "CVAE_PART_CHAIN", "CVAE_PART_DW_DEC", "CVAE_PART_DW_REST"]

@@ -11,8 +11,16 @@
 * ``conditional_vae_loss(...)`` — Training_VAE.py:229-268 via ``cvae_loss``.
 * ``TrajectoryDataset(path)`` — Training_VAE.py:105-115.
 
-Training goes through ``cvae_amd.train`` / ``CVAEEngine.train_step`` (the fused
-step); the module's outputs carry no autograd graph.
+Two ways to train:
+
+* the fused step — ``cvae_amd.train`` / ``CVAEEngine.train_step`` (forward, loss, backward and
+  Adam in two kernels, no autograd);
+* the reference's own loop, unchanged (Training_VAE.py:338-363): ``model(batch_rel, start)``
+  returns autograd-tracked outputs (``_ForwardFn``: cvae_forward, backward = cvae_backward),
+  ``conditional_vae_loss`` is differentiable (``_LossFn``: cvae_loss / cvae_loss_backward), so
+  ``loss.backward()`` fills ``p.grad`` through the HIP kernels and any torch optimizer over
+  ``model.parameters()`` steps them; the engine repacks its operand copies when it sees the
+  parameters' version counters move.
 """
 from __future__ import annotations
 
@@ -25,6 +33,62 @@ import torch.nn as nn
 
 from ._lib import CvaeLossWeights, check, lib, ptr
 from .engine import CVAEEngine
+
+
+class _ForwardFn(torch.autograd.Function):
+    """model.forward as one autograd node: outputs (recon, mu, logvar, h_c) of cvae_forward; the
+    backward recomputes the same forward (same eps / Philox offset) and back-propagates the four
+    output gradients to every parameter (cvae_backward)."""
+
+    @staticmethod
+    def forward(ctx, eng, x, start, eps, offset, *params):
+        recon, mu, lv, hc = eng.forward(x, start=start, eps=eps, offset=offset)
+        ctx.eng, ctx.offset = eng, offset
+        ctx.save_for_backward(x, start, eps)
+        return recon, mu, lv, hc
+
+    @staticmethod
+    def backward(ctx, d_recon, d_mu, d_lv, d_hc):
+        x, start, eps = ctx.saved_tensors
+        eng = ctx.eng
+        flat = eng.backward(x, start, eps, ctx.offset, d_recon, d_mu, d_lv, d_hc)
+        return (None, None, None, None, None, *eng.views(flat))
+
+
+class _LossFn(torch.autograd.Function):
+    """conditional_vae_loss as one autograd node: the 5 losses (cvae_loss); backward
+    cvae_loss_backward (dL/drecon, dL/dmu, dL/dlogvar from the 5 upstream gradients)."""
+
+    @staticmethod
+    def forward(ctx, recon, x, mu, logvar, weights):
+        B, S, D = recon.shape
+        Z = mu.shape[1]
+        dev = recon.device
+        out = torch.empty(5, device=dev, dtype=torch.float32)
+        ws = torch.empty(8 * ((B + 31) // 32), device=dev, dtype=torch.float32)
+        w = CvaeLossWeights(*weights)
+        with torch.cuda.device(dev):
+            check(lib().cvae_loss(ptr(recon), ptr(x), ptr(mu), ptr(logvar), B, S, D, Z, C.byref(w), ptr(out), ptr(ws),
+                                  C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "cvae_loss")
+        ctx.weights = weights
+        ctx.save_for_backward(recon, x, mu, logvar)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        recon, x, mu, logvar = ctx.saved_tensors
+        B, S, D = recon.shape
+        Z = mu.shape[1]
+        dev = recon.device
+        g = g.to(device=dev, dtype=torch.float32).contiguous()
+        d_recon, d_mu, d_lv = torch.empty_like(recon), torch.empty_like(mu), torch.empty_like(logvar)
+        w = CvaeLossWeights(*ctx.weights)
+        with torch.cuda.device(dev):
+            check(lib().cvae_loss_backward(ptr(recon), ptr(x), ptr(mu), ptr(logvar), B, S, D, Z, C.byref(w), ptr(g),
+                                           ptr(d_recon), ptr(d_mu), ptr(d_lv),
+                                           C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)),
+                  "cvae_loss_backward")
+        return d_recon, None, d_mu, d_lv, None
 
 
 def _need(model):
@@ -105,7 +169,27 @@ class ConditionalTrajectoryVAE(nn.Module):
         return _need(self).decode(z, hc=condition)
 
     def forward(self, x, start_points, eps=None):  # :217-226 (x relative, start absolute)
-        return _need(self).forward(x, start=start_points, eps=eps)
+        """model(batch_rel, start_points) → (recon, mu, logvar, h_c), autograd-tracked.
+
+        eps (the reparameterisation noise, :205): None draws ``torch.randn(B, Z)`` from the global
+        CPU generator — the stream the reference's CPU run consumes (Training_VAE.py:282 runs on
+        'cpu'), so a seeded loop replays it; a (B, Z) tensor is used as given; "philox" draws it
+        in-kernel (Philox at the engine's next offset)."""
+        eng = _need(self)
+        B = x.shape[0]
+        offset = 0
+        if eps is None:
+            eps = torch.randn(B, self.latent_dim)
+        if isinstance(eps, str):
+            if eps != "philox":
+                raise ValueError("eps must be None, a (B, Z) tensor or 'philox'")
+            eps, offset = None, eng.rng_offset
+            eng.rng_offset = offset + 1
+        else:
+            eps = torch.as_tensor(eps).to(device=eng.device, dtype=torch.float32).contiguous()
+        x = eng.as_input(x, keep_f32=True).detach()
+        start = torch.as_tensor(start_points).to(device=eng.device, dtype=torch.float32).contiguous().detach()
+        return _ForwardFn.apply(eng, x, start, eps, offset, *self.parameters())
 
     def generate(self, start_points, z=None, generator=None):
         """Batched sampling (Tools.py:18-65): z ~ N(0,I); returns (relative, absolute) trajectories."""
@@ -121,20 +205,14 @@ class ConditionalTrajectoryVAE(nn.Module):
 
 def conditional_vae_loss(recon_x, x, mu, logvar, condition=None, recon_weight=0.1, kld_weight=0.1,
                          start_weight=1.0, time_weight=0.5):
-    """Training_VAE.py:229-268 (5-tuple, same defaults).  HIP kernel; device tensors only."""
+    """Training_VAE.py:229-268 (5-tuple, same defaults), differentiable: the HIP kernels cvae_loss
+    (forward) and cvae_loss_backward (autograd).  Device tensors only."""
     if not recon_x.is_cuda:
         raise RuntimeError("conditional_vae_loss runs on the HIP device (cvae_loss); got a CPU tensor")
-    B, S, D = recon_x.shape
-    Z = mu.shape[1]
     dev = recon_x.device
-    f = lambda t: t.detach().to(device=dev, dtype=torch.float32).contiguous()  # noqa: E731
-    r, xx, m, lv = f(recon_x), f(x), f(mu), f(logvar)
-    out = torch.empty(5, device=dev, dtype=torch.float32)
-    ws = torch.empty(8 * ((B + 31) // 32), device=dev, dtype=torch.float32)
-    w = CvaeLossWeights(recon_weight, kld_weight, start_weight, time_weight)
-    with torch.cuda.device(dev):
-        check(lib().cvae_loss(ptr(r), ptr(xx), ptr(m), ptr(lv), B, S, D, Z, C.byref(w), ptr(out), ptr(ws),
-                              C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "cvae_loss")
+    f = lambda t: t.to(device=dev, dtype=torch.float32).contiguous()  # noqa: E731
+    w = (float(recon_weight), float(kld_weight), float(start_weight), float(time_weight))
+    out = _LossFn.apply(f(recon_x), f(x).detach(), f(mu), f(logvar), w)
     return tuple(out[i] for i in range(5))
 
 

@@ -14,7 +14,13 @@ RNG: ``torch.utils.data.DataLoader(shuffle=True)`` over row indices consumes the
 generator exactly as the reference's loader does.  ``eps="host"`` draws each step's
 ``randn(B, Z)`` from that same generator (the reference's ``randn_like`` at :205 on CPU), so a
 seeded run replays the reference's stream; ``eps="philox"`` generates eps in-kernel instead
-(Philox4x32-10, keyed by the engine seed and step) and is the throughput mode.
+(Philox4x32-10, keyed by the engine seed, the device step counter and the GLOBAL row: under data
+parallelism each rank passes its first row, so the global batch draws what one process would)
+and is the throughput mode.
+
+Precision: the dataset stays fp32 on the device whatever the operand dtype; the kernels subtract
+the start point in fp32 and round the RELATIVE coordinates once (Training_VAE.py:345-348), so a
+bf16 run on real data (absolute coordinates of ~200 m) does not quantise its offsets to ~1 m.
 
 Outputs (Training_VAE.py:373-394, Tools.py:747-771): one line per epoch in the reference
 format; ``loss_history`` (per-epoch means) and its weighted copy; the loss CSV (header = the
@@ -85,14 +91,15 @@ def cpu_state_dict(model):
 
 def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidden_dim=128,
           weights=(0.1, 0.1, 1.0, 1.0), model_save_path=None, loss_save_path=None, dtype="fp32",
-          eps="host", device=None, seed=None, engine_seed=0, log=print, model=None):
+          eps="host", device=None, seed=None, engine_seed=0, log=print, model=None, buckets=1):
     """Train like ``python Training_VAE.py`` (mode='training').
 
     data: path to the (N, seq_len, dim) ``.npy`` (TrajectoryDataset, :105-115) or an array.
     weights: (recon, kld, start, time) — the values of :300-306.
     seed: if given, ``torch.manual_seed(seed)`` first (the reference leaves it unseeded).
     Under ``torch.distributed`` every rank runs this with the same arguments; batch_size is
-    then per rank (global batch = batch_size · world) and rank 0 logs and saves.
+    then per rank (global batch = batch_size · world) and rank 0 logs and saves; ``buckets=2``
+    overlaps the decoder gradients' all-reduce with the rest of the dW GEMMs.
 
     Returns (model, loss_history, weighted_loss_history).
     """
@@ -115,9 +122,10 @@ def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidd
         raise ValueError(f"engine max_batch {eng.max_batch} < batch_size {batch_size}")
     eng.set_optimizer(lr=lr)
     eng.weights = tuple(float(w) for w in weights)
-    step = dp.DataParallelStep(eng)
+    eng.keep_f32 = True                                   # relative transform in fp32 (see above)
+    step = dp.DataParallelStep(eng, buckets=buckets)
     step.broadcast_params()
-    x_dev = eng.as_input(torch.from_numpy(arr))          # resident for the whole run
+    x_dev = eng.as_input(torch.from_numpy(arr), keep_f32=True)  # resident for the whole run
     Z = latent_dim
     gb = batch_size * world_size
     loader = torch.utils.data.DataLoader(_Rows(n), batch_size=gb, shuffle=True)
@@ -133,7 +141,7 @@ def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidd
                 e = e_all[lo:hi]
             elif eps != "philox":
                 raise ValueError("eps must be 'host' or 'philox'")
-            step.step(x_dev, idx=rows[lo:hi], eps=e, batch=hi - lo, global_batch=g)
+            step.step(x_dev, idx=rows[lo:hi], eps=e, batch=hi - lo, global_batch=g, row0=lo)
         sums = step.epoch_loss_sums().double().cpu().numpy()  # the only host sync of the epoch
         means = sums / n
         for k, v in zip(LOSS_KEYS, means):
@@ -181,7 +189,8 @@ def main(argv=None):
     ap.add_argument("--epochs", type=int, default=3000)
     ap.add_argument("--weights", type=float, nargs=4, default=(0.1, 0.1, 1.0, 1.0),
                     metavar=("RECON", "KLD", "START", "TIME"))
-    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="GEMM operand dtype; the dataset stays fp32 and the relative transform runs in fp32")
     ap.add_argument("--eps", default="host", choices=["host", "philox"])
     ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--model-out", default=None)

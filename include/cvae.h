@@ -14,7 +14,15 @@
  * never aborts.  cvae_last_error() returns a thread-local message.
  * Threading: one handle per device per process; a handle is not thread-safe.
  * No call synchronises the device: all work is queued on `stream`, so every
- * call is capturable into a hipGraph.
+ * call is capturable into a hipGraph.  With device step counters (below) a
+ * captured training step can be REPLAYED: nothing in it is a host value that
+ * changes from step to step.
+ *
+ * ABI 2 (round 2): Adam hyper-parameters are doubles (torch computes its step
+ * size and bias corrections in Python doubles, torch/optim/adam.py), loss
+ * accumulators are fp64 (the reference sums loss.item()*B in Python doubles,
+ * Training_VAE.py:366-370), eps rows are keyed by a global row offset, and the
+ * training calls take optional device step counters.
  */
 #ifndef CVAE_H
 #define CVAE_H
@@ -26,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CVAE_ABI_VERSION 1
+#define CVAE_ABI_VERSION 2
 
 enum cvae_dtype {
   CVAE_F32 = 0,
@@ -40,6 +48,23 @@ enum cvae_status {
   CVAE_E_HIP = -2,       /* a HIP runtime call failed (message has details) */
   CVAE_E_CAPACITY = -3,  /* batch larger than cfg.max_batch                  */
   CVAE_E_NOMEM = -4
+};
+
+/* Input flags (the `xflags` argument of the calls that read trajectories). */
+enum cvae_xflags {
+  CVAE_X_OPERAND = 0,  /* x is in the operand dtype (fp32 / bf16)                                   */
+  CVAE_X_F32 = 1       /* x is fp32 whatever the operand dtype: the relative transform
+                          (Training_VAE.py:345-348) runs in fp32 and rounds once — real data with
+                          absolute coordinates of ~200 m stays exact in the relative frame       */
+};
+
+/* fwd/bwd parts (cvae_train_fwd_bwd `parts`): a data-parallel caller can split the weight-gradient
+ * launch in two buckets and all-reduce the decoder bucket while the rest is computed. */
+enum cvae_parts {
+  CVAE_PART_CHAIN = 1,    /* forward + loss + every dX (the row chain)                         */
+  CVAE_PART_DW_DEC = 2,   /* dW/db of the decoder layers (a contiguous tail of the flat buffer)  */
+  CVAE_PART_DW_REST = 4,  /* dW/db of condition encoder, encoder, fc_mu, fc_logvar               */
+  CVAE_PART_ALL = 7
 };
 
 /* Model shape.  Training_VAE.py:124 ConditionalTrajectoryVAE(seq_len, dim,
@@ -63,6 +88,20 @@ typedef struct cvae_loss_weights {
   float recon, kld, start, time;
 } cvae_loss_weights;
 
+/* torch.optim.Adam(lr, betas=(beta1, beta2), eps) hyper-parameters, as the Python doubles torch
+ * computes with (amsgrad=False, weight_decay=0). */
+typedef struct cvae_adam_config {
+  double lr, beta1, beta2, eps;
+} cvae_adam_config;
+
+/* Device step counters (caller-owned device memory, 2 x uint64):
+ *   counters[0] = Philox offset of the next training step's eps draw,
+ *   counters[1] = optimizer steps begun.
+ * A training call given counters reads them ON THE DEVICE and advances them: the row chain adds 1
+ * to counters[1] (the step it begins; Adam uses t = counters[1]) and the dW launch adds 1 to
+ * counters[0].  The `offset` / `step` arguments are then ignored.  With counters == NULL the host
+ * values are used. */
+
 /* Create/destroy.  Replaces ConditionalTrajectoryVAE.__init__ (Training_VAE.py:124-167)
  * for the device side; parameters themselves live in the caller's flat fp32 buffer. */
 int cvae_create(const cvae_config* cfg, int device, cvae_handle** out);
@@ -82,27 +121,34 @@ int cvae_config_info(const cvae_config* cfg, int64_t* total_params, int* n_tenso
 /* Workspace bytes the handle allocated (informational). */
 int cvae_workspace_bytes(const cvae_handle* h, int64_t* bytes);
 
+/* First flat index of the decoder's parameters (decoder.0.weight): the CVAE_PART_DW_DEC bucket is
+ * [split, total), CVAE_PART_DW_REST is [0, split). */
+int cvae_bucket_split(const cvae_handle* h, int64_t* split);
+
 /* Rebuild the device copies of the weights (padded operand-dtype W and Wᵀ,
  * padded fp32 biases) from the flat fp32 master `params`.  Call after the
- * caller writes parameters (init, load_state_dict).  cvae_adam/cvae_train_step
- * keep the copies current themselves. */
+ * caller writes parameters (init, load_state_dict, an optimizer outside this
+ * library).  cvae_adam/cvae_train_step keep the copies current themselves. */
 int cvae_pack_weights(cvae_handle* h, const float* params, void* stream);
 
 /* Inference: encode → reparameterise → decode.  Replaces
  * ConditionalTrajectoryVAE.forward (Training_VAE.py:217-226).
- *   x      (N_total,S,D) trajectories, operand dtype, row-major.  With
- *          start == NULL x holds ABSOLUTE coordinates and the relative
+ *   x      (N_total,S,D) trajectories, operand dtype (or fp32 with CVAE_X_F32), row-major.
+ *          With start == NULL x holds ABSOLUTE coordinates and the relative
  *          transform of :345-348 is applied in-kernel (condition = x[:,0,1:3]);
  *          with start != NULL x is used as given (already relative, as
  *          model(batch_rel, start_points) at :352) and start fp32 (batch,2) is
  *          the condition.
  *   idx    optional int64[batch] row gather into x (NULL = rows 0..batch-1)
- *   eps    optional fp32 (batch,Z); NULL = in-kernel Philox(seed, offset)
+ *   eps    optional fp32 (batch,Z); NULL = in-kernel Philox(seed, offset) keyed by the global
+ *          row eps_row0 + b (a data-parallel rank passes its first global row, so the ranks of
+ *          a global batch draw what one process with that batch draws)
  *   recon  fp32 (batch,S,D) relative trajectories; mu, logvar fp32 (batch,Z);
- *   hc     fp32 (batch,H) condition features (any output may be NULL).      */
-int cvae_forward(cvae_handle* h, const void* x, const int64_t* idx, int batch,
-                 const float* start, const float* eps, uint64_t seed, uint64_t offset,
-                 float* recon, float* mu, float* logvar, float* hc, void* stream);
+ *   hc     fp32 (batch,H) condition features; eps_out fp32 (batch,Z) the eps each row used
+ *          (any output may be NULL).                                                           */
+int cvae_forward(cvae_handle* h, const void* x, const int64_t* idx, int batch, int xflags,
+                 const float* start, const float* eps, uint64_t seed, uint64_t offset, int64_t eps_row0,
+                 float* recon, float* mu, float* logvar, float* hc, float* eps_out, void* stream);
 
 /* Condition encoder only: h_c = condition_encoder(start)
  * (Training_VAE.py:132-137, called at :190 and Tools.py:55).
@@ -122,44 +168,56 @@ int cvae_decode(cvae_handle* h, const float* z, const float* start, const float*
  * the flat fp32 `grads` (overwritten, same layout as params).  Replaces
  * Training_VAE.py:351-362 (zero_grad, model(), conditional_vae_loss(),
  * loss.backward()).  `loss_out` fp32[5] = (total, recon, kld, start, time) as
- * returned by conditional_vae_loss (:268); `loss_accum` (nullable) fp32[5]
- * += loss * batch (the per-epoch accumulators of :366-370, kept on device).
+ * returned by conditional_vae_loss (:268); `loss_accum` (nullable) fp64[5]
+ * += (double)loss * batch (the per-epoch accumulators of :366-370, kept on device).
  * Means are over this call's batch, so a data-parallel caller all-reduces
- * `grads` and passes grad_scale = 1/world to cvae_adam. */
-int cvae_train_fwd_bwd(cvae_handle* h, const void* x, const int64_t* idx, int batch,
-                       const float* eps, uint64_t seed, uint64_t offset,
-                       const cvae_loss_weights* w, float* grads,
-                       float* loss_out, float* loss_accum, void* stream);
+ * `grads` and passes grad_scale = 1/world to cvae_adam.
+ * parts: CVAE_PART_ALL, or CVAE_PART_CHAIN|CVAE_PART_DW_DEC followed by a CVAE_PART_DW_REST call
+ * on the same batch (the two-bucket overlap; loss and counters advance in the first call). */
+int cvae_train_fwd_bwd(cvae_handle* h, const void* x, const int64_t* idx, int batch, int xflags,
+                       const float* eps, uint64_t seed, uint64_t offset, int64_t eps_row0,
+                       const cvae_loss_weights* w, float* grads, float* loss_out, double* loss_accum,
+                       uint64_t* counters, int parts, void* stream);
+
+/* Backward of model.forward from caller-supplied output gradients (the autograd path: the
+ * reference loop's loss.backward(), Training_VAE.py:362, when conditional_vae_loss and the
+ * model are separate autograd nodes).  Recomputes the forward of (x relative, start, eps or
+ * Philox(seed, offset, eps_row0)) — bit-identical to the cvae_forward that produced the
+ * outputs — and back-propagates d_recon fp32 (batch,S,D), d_mu / d_logvar fp32 (batch,Z) and
+ * d_hc fp32 (batch,H) (any may be NULL = zero) into the flat fp32 `grads` (overwritten). */
+int cvae_backward(cvae_handle* h, const void* x, const int64_t* idx, int batch, int xflags,
+                  const float* start, const float* eps, uint64_t seed, uint64_t offset, int64_t eps_row0,
+                  const float* d_recon, const float* d_mu, const float* d_logvar, const float* d_hc,
+                  float* grads, void* stream);
 
 /* torch.optim.Adam step (amsgrad=False, weight_decay=0) over the flat buffers
  * — replaces optimizer.step() (Training_VAE.py:363; torch/optim/adam.py
- * _single_tensor_adam).  step is the 1-based step count after increment.
+ * _single_tensor_adam).  step is the 1-based step count after increment (or t = counters[1]).
  * g_eff = grads * grad_scale.  Also refreshes the device weight copies. */
-int cvae_adam(cvae_handle* h, float* params, const float* grads, float* m, float* v,
-              int step, float lr, float beta1, float beta2, float eps, float grad_scale,
-              void* stream);
+int cvae_adam(cvae_handle* h, float* params, const float* grads, float* m, float* v, int64_t step,
+              const cvae_adam_config* adam, float grad_scale, const uint64_t* counters, void* stream);
 
 /* Fused single-device step: cvae_train_fwd_bwd + cvae_adam with the weight
  * gradient GEMMs and Adam in one kernel (the gradient never round-trips HBM).
  * Replaces the whole body of Training_VAE.py:345-370 for one batch. */
-int cvae_train_step(cvae_handle* h, const void* x, const int64_t* idx, int batch,
-                    const float* eps, uint64_t seed, uint64_t offset,
-                    const cvae_loss_weights* w,
-                    float* params, float* m, float* v, int step,
-                    float lr, float beta1, float beta2, float adam_eps,
-                    float* loss_out, float* loss_accum, void* stream);
+int cvae_train_step(cvae_handle* h, const void* x, const int64_t* idx, int batch, int xflags,
+                    const float* eps, uint64_t seed, uint64_t offset, int64_t eps_row0,
+                    const cvae_loss_weights* w, float* params, float* m, float* v, int64_t step,
+                    const cvae_adam_config* adam, float* loss_out, double* loss_accum,
+                    uint64_t* counters, void* stream);
 
 /* n_steps consecutive fused steps (cvae_train_step) enqueued by one call: step i uses the rows
  * idx[i*batch .. (i+1)*batch) of x (idx == NULL: rows 0..batch-1 every step), eps rows
- * eps[i*batch ..] (NULL: Philox(seed, offset + i)) and Adam step step0 + i.  Replaces the inner
- * `for batch in dataloader` loop of Training_VAE.py:340-370 for a run of equal-size batches
- * (an epoch's permutation uploaded once); loss_out = the last step's losses, loss_accum += every
- * step's loss * batch.  No host work per step beyond the two kernel launches. */
-int cvae_train_steps(cvae_handle* h, const void* x, const int64_t* idx, int batch, int n_steps,
-                     const float* eps, uint64_t seed, uint64_t offset, const cvae_loss_weights* w,
-                     float* params, float* m, float* v, int step0,
-                     float lr, float beta1, float beta2, float adam_eps,
-                     float* loss_out, float* loss_accum, void* stream);
+ * eps[i*batch ..] (NULL: Philox(seed, offset + i)) and Adam step step0 + i (with counters: the
+ * device counters, advanced per step).  Replaces the inner `for batch in dataloader` loop of
+ * Training_VAE.py:340-370 for a run of equal-size batches (an epoch's permutation uploaded
+ * once); loss_out = the last step's losses, loss_accum += every step's loss * batch.  No host
+ * work per step beyond the two kernel launches. */
+int cvae_train_steps(cvae_handle* h, const void* x, const int64_t* idx, int batch, int n_steps, int xflags,
+                     const float* eps, uint64_t seed, uint64_t offset, int64_t eps_row0,
+                     const cvae_loss_weights* w, float* params, float* m, float* v, int64_t step0,
+                     const cvae_adam_config* adam, float* loss_out, double* loss_accum,
+                     uint64_t* counters, void* stream);
 
 /* Standalone conditional_vae_loss (Training_VAE.py:229-268), forward only, for
  * callers holding (recon, x, mu, logvar) fp32 device tensors; x is the RELATIVE
@@ -169,6 +227,13 @@ int cvae_train_steps(cvae_handle* h, const void* x, const int64_t* idx, int batc
 int cvae_loss(const float* recon, const float* x, const float* mu, const float* logvar,
               int batch, int seq_len, int dim, int latent_dim, const cvae_loss_weights* w,
               float* loss_out, float* workspace, void* stream);
+
+/* Backward of cvae_loss (autograd of Training_VAE.py:240-267): given the upstream
+ * gradients g_out fp32[5] of (total, recon, kld, start, time) on the device, writes
+ * d_recon fp32 (batch,S,D), d_mu and d_logvar fp32 (batch,Z) (overwritten).  Handle-free. */
+int cvae_loss_backward(const float* recon, const float* x, const float* mu, const float* logvar,
+                       int batch, int seq_len, int dim, int latent_dim, const cvae_loss_weights* w,
+                       const float* g_out, float* d_recon, float* d_mu, float* d_logvar, void* stream);
 
 /* Per-kernel device time, measured with HIP events recorded on `stream`
  * around every kernel of every call made while timing is enabled (no
@@ -186,12 +251,20 @@ int cvae_kernel_times(cvae_handle* h, char* names, int names_len, float* ms, int
  * `stream`; SYNCHRONISES the stream (measurement only).  The row-chain and step runs update
  * params/m/v like training steps (step numbers step0..). */
 int cvae_bench_kernels(cvae_handle* h, const void* x, const int64_t* idx, int batch, int reps,
-                       float* params, float* m, float* v, int step0, float* ms, void* stream);
+                       float* params, float* m, float* v, int64_t step0, float* ms, void* stream);
 
 /* The five hand-off words of the fused training launch (three group counters, finished tiles, spin
- * time-out flag), copied to `out` (host, 5 entries).  All zero between launches; a non-zero time-out
- * flag means a tile gave up waiting (results of that step invalid).  Synchronises the device. */
+ * time-out flag), copied to `out` (host, 5 entries).  The counters are zeroed before every fused
+ * launch; a non-zero time-out flag means a tile gave up waiting and skipped its update (that
+ * step's parameters are incomplete: the caller must treat the step as failed).  Synchronises
+ * the device. */
 int cvae_sync_words(cvae_handle* h, unsigned* out);
+
+/* Adam's per-step scalars as the device computes them from a step counter (t = 1..n): writes
+ * out[2*(t-1)] = -lr/(1-beta1^t) and out[2*(t-1)+1] = sqrt(1-beta2^t), both rounded to fp32 —
+ * the values torch's CPU Adam forms in Python doubles.  Check/diagnostic entry point for the
+ * device-counter path (the host path computes them on the host). */
+int cvae_adam_scalars(const cvae_adam_config* adam, int64_t n, float* out, void* stream);
 
 const char* cvae_last_error(void);
 int cvae_abi_version(void);

@@ -23,7 +23,8 @@ class OracleEngine:
         self.m = torch.zeros(n)
         self.v = torch.zeros(n)
         self.loss = torch.zeros(5)
-        self.loss_accum = torch.zeros(5)
+        self.loss_accum = torch.zeros(5, dtype=torch.float64)
+        self.bucket_split = sum(p.numel() for p in self.plist[:-2 * 4])  # decoder.* = the last 8 tensors
         self.step_count = 0
         self.lr, self.betas, self.eps = 1e-3, (0.9, 0.999), 1e-8
         self.weights = DEFAULT_WEIGHTS
@@ -33,7 +34,9 @@ class OracleEngine:
     def set_optimizer(self, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
         self.lr, self.betas, self.eps = lr, betas, eps
 
-    def as_input(self, x):
+    keep_f32 = True
+
+    def as_input(self, x, keep_f32=False):
         return torch.as_tensor(x, dtype=torch.float32).contiguous()
 
     def pack(self):
@@ -43,8 +46,8 @@ class OracleEngine:
                 p.copy_(self.params[o:o + p.numel()].view_as(p))
                 o += p.numel()
 
-    def forward_backward(self, x, idx=None, eps=None, batch=None, weights=None, accumulate=True):
-        self.calls.append(("fb", None if idx is None else idx.clone(), batch))
+    def forward_backward(self, x, idx=None, eps=None, batch=None, weights=None, accumulate=True, row0=0, parts=7):
+        self.calls.append(("fb", None if idx is None else idx.clone(), batch, row0, parts))
         rows = x[idx] if idx is not None else x[:batch]
         rel, start = relative(rows)
         for p in self.plist:
@@ -56,9 +59,12 @@ class OracleEngine:
         ls[0].backward()
         self.grads.copy_(torch.cat([p.grad.reshape(-1) for p in self.plist]))
         self.loss.copy_(torch.stack([v.detach() for v in ls]))
-        if accumulate:
-            self.loss_accum += self.loss * float(rows.shape[0])
+        if accumulate:  # the reference's loss.item() * B in Python doubles
+            self.loss_accum += self.loss.double() * float(rows.shape[0])
         return self.loss
+
+    def wgrad_rest(self, batch=None):
+        self.calls.append(("rest", None, batch, None, 4))
 
     def adam_step(self, grad_scale=1.0):
         self.step_count += 1
@@ -72,7 +78,7 @@ class OracleEngine:
         self.params.addcdiv_(self.m, denom, value=-(self.lr / bc1))
         self.pack()
 
-    def train_step(self, x, idx=None, eps=None, batch=None, weights=None, accumulate=True):
+    def train_step(self, x, idx=None, eps=None, batch=None, weights=None, accumulate=True, row0=0):
         self.forward_backward(x, idx=idx, eps=eps, batch=batch, weights=weights, accumulate=accumulate)
         self.adam_step()
         return self.loss

@@ -23,7 +23,8 @@ def test_library_exports_every_header_symbol(cl):
     L = cl.lib()
     for n in names:
         assert hasattr(L, n), n
-    assert L.cvae_abi_version() == 1
+    assert L.cvae_abi_version() == 2
+    assert cl.missing_signatures(os.path.join(ROOT, "include", "cvae.h")) == []  # ctypes covers the whole ABI
 
 
 @pytest.mark.parametrize("S,D,Z,H,dtype", [(10, 3, 8, 128, "fp32"), (100, 6, 8, 128, "bf16"),
