@@ -146,6 +146,11 @@ def cpu_baseline(B, S, D, Z, H, seconds, n_enc=4, n_dec=4, data=None):
 
 
 def main():
+    # ONE JSON line on stdout: native libraries (RCCL's version banner) write to fd 1 directly, so
+    # fd 1 becomes stderr for the whole run and the result goes to a duplicate of the original stdout
+    out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -330,7 +335,7 @@ def main():
             res["cpu_baseline"] = cpu_baseline(B, S, D, Z, H, args.cpu_seconds, NE, ND,
                                                data=data_cpu if wl == "cfg1" else None)
             res["speedup_vs_cpu"] = round(value / res["cpu_baseline"]["value"], 1)
-        print(json.dumps(res), flush=True)
+        print(json.dumps(res), file=out, flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
 

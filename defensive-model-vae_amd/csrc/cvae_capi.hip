@@ -583,6 +583,7 @@ struct CallX {
   int64_t eps_row0;
   const cvae_loss_weights* w;
   uint64_t* ctr;
+  const cvae_adam_config* adam;  // with ctr: the chain precomputes the step's Adam scalars
 };
 
 RowArgs row_args(cvae_handle* h, const CallX& c) {
@@ -591,6 +592,10 @@ RowArgs row_args(cvae_handle* h, const CallX& c) {
   ra.eps_row0 = c.eps_row0;
   ra.x_f32 = (c.xflags & CVAE_X_F32) && is16(h) ? 1 : 0;
   ra.ctr = c.ctr;
+  if (c.ctr && c.adam) {
+    ra.adam_pre = 1;
+    ra.lr = c.adam->lr; ra.beta1 = c.adam->beta1; ra.beta2 = c.adam->beta2;
+  }
   ra.w_recon = c.w ? c.w->recon : 0.1f; ra.w_kld = c.w ? c.w->kld : 0.1f;
   ra.w_start = c.w ? c.w->start : 1.0f; ra.w_time = c.w ? c.w->time : 1.0f;
   ra.partials = h->d_partials;
@@ -660,7 +665,9 @@ int launch_wgrad(cvae_handle* h, int batch, const AdamArgs& aa, const LossArgs& 
 // device counters, fused launch: its chain blocks do not bump the step (its dW tiles read it in the
 // same launch), so the step begins with this one-lane kernel; the loss tile advances the offset
 // after every chain block has published (read) it
-__global__ void counter_bump_kernel(uint64_t* c) { c[0] = c[0] + 1; }
+__global__ void counter_bump_kernel(uint64_t* c, double lr, double b1, double b2) {
+  adam_precompute(c, lr, b1, b2, true);
+}
 
 // one training step as a single fused_step_kernel launch (fast configuration, 16-B aligned x)
 int launch_fused(cvae_handle* h, RowArgs ra, const AdamArgs& aa, float* loss_out, double* loss_accum,
@@ -676,7 +683,7 @@ int launch_fused(cvae_handle* h, RowArgs ra, const AdamArgs& aa, float* loss_out
   // the group counters start every launch at zero (stream-ordered; the sticky time-out flag stays)
   HIPCK(hipMemsetAsync(h->d_sync, 0, 4 * sizeof(unsigned), s));
   if (ra.ctr) {
-    hipLaunchKernelGGL(counter_bump_kernel, dim3(1), dim3(1), 0, s, ra.ctr + 1);
+    hipLaunchKernelGGL(counter_bump_kernel, dim3(1), dim3(1), 0, s, ra.ctr, ra.lr, ra.beta1, ra.beta2);
     HIPCK(hipGetLastError());
   }
   int rc = tmark(h, s, "fused_step");
@@ -718,7 +725,9 @@ int train_step_impl(cvae_handle* h, const CallX& c, float* params, float* m, flo
                     const cvae_adam_config* adam, float* loss_out, double* loss_accum, hipStream_t s) {
   tbegin(h);
   AdamArgs aa = make_adam(params, nullptr, m, v, step, *adam, 1.f, c.ctr);
-  const RowArgs ra = row_args(h, c);
+  CallX ca = c;
+  ca.adam = adam;
+  const RowArgs ra = row_args(h, ca);
   if (use_fused(h, ra)) return launch_fused(h, ra, aa, loss_out, loss_accum, s);
   int rc = is16(h) ? launch_train_chain<__bf16>(h, ra, s) : launch_train_chain<float>(h, ra, s);
   if (rc) return rc;
@@ -825,7 +834,7 @@ int cvae_forward(cvae_handle* h, const void* x, const int64_t* idx, int batch, i
   if (!h || !x) return fail(CVAE_E_INVALID, "null argument");
   int rc = check_batch(h, batch);
   if (rc) return rc;
-  RowArgs a = row_args(h, CallX{x, idx, batch, xflags, eps, seed, offset, eps_row0, nullptr, nullptr});
+  RowArgs a = row_args(h, CallX{x, idx, batch, xflags, eps, seed, offset, eps_row0, nullptr, nullptr, nullptr});
   a.start_in = start; a.x_relative = start ? 1 : 0;
   a.recon_out = recon; a.mu_out = mu; a.lv_out = logvar; a.hc_out = hc; a.eps_out = eps_out;
   hipStream_t s = (hipStream_t)stream;
@@ -859,14 +868,16 @@ int cvae_decode(cvae_handle* h, const float* z, const float* start, const float*
 
 int cvae_train_fwd_bwd(cvae_handle* h, const void* x, const int64_t* idx, int batch, int xflags, const float* eps,
                        uint64_t seed, uint64_t offset, int64_t eps_row0, const cvae_loss_weights* w, float* grads,
-                       float* loss_out, double* loss_accum, uint64_t* counters, int parts, void* stream) {
+                       float* loss_out, double* loss_accum, uint64_t* counters, const cvae_adam_config* adam,
+                       int parts, void* stream) {
   if (!h || !grads || ((parts & CVAE_PART_CHAIN) && !x)) return fail(CVAE_E_INVALID, "null argument");
   if (parts != CVAE_PART_ALL && parts != (CVAE_PART_CHAIN | CVAE_PART_DW_DEC) && parts != CVAE_PART_DW_REST)
     return fail(CVAE_E_INVALID, "parts must be CVAE_PART_ALL, CHAIN|DW_DEC, or DW_REST");
   int rc = check_batch(h, batch);
   if (rc) return rc;
-  return fwd_bwd_impl(h, CallX{x, idx, batch, xflags, eps, seed, offset, eps_row0, w, counters}, grads, loss_out,
-                      loss_accum, parts, (hipStream_t)stream);
+  if (adam && (rc = check_adam(adam))) return rc;
+  return fwd_bwd_impl(h, CallX{x, idx, batch, xflags, eps, seed, offset, eps_row0, w, counters, adam}, grads,
+                      loss_out, loss_accum, parts, (hipStream_t)stream);
 }
 
 int cvae_backward(cvae_handle* h, const void* x, const int64_t* idx, int batch, int xflags, const float* start,
@@ -877,7 +888,7 @@ int cvae_backward(cvae_handle* h, const void* x, const int64_t* idx, int batch, 
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   tbegin(h);
-  RowArgs ra = row_args(h, CallX{x, idx, batch, xflags, eps, seed, offset, eps_row0, nullptr, nullptr});
+  RowArgs ra = row_args(h, CallX{x, idx, batch, xflags, eps, seed, offset, eps_row0, nullptr, nullptr, nullptr});
   ra.start_in = start; ra.x_relative = start ? 1 : 0;
   ra.ext = 1;
   ra.d_recon = d_recon; ra.d_mu = d_mu; ra.d_lv = d_logvar; ra.d_hc = d_hc;
@@ -916,7 +927,7 @@ int cvae_train_step(cvae_handle* h, const void* x, const int64_t* idx, int batch
   int rc = check_batch(h, batch);
   if (!rc) rc = check_adam(adam);
   if (rc) return rc;
-  return train_step_impl(h, CallX{x, idx, batch, xflags, eps, seed, offset, eps_row0, w, counters}, params, m, v,
+  return train_step_impl(h, CallX{x, idx, batch, xflags, eps, seed, offset, eps_row0, w, counters, adam}, params, m, v,
                          step, adam, loss_out, loss_accum, (hipStream_t)stream);
 }
 
@@ -954,7 +965,7 @@ int cvae_bench_kernels(cvae_handle* h, const void* x, const int64_t* idx, int ba
     HIPCK(hipEventRecord(e0, s));
     for (int r = 0; r < reps; ++r) {
       int rc2 = CVAE_OK;
-      const CallX c{x, idx, batch, 0, nullptr, 1, (uint64_t)r, 0, &w, nullptr};
+      const CallX c{x, idx, batch, 0, nullptr, 1, (uint64_t)r, 0, &w, nullptr, nullptr};
       if (which == 0) {
         rc2 = is16(h) ? launch_train_chain<__bf16>(h, row_args(h, c), s) : launch_train_chain<float>(h, row_args(h, c), s);
       } else if (which == 1) {

@@ -177,6 +177,29 @@ __device__ __forceinline__ V gld(const void* p) { return *(const CVAE_GLOBAL V*)
 template <typename V>
 __device__ __forceinline__ void gst(void* p, V v) { *(CVAE_GLOBAL V*)p = v; }
 
+// ------------------------------------------------------------------ Adam step scalars (device step counters)
+// torch's two per-step Adam scalars from the step count t, in doubles as Python forms them
+// (torch/optim/adam.py: bias_correction1 = 1 - beta1 ** step, step_size = lr / bias_correction1,
+// bias_correction2_sqrt = bias_correction2 ** 0.5), rounded to fp32 where the tensor op takes them
+__device__ __forceinline__ void adam_scalars(double lr, double b1, double b2, double t, float& lr_neg_step,
+                                             float& bc2_sqrt) {
+  const double bc1 = 1.0 - pow(b1, t);
+  const double bc2 = 1.0 - pow(b2, t);
+  lr_neg_step = (float)(-(lr / bc1));
+  bc2_sqrt = (float)sqrt(bc2);
+}
+typedef float adam_f32x2 __attribute__((ext_vector_type(2)));
+// one lane, at the start of a training step: ctr[1] += 1 and the scalars of that step into ctr[2]
+__device__ __forceinline__ void adam_precompute(uint64_t* ctr, double lr, double b1, double b2, bool scalars) {
+  const uint64_t t = ctr[1] + 1;
+  ctr[1] = t;
+  if (scalars) {
+    float a, b;
+    adam_scalars(lr, b1, b2, (double)t, a, b);
+    *(adam_f32x2*)(ctr + 2) = adam_f32x2{a, b};
+  }
+}
+
 // ------------------------------------------------------------------ Philox4x32-10
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
 #pragma unroll

@@ -319,6 +319,10 @@ __device__ __forceinline__ void chain_body(const FastNet& net, const RowArgs& a,
     // the weights of the first step queue behind the x tile and the biases (vmcnt retires in order)
     wload(wC0, Wf(LC0), LY::Kp(LC0), wave);
     wload_part<0, NKI / 2>(wE0, Wf(LE0), Ip, wave);
+    // device counters: this launch begins optimizer step ctr[1] + 1 and precomputes its Adam scalars
+    // (the dW kernel behind it reads them); one lane of block 0, while its wave waits for the x tile.
+    // The fused launch (pub) does this in a kernel before it: its dW tiles run beside the chain.
+    if (a.ctr && blk == 0 && tid == 0 && !pub) adam_precompute(a.ctr, a.lr, a.beta1, a.beta2, a.adam_pre);
     stamp();
     // eps: 8 latents × 16 rows, 4 per thread (host-given, or Philox as philox_normal), on the last
     // wave: it has one x-tile task fewer than waves 0-2
@@ -734,8 +738,6 @@ __device__ __forceinline__ void chain_body(const FastNet& net, const RowArgs& a,
     lbar();
     if (tid == 0) __hip_atomic_fetch_add(pub + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  // device counters: this launch begins optimizer step ctr[1] + 1 (the Adam kernel behind it reads it)
-  if (a.ctr && blk == 0 && tid == 0 && !pub) a.ctr[1] = a.ctr[1] + 1;
   if (CVAE_DIAG_STAMPS && a.stamps && tid < 64) {
     stamp();
     gst<unsigned long long>(a.stamps + blk * 64 + tid, tid < stamp_i ? STAMPS[tid] : 0ull);

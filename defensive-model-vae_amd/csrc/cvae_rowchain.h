@@ -182,7 +182,9 @@ struct RowArgs {
   int x_relative;         // 1: x is relative, condition = start_in (no transform)
   int x_f32;              // 1: x is fp32 whatever T (relative transform in fp32, one rounding)
   int64_t eps_row0;       // Philox rows are keyed by the GLOBAL row eps_row0 + b (data parallelism)
-  uint64_t* ctr;          // device step counters (cvae.h): offset = ctr[0]; block 0 adds 1 to ctr[1]
+  uint64_t* ctr;          // device step counters (cvae.h): offset = ctr[0]; block 0 begins step ctr[1] + 1
+  int adam_pre;           // ... and precomputes that step's Adam scalars into ctr[2] (lr, betas below)
+  double lr, beta1, beta2;
   float* eps_out;         // FWD: the eps each row used (fp32 (batch, Z), nullable)
   // external-gradient backward (cvae_backward): the loss gradient is given, not computed
   int ext;
@@ -592,6 +594,9 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
     const StepDesc s0 = a.steps[0];
     load_block(pre, (const T*)s0.W, s0.Kp & 0x3FFFFFFF, s0.Np, wave, 0);
   }
+  // device counters: this launch begins optimizer step ctr[1] + 1 (the Adam kernel behind it reads
+  // it and its scalars); one lane of block 0, while its wave waits for the first loads
+  if (TRAIN && a.ctr && blockIdx.x == 0 && tid == 0) adam_precompute(a.ctr, a.lr, a.beta1, a.beta2, a.adam_pre);
   stamp();
 
   // ---------------------------------------------------------------- prologue: x tile, start points, LDS state
@@ -1074,8 +1079,6 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
     stamp();
   }
   if (!TRAIN) return;
-  // device counters: this launch begins optimizer step ctr[1] + 1 (the Adam kernel behind it reads it)
-  if (a.ctr && blockIdx.x == 0 && tid == 0) a.ctr[1] = a.ctr[1] + 1;
 
   // ---------------------------------------------------------------- loss partial sums (deterministic order)
   s_recon = wave_sum(s_recon);

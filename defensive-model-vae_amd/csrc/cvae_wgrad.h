@@ -63,24 +63,18 @@ struct AdamArgs {
   double lr, beta1d, beta2d;
 };
 
-// torch's two per-step Adam scalars from the step count t, in doubles as Python forms them
-// (torch/optim/adam.py: bias_correction1 = 1 - beta1 ** step, step_size = lr / bias_correction1,
-// bias_correction2_sqrt = bias_correction2 ** 0.5), rounded to fp32 where the tensor op takes them
-__device__ __forceinline__ void adam_scalars(double lr, double b1, double b2, double t, float& lr_neg_step,
-                                             float& bc2_sqrt) {
-  const double bc1 = 1.0 - pow(b1, t);
-  const double bc2 = 1.0 - pow(b2, t);
-  lr_neg_step = (float)(-(lr / bc1));
-  bc2_sqrt = (float)sqrt(bc2);
+// device-counter path: the step's two scalars are precomputed once per step (by the row chain that
+// begins the step, adam_precompute) into ctr[2] as two fp32 — a kernel loads 8 bytes instead of
+// doing double pow in every block.  Issued first (vmcnt retires in order).
+__device__ __forceinline__ adam_f32x2 adam_step_load(const AdamArgs& a) {
+  return a.ctr ? gld<adam_f32x2>(a.ctr + 2) : adam_f32x2{0.f, 0.f};
 }
-// device-counter path: the scalars of step t = ctr[1] (every thread; wave-uniform).  Split in two
-// so a kernel can issue the counter load first and do the double arithmetic once its operand loads
-// are in flight (vmcnt retires in order: a load issued after them would wait for all of them).
-__device__ __forceinline__ uint64_t adam_step_load(const AdamArgs& a) { return a.ctr ? gld<uint64_t>(a.ctr + 1) : 0; }
-__device__ __forceinline__ void adam_resolve(AdamArgs& a, uint64_t t) {
-  if (a.ctr) adam_scalars(a.lr, a.beta1d, a.beta2d, (double)t, a.lr_neg_step, a.bc2_sqrt);
+__device__ __forceinline__ void adam_resolve(AdamArgs& a, adam_f32x2 sc) {
+  if (a.ctr) {
+    a.lr_neg_step = sc[0];
+    a.bc2_sqrt = sc[1];
+  }
 }
-
 struct LossArgs {
   const float* partials;  // [ntiles][8]
   int ntiles;
@@ -381,7 +375,7 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
   const int o = tid / TPR, iv = (tid % TPR) * EPT;
 
   WSTAMP(0);
-  const uint64_t t_step = MODE == PM_ADAM ? adam_step_load(aa) : 0;
+  const adam_f32x2 t_step = MODE == PM_ADAM ? adam_step_load(aa) : adam_f32x2{0.f, 0.f};
   f32x4 acc[2][NX];
 #pragma unroll
   for (int m = 0; m < 2; ++m)

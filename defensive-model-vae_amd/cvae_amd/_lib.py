@@ -47,8 +47,9 @@ _SIGS = {
     "cvae_forward": (_i, [_v, _v, _v, _i, _i, _v, _v, _u64, _u64, _i64, _v, _v, _v, _v, _v, _v]),
     "cvae_condition": (_i, [_v, _v, _i, _v, _v]),
     "cvae_decode": (_i, [_v, _v, _v, _v, _i, _v, _v]),
-    # h, x, idx, batch, xflags, eps, seed, offset, eps_row0, w, grads, loss_out, loss_accum, counters, parts, stream
-    "cvae_train_fwd_bwd": (_i, [_v, _v, _v, _i, _i, _v, _u64, _u64, _i64, _W, _v, _v, _v, _v, _i, _v]),
+    # h, x, idx, batch, xflags, eps, seed, offset, eps_row0, w, grads, loss_out, loss_accum, counters, adam,
+    # parts, stream
+    "cvae_train_fwd_bwd": (_i, [_v, _v, _v, _i, _i, _v, _u64, _u64, _i64, _W, _v, _v, _v, _v, _A, _i, _v]),
     # h, x, idx, batch, xflags, start, eps, seed, offset, eps_row0, d_recon, d_mu, d_logvar, d_hc, grads, stream
     "cvae_backward": (_i, [_v, _v, _v, _i, _i, _v, _v, _u64, _u64, _i64, _v, _v, _v, _v, _v, _v]),
     # h, params, grads, m, v, step, adam, grad_scale, counters, stream

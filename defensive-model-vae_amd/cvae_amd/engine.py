@@ -80,7 +80,8 @@ class CVAEEngine:
         self.grads = torch.zeros(self.n_params, **kw)
         self.loss = torch.zeros(5, **kw)
         self.loss_accum = torch.zeros(5, device=self.device, dtype=torch.float64)
-        self.counters = torch.zeros(2, device=self.device, dtype=torch.int64)
+        # [offset, steps begun, Adam scalars of that step (2 x fp32), reserved] — include/cvae.h
+        self.counters = torch.zeros(4, device=self.device, dtype=torch.int64)
         self._ctr = [0, 0]  # host mirrors of counters
         self.seed = int(seed)
         self.lr, self.betas, self.eps = 1e-3, (0.9, 0.999), 1e-8
@@ -172,7 +173,7 @@ class CVAEEngine:
 
     def sync_counters(self):
         """Host mirrors ← device counters (after graph replays the host did not count)."""
-        c = self.counters.cpu().tolist()
+        c = self.counters[:2].cpu().tolist()
         self._ctr = [int(c[0]), int(c[1])]
         return tuple(self._ctr)
 
@@ -300,10 +301,11 @@ class CVAEEngine:
         e = self._eps(eps, B)
         self.ensure_packed()
         w = self._weights(weights)
+        a = self._adam()
         check(lib().cvae_train_fwd_bwd(
             self._h, ptr(x), ptr(idx), B, self._xflags(x), ptr(e), self.seed, 0, int(row0), C.byref(w),
             ptr(self.grads), ptr(self.loss), ptr(self.loss_accum) if accumulate else None, ptr(self.counters),
-            int(parts), self._stream()), "cvae_train_fwd_bwd")
+            C.byref(a), int(parts), self._stream()), "cvae_train_fwd_bwd")
         self._ctr[0] += 1
         self._ctr[1] += 1
         self._last_batch = B
@@ -314,8 +316,8 @@ class CVAEEngine:
         ``forward_backward(parts=CHAIN|DW_DEC)`` ran."""
         B = int(batch if batch is not None else self._last_batch)
         check(lib().cvae_train_fwd_bwd(
-            self._h, None, None, B, 0, None, 0, 0, 0, None, ptr(self.grads), None, None, None, CVAE_PART_DW_REST,
-            self._stream()), "cvae_train_fwd_bwd(rest)")
+            self._h, None, None, B, 0, None, 0, 0, 0, None, ptr(self.grads), None, None, None, None,
+            CVAE_PART_DW_REST, self._stream()), "cvae_train_fwd_bwd(rest)")
 
     def adam_step(self, grad_scale=1.0):
         """optimizer.step() on the flat buffers with g = grads * grad_scale (Training_VAE.py:363);

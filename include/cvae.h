@@ -94,13 +94,16 @@ typedef struct cvae_adam_config {
   double lr, beta1, beta2, eps;
 } cvae_adam_config;
 
-/* Device step counters (caller-owned device memory, 2 x uint64):
+/* Device step counters (caller-owned device memory, 4 x uint64, zero-initialised by the caller or
+ * set to a resume point):
  *   counters[0] = Philox offset of the next training step's eps draw,
- *   counters[1] = optimizer steps begun.
- * A training call given counters reads them ON THE DEVICE and advances them: the row chain adds 1
- * to counters[1] (the step it begins; Adam uses t = counters[1]) and the dW launch adds 1 to
- * counters[0].  The `offset` / `step` arguments are then ignored.  With counters == NULL the host
- * values are used. */
+ *   counters[1] = optimizer steps begun,
+ *   counters[2] = the Adam scalars of step counters[1] (two fp32: -lr/(1-beta1^t), sqrt(1-beta2^t),
+ *                 written by the library), counters[3] reserved.
+ * A training call given counters reads them ON THE DEVICE and advances them: the row chain that
+ * begins a step adds 1 to counters[1] and (given the Adam config) stores that step's scalars, the
+ * Adam update uses t = counters[1] and those scalars, and the dW launch adds 1 to counters[0].  The
+ * `offset` / `step` arguments are then ignored.  With counters == NULL the host values are used. */
 
 /* Create/destroy.  Replaces ConditionalTrajectoryVAE.__init__ (Training_VAE.py:124-167)
  * for the device side; parameters themselves live in the caller's flat fp32 buffer. */
@@ -173,11 +176,13 @@ int cvae_decode(cvae_handle* h, const float* z, const float* start, const float*
  * Means are over this call's batch, so a data-parallel caller all-reduces
  * `grads` and passes grad_scale = 1/world to cvae_adam.
  * parts: CVAE_PART_ALL, or CVAE_PART_CHAIN|CVAE_PART_DW_DEC followed by a CVAE_PART_DW_REST call
- * on the same batch (the two-bucket overlap; loss and counters advance in the first call). */
+ * on the same batch (the two-bucket overlap; loss and counters advance in the first call).
+ * counters + adam (nullable): the step this call begins, with its Adam scalars precomputed for the
+ * cvae_adam(counters) that completes it — a data-parallel step is capturable as one graph. */
 int cvae_train_fwd_bwd(cvae_handle* h, const void* x, const int64_t* idx, int batch, int xflags,
                        const float* eps, uint64_t seed, uint64_t offset, int64_t eps_row0,
                        const cvae_loss_weights* w, float* grads, float* loss_out, double* loss_accum,
-                       uint64_t* counters, int parts, void* stream);
+                       uint64_t* counters, const cvae_adam_config* adam, int parts, void* stream);
 
 /* Backward of model.forward from caller-supplied output gradients (the autograd path: the
  * reference loop's loss.backward(), Training_VAE.py:362, when conditional_vae_loss and the
@@ -192,7 +197,8 @@ int cvae_backward(cvae_handle* h, const void* x, const int64_t* idx, int batch, 
 
 /* torch.optim.Adam step (amsgrad=False, weight_decay=0) over the flat buffers
  * — replaces optimizer.step() (Training_VAE.py:363; torch/optim/adam.py
- * _single_tensor_adam).  step is the 1-based step count after increment (or t = counters[1]).
+ * _single_tensor_adam).  step is the 1-based step count after increment; with counters, t and its
+ * scalars come from the cvae_train_fwd_bwd(counters, adam) that began the step.
  * g_eff = grads * grad_scale.  Also refreshes the device weight copies. */
 int cvae_adam(cvae_handle* h, float* params, const float* grads, float* m, float* v, int64_t step,
               const cvae_adam_config* adam, float grad_scale, const uint64_t* counters, void* stream);

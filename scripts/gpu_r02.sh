@@ -18,9 +18,15 @@ if [ "$WHAT" = all ] || [ "$WHAT" = bench ]; then
   $B --steps 200 --warmup 20 --no-cpu-baseline --dp > $OUT/bench_dp.json 2> $OUT/bench_dp.err && \
   $B --steps 200 --warmup 20 --no-cpu-baseline --dp --buckets 2 > $OUT/bench_dp_b2.json 2> $OUT/bench_dp_b2.err && \
   $B --steps 200 --warmup 20 --no-cpu-baseline --dp --graph > $OUT/bench_dp_graph.json 2> $OUT/bench_dp_graph.err && \
+  $B --steps 200 --warmup 20 --no-cpu-baseline --dp --graph --buckets 2 > $OUT/bench_dp_graph_b2.json 2> $OUT/bench_dp_graph_b2.err && \
   $B --steps 200 --warmup 20 --no-cpu-baseline --graph > $OUT/bench_graph.json 2> $OUT/bench_graph.err && \
+  $B --steps 400 --warmup 20 --workload cfg1 --dtype bf16 --no-cpu-baseline > $OUT/bench_cfg1_bf16.json 2> $OUT/bench_cfg1_bf16.err && \
   $B --steps 400 --warmup 20 --workload cfg1 > $OUT/bench_cfg1.json 2> $OUT/bench_cfg1.err && \
   $B --steps 400 --warmup 20 --workload cfg1 --batch 38 --no-cpu-baseline > $OUT/bench_cfg1_b38.json 2> $OUT/bench_cfg1_b38.err || \
   { echo BENCH FAILED; tail -20 $OUT/*.err; exit 1; }
   for f in $OUT/bench_*.json; do echo "$f"; python3 -c "import json,sys; d=json.load(open('$f')); print(d['value'], d['ms_per_step'], d['roofline']['kernels_ms'], d.get('cpu_baseline',{}).get('value'))"; done
+fi
+if [ "$WHAT" = stamps ]; then
+  CVAE_LIB=$PWD/build/diag/stamps.so timeout -k 10 120 python -u scripts/diag_stamps.py > $OUT/stamps.txt 2>&1 || { tail -20 $OUT/stamps.txt; exit 1; }
+  cat $OUT/stamps.txt
 fi
