@@ -166,7 +166,10 @@ def main():
     ap.add_argument("--buckets", type=int, default=1, choices=[1, 2],
                     help="split step: 2 = decoder-gradient all-reduce overlapped with the rest of dW")
     ap.add_argument("--graph", action="store_true",
-                    help="capture one step into a hipGraph and replay it (device step counters)")
+                    help="capture the step into a hipGraph and replay it (device step counters); the default "
+                         "for the split (data-parallel) step")
+    ap.add_argument("--no-graph", action="store_true", help="split step issued eagerly (no hipGraph)")
+    ap.add_argument("--graph-steps", type=int, default=1, help="training steps captured per graph replay")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-b2b", action="store_true",
@@ -237,14 +240,23 @@ def main():
         x = eng.as_input(x)  # resident in HBM, operand dtype
         rows_per_step = B
         graphed = None
-        if args.graph:
-            graphed = GraphedStep(eng, lambda: dp.step(x, batch=B, global_batch=B * world), n=1, warmup=2)
+        use_graph = args.graph or (dp.split and not args.no_graph)
+        graph_note = ""
+        if use_graph:
+            try:
+                graphed = GraphedStep(eng, lambda: dp.step(x, batch=B, global_batch=B * world),
+                                      n=args.graph_steps, warmup=2)
+            except Exception as e:  # capture refused (e.g. a collective backend that cannot be captured)
+                graphed, graph_note = None, f" (graph capture failed, eager: {type(e).__name__})"
+                torch.cuda.synchronize(dev)
+        if graphed is not None and args.steps % graphed.n:
+            raise SystemExit("--steps must be a multiple of --graph-steps")
 
         def run(k):
             """k training steps: on one GPU one cvae_train_steps call (no host work per step); split
             (data-parallel) path: fwd/bwd → RCCL all-reduce → Adam per step; --graph: replays."""
             if graphed is not None:
-                for _ in range(k):
+                for _ in range(-(-k // graphed.n)):
                     graphed.replay()
             elif not dp.split:
                 eng.train_steps(x, k, batch=B)
@@ -267,7 +279,7 @@ def main():
     # launch stream between kernels (events inside the timed pass would add ~10 us per step;
     # graph replays record none, so this pass runs eagerly)
     eng.set_timing(True)
-    if args.graph and wl != "cfg1":
+    if wl != "cfg1" and graphed is not None:
         for _ in range(args.steps):
             dp.step(x, batch=B, global_batch=B * world)
     else:
@@ -319,7 +331,11 @@ def main():
         else:
             metric = f"trajectories/sec per ELBO step, batch={B} seq_len={S} (BASELINE cfg5 shape)"
             data = "synthetic x~N(0,1) (seeded), random-init weights (torch.manual_seed(0))"
-        path = "graph" if args.graph else ("split" if dp.split else "fused")
+        if wl == "cfg1":
+            path = "split" if dp.split else "fused"
+        else:
+            path = (("graphed " if graphed is not None else "") + ("split" if dp.split else "fused")
+                    + (f" x{graphed.n}/replay" if graphed is not None and graphed.n > 1 else "") + graph_note)
         res = {"metric": metric,
                "value": round(value, 1), "unit": "trajectories/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(t / args.steps * 1e3, 5), "higher_is_better": True,

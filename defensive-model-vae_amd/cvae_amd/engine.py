@@ -152,6 +152,16 @@ class CVAEEngine:
         self.v.zero_()
         self.step_count = 0
 
+    # ------------------------------------------------------------------ optimizer state (resume)
+    def optimizer_state_dict(self):
+        """Adam state in torch.optim.Adam.state_dict() format (CPU tensors): per parameter index
+        {'step', 'exp_avg', 'exp_avg_sq'} and one param group — loadable by torch's Adam over
+        model.parameters(), and by load_optimizer_state_dict."""
+        return optimizer_state_dict(self)
+
+    def load_optimizer_state_dict(self, sd):
+        load_optimizer_state_dict(self, sd)
+
     # ------------------------------------------------------------------ step counters
     @property
     def rng_offset(self):
@@ -437,6 +447,42 @@ class CVAEEngine:
         return b.value
 
 
+def optimizer_state_dict(eng):
+    """torch.optim.Adam.state_dict() of the engine's flat m / v (works for any engine with
+    tensors/m/v/step_count/lr/betas/eps: the CPU oracle stand-in too)."""
+    steps = float(eng.step_count)
+    state = {}
+    for i, (o, n, shape) in enumerate(eng.tensors):
+        state[i] = {"step": torch.tensor(steps),
+                    "exp_avg": eng.m[o:o + n].detach().view(shape).cpu().clone(),
+                    "exp_avg_sq": eng.v[o:o + n].detach().view(shape).cpu().clone()}
+    group = {"lr": eng.lr, "betas": tuple(eng.betas), "eps": eng.eps, "weight_decay": 0, "amsgrad": False,
+             "maximize": False, "foreach": None, "capturable": False, "differentiable": False, "fused": None,
+             "decoupled_weight_decay": False, "params": list(range(len(eng.tensors)))}
+    return {"state": state, "param_groups": [group]}
+
+
+def load_optimizer_state_dict(eng, sd):
+    """Inverse of optimizer_state_dict (also accepts torch Adam's own state_dict of the same
+    parameter order); sets m, v, the step count and the hyper-parameters."""
+    g = sd["param_groups"][0]
+    eng.set_optimizer(lr=g["lr"], betas=g["betas"], eps=g["eps"])
+    steps = set()
+    with torch.no_grad():
+        for i, (o, n, shape) in enumerate(eng.tensors):
+            st = sd["state"].get(i) or sd["state"].get(str(i))
+            if st is None:  # a parameter torch never stepped
+                eng.m[o:o + n].zero_()
+                eng.v[o:o + n].zero_()
+                continue
+            eng.m[o:o + n].copy_(st["exp_avg"].reshape(-1).to(eng.m.device, torch.float32))
+            eng.v[o:o + n].copy_(st["exp_avg_sq"].reshape(-1).to(eng.v.device, torch.float32))
+            steps.add(int(float(st["step"])))
+    if len(steps) > 1:
+        raise ValueError(f"parameters carry different Adam step counts {sorted(steps)}")
+    eng.step_count = steps.pop() if steps else 0
+
+
 def adam_scalars(n, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, device="cuda"):
     """The device's (−lr/(1−β1^t), sqrt(1−β2^t)) for t = 1..n (cvae_adam_scalars), as an (n, 2)
     fp32 tensor — the check of the device-counter Adam path against torch's Python doubles."""
@@ -447,5 +493,5 @@ def adam_scalars(n, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, device="cuda"):
     return out
 
 
-__all__ = ["CVAEEngine", "config_info", "adam_scalars", "DTYPES", "DEFAULT_WEIGHTS", "CVAE_PART_ALL",
+__all__ = ["CVAEEngine", "config_info", "adam_scalars", "optimizer_state_dict", "load_optimizer_state_dict", "DTYPES", "DEFAULT_WEIGHTS", "CVAE_PART_ALL",
            "CVAE_PART_CHAIN", "CVAE_PART_DW_DEC", "CVAE_PART_DW_REST"]

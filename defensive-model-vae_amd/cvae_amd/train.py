@@ -89,9 +89,23 @@ def cpu_state_dict(model):
     return OrderedDict((k, v.detach().to("cpu", torch.float32).clone()) for k, v in model.state_dict().items())
 
 
+def save_checkpoint(path, model, eng, epoch, loss_history):
+    """Resume point (the reference saves only the final state_dict, Training_VAE.py:393): the
+    24-key state_dict, the Adam state in torch's Adam.state_dict() format, the epoch, the loss
+    history, the Philox offset and the global CPU RNG state (DataLoader order and host eps)."""
+    from .engine import optimizer_state_dict
+    d = os.path.dirname(str(path))
+    if d:
+        os.makedirs(d, exist_ok=True)
+    torch.save({"model": cpu_state_dict(model), "optimizer": optimizer_state_dict(eng), "epoch": int(epoch),
+                "loss_history": {k: list(v) for k, v in loss_history.items()},
+                "rng_offset": int(eng.rng_offset), "cpu_rng_state": torch.get_rng_state()}, path)
+
+
 def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidden_dim=128,
           weights=(0.1, 0.1, 1.0, 1.0), model_save_path=None, loss_save_path=None, dtype="fp32",
-          eps="host", device=None, seed=None, engine_seed=0, log=print, model=None, buckets=1):
+          eps="host", device=None, seed=None, engine_seed=0, log=print, model=None, buckets=1,
+          checkpoint_path=None, resume=None):
     """Train like ``python Training_VAE.py`` (mode='training').
 
     data: path to the (N, seq_len, dim) ``.npy`` (TrajectoryDataset, :105-115) or an array.
@@ -100,6 +114,10 @@ def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidd
     Under ``torch.distributed`` every rank runs this with the same arguments; batch_size is
     then per rank (global batch = batch_size · world) and rank 0 logs and saves; ``buckets=2``
     overlaps the decoder gradients' all-reduce with the rest of the dW GEMMs.
+
+    checkpoint_path: write a resume point (save_checkpoint) after every epoch; resume: continue
+    from one — ``epochs`` counts the total, so train(epochs=4, resume=ckpt_after_2) runs epochs 3-4
+    and ends where an uninterrupted 4-epoch run ends.
 
     Returns (model, loss_history, weighted_loss_history).
     """
@@ -131,7 +149,19 @@ def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidd
     loader = torch.utils.data.DataLoader(_Rows(n), batch_size=gb, shuffle=True)
     eng.loss_accum.zero_()
     loss_history = {k: [] for k in LOSS_KEYS}
-    for epoch in range(epochs):
+    first = 0
+    if resume is not None:
+        from .engine import load_optimizer_state_dict
+        ck = torch.load(resume, weights_only=True)
+        model.load_state_dict(ck["model"])
+        load_optimizer_state_dict(eng, ck["optimizer"])
+        eng.set_optimizer(lr=lr)
+        eng.rng_offset = ck["rng_offset"]
+        torch.set_rng_state(ck["cpu_rng_state"])
+        loss_history = {k: list(ck["loss_history"][k]) for k in LOSS_KEYS}
+        first = ck["epoch"]
+        step.broadcast_params()
+    for epoch in range(first, epochs):
         for rows in loader:                               # (:340) one global batch
             g = rows.numel()
             lo, hi = dp.split_rows(g, world_size, rank)
@@ -148,6 +178,8 @@ def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidd
             loss_history[k].append(float(v))
         if rank == 0 and log:
             log(epoch_line(epoch, means))
+        if rank == 0 and checkpoint_path:
+            save_checkpoint(checkpoint_path, model, eng, epoch + 1, loss_history)
     weighted = weighted_history(loss_history, weights)
     if rank == 0:
         if loss_save_path:
@@ -194,6 +226,8 @@ def main(argv=None):
     ap.add_argument("--eps", default="host", choices=["host", "philox"])
     ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--model-out", default=None)
+    ap.add_argument("--checkpoint", default=None, help="write a resume point (model + Adam + RNG) every epoch")
+    ap.add_argument("--resume", default=None, help="continue from a --checkpoint file (--epochs = total)")
     ap.add_argument("--loss-out", default=None)
     a = ap.parse_args(argv)
     model_out, loss_out = default_paths(a.data, a.latent, a.epochs)
@@ -209,7 +243,8 @@ def main(argv=None):
     try:
         train(a.data, a.seq_len, a.dim, a.latent, batch_size=a.batch_size, lr=a.lr, epochs=a.epochs,
               hidden_dim=a.hidden, weights=tuple(a.weights), model_save_path=a.model_out or model_out,
-              loss_save_path=a.loss_out or loss_out, dtype=a.dtype, eps=a.eps, device=device, seed=a.seed)
+              loss_save_path=a.loss_out or loss_out, dtype=a.dtype, eps=a.eps, device=device, seed=a.seed,
+              checkpoint_path=a.checkpoint, resume=a.resume)
     finally:
         if world_size > 1:
             torch.distributed.destroy_process_group()

@@ -29,6 +29,11 @@ class OracleEngine:
         self.lr, self.betas, self.eps = 1e-3, (0.9, 0.999), 1e-8
         self.weights = DEFAULT_WEIGHTS
         self.calls = []
+        self.rng_offset = 0
+        o, self.tensors = 0, []
+        for p in self.plist:
+            self.tensors.append((o, p.numel(), tuple(p.shape)))
+            o += p.numel()
 
     # --- engine surface
     def set_optimizer(self, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
@@ -90,3 +95,9 @@ class OracleModel(OracleCVAE):
     def __init__(self, *a, **k):
         super().__init__(*a, **k)
         self.__dict__["_engine"] = OracleEngine(self)
+
+    def load_state_dict(self, sd, strict=True, assign=False):
+        res = super().load_state_dict(sd, strict=strict, assign=assign)
+        eng = self.__dict__["_engine"]
+        eng.params.copy_(torch.cat([p.detach().reshape(-1) for p in eng.plist]))
+        return res

@@ -332,3 +332,21 @@ def test_bf16_real_data_fp32_relative_transform(cvae, golden):
     errbf = np.abs(lbf - want) / np.abs(want)
     print("bf16 on sce1: rel loss error vs fp32 golden, fp32 transform", err32, "bf16 input", errbf)
     assert err32[0] < 0.6 * errbf[0] and err32[1] < 0.5 * errbf[1], (err32, errbf)
+
+
+@pytest.mark.parametrize("eps", ["host", "philox"])
+def test_train_resume_equals_uninterrupted(cvae, golden, tmp_path, eps):
+    """cvae_amd.train on the device: 2 epochs + checkpoint, then resume to 4 == 4 epochs straight,
+    bit for bit (model, Adam state, device Philox offset / step counters, host RNG)."""
+    from cvae_amd.train import train
+    x = golden("sce_fixed.npz")["sce1_x"]
+    kw = dict(batch_size=16, weights=W, log=None, eps=eps, dtype="fp32")
+    m4, h4, _ = train(x, 10, 3, 8, epochs=4, seed=0, **kw)
+    ck = tmp_path / "ck.pt"
+    train(x, 10, 3, 8, epochs=2, seed=0, checkpoint_path=str(ck), **kw)
+    m22, h22, _ = train(x, 10, 3, 8, epochs=4, seed=0, resume=str(ck), **kw)
+    assert h22 == h4
+    for k, v in m4.state_dict().items():
+        assert torch.equal(v, m22.state_dict()[k]), k
+    e4, e22 = m4.engine, m22.engine
+    assert torch.equal(e4.m, e22.m) and torch.equal(e4.v, e22.v) and torch.equal(e4.counters, e22.counters)
