@@ -169,7 +169,8 @@ def main():
                     help="capture the step into a hipGraph and replay it (device step counters); the default "
                          "for the split (data-parallel) step")
     ap.add_argument("--no-graph", action="store_true", help="split step issued eagerly (no hipGraph)")
-    ap.add_argument("--graph-steps", type=int, default=1, help="training steps captured per graph replay")
+    ap.add_argument("--graph-steps", type=int, default=8,
+                    help="training steps captured per graph replay (a remainder runs a 1-step graph)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-b2b", action="store_true",
@@ -242,22 +243,24 @@ def main():
         graphed = None
         use_graph = args.graph or (dp.split and not args.no_graph)
         graph_note = ""
+        graphed1 = None
         if use_graph:
+            one = lambda: dp.step(x, batch=B, global_batch=B * world)  # noqa: E731
             try:
-                graphed = GraphedStep(eng, lambda: dp.step(x, batch=B, global_batch=B * world),
-                                      n=args.graph_steps, warmup=2)
+                graphed = GraphedStep(eng, one, n=max(1, args.graph_steps), warmup=2)
+                graphed1 = graphed if graphed.n == 1 else GraphedStep(eng, one, n=1, warmup=0)
             except Exception as e:  # capture refused (e.g. a collective backend that cannot be captured)
                 graphed, graph_note = None, f" (graph capture failed, eager: {type(e).__name__})"
                 torch.cuda.synchronize(dev)
-        if graphed is not None and args.steps % graphed.n:
-            raise SystemExit("--steps must be a multiple of --graph-steps")
 
         def run(k):
             """k training steps: on one GPU one cvae_train_steps call (no host work per step); split
             (data-parallel) path: fwd/bwd → RCCL all-reduce → Adam per step; --graph: replays."""
             if graphed is not None:
-                for _ in range(-(-k // graphed.n)):
+                for _ in range(k // graphed.n):
                     graphed.replay()
+                for _ in range(k % graphed.n):
+                    graphed1.replay()
             elif not dp.split:
                 eng.train_steps(x, k, batch=B)
             else:

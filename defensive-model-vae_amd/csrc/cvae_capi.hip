@@ -93,9 +93,14 @@ int build_plan(cvae_handle* h) {
   n.S = c.seq_len; n.D = c.dim; n.Z = c.latent_dim; n.H = c.hidden_dim;
   n.I = c.seq_len * c.dim;
   n.n_enc = c.n_enc; n.n_dec = c.n_dec;
-  n.n_layers = 2 + c.n_enc + 1 + c.n_dec;
-  n.Ip = rup_i(n.I, 32); n.Hp = rup_i(n.H, 32); n.Hcp = rup_i(2 * n.H, 32);
-  n.ZHp = rup_i(n.Z + n.H, 32); n.Zp2 = rup_i(2 * n.Z, 32); n.Cp = 32;
+  n.n_layers = 2 + c.n_enc + 1 + c.n_dec + (c.n_classes > 0 ? 1 : 0);
+  // cfg4 class embedding: e = table[class] (class_dim wide) joins both concatenations
+  n.n_cls = c.n_classes > 0 ? c.n_classes : 0;
+  n.cls_dim = n.n_cls ? c.class_dim : 0;
+  n.Clsp = n.n_cls ? rup_i(n.n_cls, 32) : 0;
+  const int E = n.cls_dim;
+  n.Ip = rup_i(n.I, 32); n.Hp = rup_i(n.H, 32); n.Hcp = rup_i(2 * n.H + E, 32);
+  n.ZHp = rup_i(n.Z + n.H + E, 32); n.Zp2 = rup_i(2 * n.Z, 32); n.Cp = 32;
   n.dtype = c.dtype;
   h->tsize = c.dtype == CVAE_F32 ? 4 : 2;  // CVAE_FP8 keeps bf16 activations (only forward W/X operands are e4m3)
   // arena rows: whole row tiles, and a multiple of the K chunk of the wgrad GEMM
@@ -107,11 +112,12 @@ int build_plan(cvae_handle* h) {
   ld.push_back({2, n.H, 1});
   ld.push_back({n.H, n.H, 1});
   for (int i = 0; i < n.n_enc; ++i) ld.push_back({i == 0 ? n.I : n.H, n.H, 1});
-  ld.push_back({2 * n.H, 2 * n.Z, 0});
+  ld.push_back({2 * n.H + E, 2 * n.Z, 0});                       // [h_traj ‖ h_c (‖ e)] → mu ‖ logvar
   for (int i = 0; i < n.n_dec; ++i) {
     const bool last = i == n.n_dec - 1;
-    ld.push_back({i == 0 ? n.Z + n.H : n.H, last ? n.I : n.H, last ? 0 : 1});
+    ld.push_back({i == 0 ? n.Z + n.H + E : n.H, last ? n.I : n.H, last ? 0 : 1});  // [z ‖ h_c (‖ e)] first
   }
+  if (n.n_cls) ld.push_back({n.n_cls, E, 0});                    // one-hot(class) → e (the table)
   if ((int)ld.size() > CVAE_MAX_LAYERS) return fail(CVAE_E_INVALID, "too many layers");
 
   // flat parameter table (state_dict order; fc splits into fc_mu / fc_logvar)
@@ -127,7 +133,16 @@ int build_plan(cvae_handle* h) {
     LayerDev& L = n.L[l];
     L.K = ld[l].K; L.N = ld[l].N; L.Kp = rup_i(L.K, 32); L.Np = rup_i(L.N, 32); L.relu = ld[l].relu;
     L.f8 = c.dtype == CVAE_FP8 && L.Kp % 64 == 0;  // fp8 forward GEMM where K pairs up (cvae_device.h)
-    if (l == lFC(n)) {
+    L.has_bias = 1;
+    L.wt = 0;
+    if (n.n_cls && l == lCE(n)) {  // nn.Embedding(n_classes, class_dim).weight: [K][N], no bias
+      L.f8 = 0;
+      L.wt = 1;
+      L.has_bias = 0;
+      L.nseg = 1; L.seg_rows0 = L.N;
+      L.pw[0] = L.pw[1] = add(n.n_cls, E);
+      L.pb[0] = L.pb[1] = -1;
+    } else if (l == lFC(n)) {
       L.nseg = 2; L.seg_rows0 = n.Z;
       L.pw[0] = add(n.Z, L.K); L.pb[0] = add(n.Z, 0);
       L.pw[1] = add(n.Z, L.K); L.pb[1] = add(n.Z, 0);
@@ -164,6 +179,8 @@ int build_plan(cvae_handle* h) {
   if (c.dim < 3) return fail(CVAE_E_INVALID, "dim must be >= 3 (channel 0 = time, 1:3 = x,y)");
   if (c.hidden_dim % 4 || c.latent_dim % 4)
     return fail(CVAE_E_INVALID, "hidden_dim and latent_dim must be multiples of 4 (4-feature epilogue vectors)");
+  if (c.n_classes < 0 || (c.n_classes > 0 && (c.class_dim < 4 || c.class_dim % 4)))
+    return fail(CVAE_E_INVALID, "class_dim must be a positive multiple of 4 when n_classes > 0");
 
   // Weight-gradient / parameter tiles: 32×32 over each layer's padded (Np × Kp), laid out for
   // the 8 XCDs.  Workgroup b runs on XCD b % 8 and every XCD has its own L2, so a tile's G rows
@@ -251,6 +268,13 @@ std::vector<StepSpec> build_steps(const NetDev& n, int mode) {
     v.push_back(s);
   }
   if (mode == cvae_handle::ST_COND) return v;
+  if (n.n_cls) {  // cfg4: e = table[class] → [.. ‖ e] of the fc input and of the decoder input
+    StepSpec s = fwd(lCE(n), B_CLS, E_RELU);
+    s.linear = 1; s.concat = 1;
+    s.dst1 = B_HC; s.off1 = 2 * H; s.dst2 = B_DEC; s.off2 = Z + H;
+    s.g1 = arena(n.L[lFC(n)].xT); s.goff1 = 2 * H; s.g2 = arena(n.L[lD(n, 0)].xT); s.goff2 = Z + H;
+    v.push_back(s);
+  }
   if (mode == cvae_handle::ST_TRAIN || mode == cvae_handle::ST_FWD) {
     for (int i = 0; i < ne; ++i) {
       StepSpec s = fwd(lE(n, i), i == 0 ? B_XIN : pb(i - 1), E_RELU);
@@ -546,7 +570,8 @@ int plan_fast(cvae_handle* h) {
   const NetDev& n = h->net;
   h->fast_nki = 0;
   const char* env = std::getenv("CVAE_GENERIC");
-  if ((env && env[0] == '1') || c.dtype != CVAE_BF16 || c.hidden_dim != fchain::H || c.latent_dim != fchain::Z ||
+  if ((env && env[0] == '1') || c.dtype != CVAE_BF16 || c.n_classes > 0 || c.hidden_dim != fchain::H ||
+      c.latent_dim != fchain::Z ||
       c.n_enc != 4 || c.n_dec != 4 || n.I % 8 != 0 || n.nbias > 16 * fchain::NT || h->R != 16)
     return CVAE_OK;
   for (int nki : kFastNki) {
@@ -576,6 +601,7 @@ int plan_fast(cvae_handle* h) {
 struct CallX {
   const void* x;
   const int64_t* idx;
+  const int32_t* classes;
   int batch;
   int xflags;
   const float* eps;
@@ -588,7 +614,7 @@ struct CallX {
 
 RowArgs row_args(cvae_handle* h, const CallX& c) {
   RowArgs ra{};
-  ra.x = c.x; ra.idx = c.idx; ra.batch = c.batch; ra.eps = c.eps; ra.seed = c.seed; ra.offset = c.offset;
+  ra.x = c.x; ra.idx = c.idx; ra.classes = c.classes; ra.batch = c.batch; ra.eps = c.eps; ra.seed = c.seed; ra.offset = c.offset;
   ra.eps_row0 = c.eps_row0;
   ra.x_f32 = (c.xflags & CVAE_X_F32) && is16(h) ? 1 : 0;
   ra.ctr = c.ctr;
@@ -828,13 +854,14 @@ int cvae_pack_weights(cvae_handle* h, const float* params, void* stream) {
   return CVAE_OK;
 }
 
-int cvae_forward(cvae_handle* h, const void* x, const int64_t* idx, int batch, int xflags, const float* start,
+int cvae_forward(cvae_handle* h, const void* x, const int64_t* idx, const int32_t* classes, int batch, int xflags,
+                 const float* start,
                  const float* eps, uint64_t seed, uint64_t offset, int64_t eps_row0, float* recon, float* mu,
                  float* logvar, float* hc, float* eps_out, void* stream) {
   if (!h || !x) return fail(CVAE_E_INVALID, "null argument");
   int rc = check_batch(h, batch);
   if (rc) return rc;
-  RowArgs a = row_args(h, CallX{x, idx, batch, xflags, eps, seed, offset, eps_row0, nullptr, nullptr, nullptr});
+  RowArgs a = row_args(h, CallX{x, idx, classes, batch, xflags, eps, seed, offset, eps_row0, nullptr, nullptr, nullptr});
   a.start_in = start; a.x_relative = start ? 1 : 0;
   a.recon_out = recon; a.mu_out = mu; a.lv_out = logvar; a.hc_out = hc; a.eps_out = eps_out;
   hipStream_t s = (hipStream_t)stream;
@@ -853,20 +880,21 @@ int cvae_condition(cvae_handle* h, const float* start, int batch, float* hc, voi
                                    : launch_rowchain<float, RC_DECODE>(h, a, s);
 }
 
-int cvae_decode(cvae_handle* h, const float* z, const float* start, const float* hc, int batch, float* out,
-                void* stream) {
+int cvae_decode(cvae_handle* h, const float* z, const float* start, const float* hc, const int32_t* classes, int batch,
+                float* out, void* stream) {
   if (!h || !z || !out || (!start && !hc)) return fail(CVAE_E_INVALID, "null argument");
   int rc = check_batch(h, batch);
   if (rc) return rc;
   RowArgs a{};
-  a.batch = batch; a.z_in = z; a.start_in = start; a.hc_in = hc; a.recon_out = out;
+  a.batch = batch; a.z_in = z; a.start_in = start; a.hc_in = hc; a.recon_out = out; a.classes = classes;
   a.partials = h->d_partials;
   hipStream_t s = (hipStream_t)stream;
   return is16(h) ? launch_rowchain<__bf16, RC_DECODE>(h, a, s)
                                    : launch_rowchain<float, RC_DECODE>(h, a, s);
 }
 
-int cvae_train_fwd_bwd(cvae_handle* h, const void* x, const int64_t* idx, int batch, int xflags, const float* eps,
+int cvae_train_fwd_bwd(cvae_handle* h, const void* x, const int64_t* idx, const int32_t* classes, int batch, int xflags,
+                       const float* eps,
                        uint64_t seed, uint64_t offset, int64_t eps_row0, const cvae_loss_weights* w, float* grads,
                        float* loss_out, double* loss_accum, uint64_t* counters, const cvae_adam_config* adam,
                        int parts, void* stream) {
@@ -876,11 +904,12 @@ int cvae_train_fwd_bwd(cvae_handle* h, const void* x, const int64_t* idx, int ba
   int rc = check_batch(h, batch);
   if (rc) return rc;
   if (adam && (rc = check_adam(adam))) return rc;
-  return fwd_bwd_impl(h, CallX{x, idx, batch, xflags, eps, seed, offset, eps_row0, w, counters, adam}, grads,
+  return fwd_bwd_impl(h, CallX{x, idx, classes, batch, xflags, eps, seed, offset, eps_row0, w, counters, adam}, grads,
                       loss_out, loss_accum, parts, (hipStream_t)stream);
 }
 
-int cvae_backward(cvae_handle* h, const void* x, const int64_t* idx, int batch, int xflags, const float* start,
+int cvae_backward(cvae_handle* h, const void* x, const int64_t* idx, const int32_t* classes, int batch, int xflags,
+                  const float* start,
                   const float* eps, uint64_t seed, uint64_t offset, int64_t eps_row0, const float* d_recon,
                   const float* d_mu, const float* d_logvar, const float* d_hc, float* grads, void* stream) {
   if (!h || !x || !grads) return fail(CVAE_E_INVALID, "null argument");
@@ -888,7 +917,7 @@ int cvae_backward(cvae_handle* h, const void* x, const int64_t* idx, int batch, 
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   tbegin(h);
-  RowArgs ra = row_args(h, CallX{x, idx, batch, xflags, eps, seed, offset, eps_row0, nullptr, nullptr, nullptr});
+  RowArgs ra = row_args(h, CallX{x, idx, classes, batch, xflags, eps, seed, offset, eps_row0, nullptr, nullptr, nullptr});
   ra.start_in = start; ra.x_relative = start ? 1 : 0;
   ra.ext = 1;
   ra.d_recon = d_recon; ra.d_mu = d_mu; ra.d_lv = d_logvar; ra.d_hc = d_hc;
@@ -918,7 +947,8 @@ int cvae_adam(cvae_handle* h, float* params, const float* grads, float* m, float
                  (const TileDesc*)h->d_tiles, aa);
 }
 
-int cvae_train_step(cvae_handle* h, const void* x, const int64_t* idx, int batch, int xflags, const float* eps,
+int cvae_train_step(cvae_handle* h, const void* x, const int64_t* idx, const int32_t* classes, int batch, int xflags,
+                    const float* eps,
                     uint64_t seed, uint64_t offset, int64_t eps_row0, const cvae_loss_weights* w, float* params,
                     float* m, float* v, int64_t step, const cvae_adam_config* adam, float* loss_out,
                     double* loss_accum, uint64_t* counters, void* stream) {
@@ -927,11 +957,12 @@ int cvae_train_step(cvae_handle* h, const void* x, const int64_t* idx, int batch
   int rc = check_batch(h, batch);
   if (!rc) rc = check_adam(adam);
   if (rc) return rc;
-  return train_step_impl(h, CallX{x, idx, batch, xflags, eps, seed, offset, eps_row0, w, counters, adam}, params, m, v,
+  return train_step_impl(h, CallX{x, idx, classes, batch, xflags, eps, seed, offset, eps_row0, w, counters, adam}, params, m, v,
                          step, adam, loss_out, loss_accum, (hipStream_t)stream);
 }
 
-int cvae_train_steps(cvae_handle* h, const void* x, const int64_t* idx, int batch, int n_steps, int xflags,
+int cvae_train_steps(cvae_handle* h, const void* x, const int64_t* idx, const int32_t* classes, int batch, int n_steps,
+                     int xflags,
                      const float* eps, uint64_t seed, uint64_t offset, int64_t eps_row0,
                      const cvae_loss_weights* w, float* params, float* m, float* v, int64_t step0,
                      const cvae_adam_config* adam, float* loss_out, double* loss_accum, uint64_t* counters,
@@ -940,7 +971,7 @@ int cvae_train_steps(cvae_handle* h, const void* x, const int64_t* idx, int batc
   if (n_steps < 0) return fail(CVAE_E_INVALID, "n_steps must be >= 0");
   const int Z = h->cfg.latent_dim;
   for (int i = 0; i < n_steps; ++i) {
-    const int rc = cvae_train_step(h, x, idx ? idx + (size_t)i * batch : nullptr, batch, xflags,
+    const int rc = cvae_train_step(h, x, idx ? idx + (size_t)i * batch : nullptr, classes, batch, xflags,
                                    eps ? eps + (size_t)i * batch * Z : nullptr, seed, offset + (uint64_t)i, eps_row0,
                                    w, params, m, v, step0 + i, adam, loss_out, loss_accum, counters, stream);
     if (rc) return rc;
@@ -965,7 +996,7 @@ int cvae_bench_kernels(cvae_handle* h, const void* x, const int64_t* idx, int ba
     HIPCK(hipEventRecord(e0, s));
     for (int r = 0; r < reps; ++r) {
       int rc2 = CVAE_OK;
-      const CallX c{x, idx, batch, 0, nullptr, 1, (uint64_t)r, 0, &w, nullptr, nullptr};
+      const CallX c{x, idx, nullptr, batch, 0, nullptr, 1, (uint64_t)r, 0, &w, nullptr, nullptr};
       if (which == 0) {
         rc2 = is16(h) ? launch_train_chain<__bf16>(h, row_args(h, c), s) : launch_train_chain<float>(h, row_args(h, c), s);
       } else if (which == 1) {

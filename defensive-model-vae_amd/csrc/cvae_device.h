@@ -32,6 +32,8 @@ struct LayerDev {
   int relu;              // 1: ReLU after this layer
   int nseg, seg_rows0;   // parameter segments along N (fc fuses mu‖logvar: 2 segments)
   int f8;                // CVAE_FP8: Wf holds OCP e4m3 fragments (pair-chunk order, f8_wf_off), see below
+  int wt;                // master weight stored [K][N] (nn.Embedding layout: the class-embedding layer)
+  int has_bias;          // 0: no bias parameter (the class-embedding layer); its padded bias stays 0
   int64_t pw[2], pb[2];  // flat fp32 offsets of weight / bias of each segment
   void* Wf;              // [Np][Kp] T  (f8: [Np][Kp] e4m3, preceded by the F8Scale header)
   void* Wb;              // [Kp][Np] T
@@ -44,6 +46,7 @@ struct NetDev {
   int S, D, Z, H, I;
   int n_enc, n_dec, n_layers;
   int Ip, Hp, Hcp, ZHp, Zp2, Cp;
+  int n_cls, cls_dim, Clsp;  // BASELINE cfg4 class embedding (0 = the reference model); Clsp = rup(n_cls, 32)
   int Bp;                // arena row capacity
   int dtype;             // 0 fp32, 1 bf16
   const float* zbias;    // zeros (>= max Np floats): the "bias" of the dX GEMMs
@@ -59,6 +62,9 @@ __host__ __device__ inline int lC1(const NetDev&) { return 1; }
 __host__ __device__ inline int lE(const NetDev&, int i) { return 2 + i; }
 __host__ __device__ inline int lFC(const NetDev& n) { return 2 + n.n_enc; }
 __host__ __device__ inline int lD(const NetDev& n, int i) { return 3 + n.n_enc + i; }
+// class-embedding layer (cfg4): one-hot(class) → e, after the decoder (its table is the last
+// parameter tensor, so the reference's 24 keys and init order come first)
+__host__ __device__ inline int lCE(const NetDev& n) { return 3 + n.n_enc + n.n_dec; }
 
 struct TileDesc { int layer, o0, i0, pad_; };
 

@@ -111,6 +111,7 @@ __host__ __device__ inline LayerDev fast_layer(int l, char* arena, int Bp, int I
   L.Kp = (int)P([](int k) { return (int64_t)LY::Kp(k); });
   L.Np = (int)P([](int k) { return (int64_t)LY::Np(k); });
   L.relu = (l == LFC || l == LD3) ? 0 : 1;
+  L.has_bias = 1;
   const int64_t off = P([](int k) { return poff_const<NKI>(k); }) + (l > LE0 ? (int64_t)H * I : 0);
   const bool fc = l == LFC;  // fc_mu.weight, fc_mu.bias, fc_logvar.weight, fc_logvar.bias
   L.nseg = fc ? 2 : 1;

@@ -107,7 +107,7 @@ __device__ int g_sub_step;
 #endif
 
 // LDS buffers a step can read or write
-enum { B_NONE = -1, B_XIN = 0, B_P0 = 1, B_P1 = 2, B_HC = 3, B_DEC = 4, B_CIN = 5 };
+enum { B_NONE = -1, B_XIN = 0, B_P0 = 1, B_P1 = 2, B_HC = 3, B_DEC = 4, B_CIN = 5, B_CLS = 6 };
 // epilogue kinds; post-step element-wise phases
 enum { E_RELU = 0, E_FC = 1, E_LOSS = 2, E_RECON = 3, E_BWD = 4, E_D0B = 5, E_FCB = 6 };
 
@@ -127,6 +127,7 @@ struct StepSpec {
   int dst2, off2;
   int goff1, goff2;  // arena row offsets of g1 / g2
   int concat;        // skip columns >= N (destination is part of a concatenation)
+  int linear;        // forward step without ReLU and mask (the class embedding)
   int hc_out;        // inference: also write h_c (fp32) to RowArgs::hc_out
   int kf1, kf2;      // feature rows of the g1 / g2 arena matrices (aoff)
   int f8;            // CVAE_FP8 forward step (e4m3 W and X)
@@ -141,7 +142,7 @@ struct StepDesc {
   void* g1;
   void* g2;
   int Kp, Np, N, bias_off;
-  int code;          // xbuf | epi<<4 | (dst1+1)<<8 | (dst2+1)<<12 | concat<<16 | hc_out<<17 | (mask_out+1)<<20 | (mask_in+1)<<26
+  int code;          // xbuf | epi<<4 | (dst1+1)<<8 | (dst2+1)<<12 | concat<<16 | hc_out<<17 | linear<<18 | (mask_out+1)<<20 | (mask_in+1)<<26
   int off1, off2;
   int goff;          // goff1 | goff2 << 16
   int kf1, kf2;      // feature rows of the g1 / g2 arena matrices
@@ -154,7 +155,7 @@ inline StepDesc encode_step(const StepSpec& s) {
   d.Kp = s.f8 ? (s.Kp / 2) | (1 << 30) : s.Kp;  // f8: the weight stream counts 64-wide K pairs
   d.Np = s.Np; d.N = s.N; d.bias_off = s.bias_off;
   d.code = s.xbuf | (s.epi << 4) | ((s.dst1 + 1) << 8) | ((s.dst2 + 1) << 12) | (s.concat << 16) |
-           (s.hc_out << 17) | ((s.mask_out + 1) << 20) | ((s.mask_in + 1) << 26);
+           (s.hc_out << 17) | (s.linear << 18) | ((s.mask_out + 1) << 20) | ((s.mask_in + 1) << 26);
   d.off1 = s.off1; d.off2 = s.off2;
   d.goff = s.goff1 | (s.goff2 << 16);
   d.kf1 = s.kf1; d.kf2 = s.kf2;
@@ -192,6 +193,7 @@ struct RowArgs {
   const float* d_mu;      // (batch, Z)
   const float* d_lv;      // (batch, Z)
   const float* d_hc;      // (batch, H)
+  const int* classes;     // cfg4: class id per row of x (gathered by idx like x); NULL = class 0
 };
 
 // Philox offset of this launch's eps draws: the device counter when given (a replayable step)
@@ -202,6 +204,7 @@ struct LdsPlan {
   int mw;                        // mask words per row
   int oXin, oP0, oP1, oHc, oDec, oCin, oMuLv, oDz, oU, oRch0, oGd0, oStart, oRow, oMask, oPart, oBias, oSteps;
   int oF8;                       // CVAE_FP8: e4m3 image of a wide step's input (R x F8_LD bytes)
+  int scls, oCls, oDce;          // cfg4: one-hot class input (R x scls T), decoder share of de (R x cls_dim fp32)
   int total;
 };
 // CVAE_FP8 steps with K <= 256 convert their input once per step into an e4m3 LDS image in
@@ -245,6 +248,9 @@ __host__ __device__ inline LdsPlan lds_plan(const NetDev& n, int R, int tsize) {
   p.oBias = take((n.nbias + 4) * 4);  // + 4 zero floats: the bias of backward steps
   p.oSteps = take(64 * (int)sizeof(StepDesc));
   p.oF8 = take(n.dtype == 2 /* CVAE_FP8 */ ? R * F8_LD : 0);
+  p.scls = n.Clsp + pad;
+  p.oCls = take(n.n_cls ? R * p.scls * tsize : 0);
+  p.oDce = take(n.n_cls ? R * n.cls_dim * 4 : 0);
   p.total = o;
   return p;
 }
@@ -562,11 +568,15 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
   float* const BiasL = (float*)(smem + P.oBias);
   uint8_t* const F8img = (uint8_t*)(smem + P.oF8);  // CVAE_FP8 only (0 B otherwise)
   // LDS buffer by id (a select chain on a uniform value: no runtime-indexed pointer array)
+  T* const Cls = (T*)(smem + P.oCls);      // cfg4 only
+  float* const Dce = (float*)(smem + P.oDce);
   auto buf = [&](int id) -> T* {
-    return id == B_XIN ? Xin : id == B_P0 ? P0b : id == B_P1 ? P1b : id == B_HC ? Hc : id == B_DEC ? Dec : Cin;
+    return id == B_XIN ? Xin : id == B_P0 ? P0b : id == B_P1 ? P1b : id == B_HC ? Hc : id == B_DEC ? Dec
+         : id == B_CLS ? Cls : Cin;
   };
   auto ld_of = [&](int id) -> int {
-    return id == B_XIN ? P.sx : (id == B_P0 || id == B_P1) ? P.sp : id == B_HC ? P.shc : id == B_DEC ? P.sdec : P.scin;
+    return id == B_XIN ? P.sx : (id == B_P0 || id == B_P1) ? P.sp : id == B_HC ? P.shc : id == B_DEC ? P.sdec
+         : id == B_CLS ? P.scls : P.scin;
   };
 
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
@@ -612,6 +622,19 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
     zero(Hc, R * P.shc * (int)sizeof(T));
     zero(Dec, R * P.sdec * (int)sizeof(T));
     zero(Mask, rup(n_masks(net) * R * mw, 16));
+    if (net.n_cls) {  // cfg4: the rows' one-hot class vectors (the class-embedding layer's input)
+      for (int e = tid; e < R * P.scls; e += RC_THREADS) Cls[e] = to_t<T>(0.f);
+    }
+  };
+  // after setup_lds and a barrier: set the one-hot entries (class of row r = classes[idx[b0+r]])
+  auto set_classes = [&]() {
+    if (!net.n_cls) return;
+    for (int r = tid; r < nrows; r += RC_THREADS) {
+      const int64_t g = a.idx ? gld<int64_t>(a.idx + b0 + r) : (int64_t)(b0 + r);
+      int c = a.classes ? gld<int>(a.classes + g) : 0;
+      c = c < 0 ? 0 : (c >= net.n_cls ? net.n_cls - 1 : c);  // out-of-range ids clamp (host validates)
+      Cls[r * P.scls + c] = to_t<T>(1.f);
+    }
   };
   // Fast path (absolute trajectories, 16-B aligned rows): task v = one 16-B vector of one row,
   // the 4 lanes of a quad holding the same vector of 4 consecutive rows.  Every lane loads its
@@ -750,21 +773,27 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
   lds_barrier();
   stamp();
 
-  // slow path only: feature-major copy of the input tiles for the weight-gradient kernel (one
-  // 4-row × 1-column quad per task → one 8-B / 16-B store; the arena pads stay zero from creation)
-  if (TRAIN && !fast && !CVAE_DIAG_NOSTORE) {
-    auto copy_T = [&](const T* src, int ld, int ncols, T* dst, int Kf) {
-      constexpr int RQ = R / 4;
-      for (int t = tid; t < ncols * RQ; t += RC_THREADS) {
-        const int c = t / RQ, q = t - c * RQ;
-        f32x4 v;
+  // feature-major copy of input tiles for the weight-gradient kernel (one 4-row × 1-column quad
+  // per task → one 8-B / 16-B store; the arena pads stay zero from creation)
+  auto copy_T = [&](const T* src, int ld, int ncols, T* dst, int Kf) {
+    constexpr int RQ = R / 4;
+    for (int t = tid; t < ncols * RQ; t += RC_THREADS) {
+      const int c = t / RQ, q = t - c * RQ;
+      f32x4 v;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = to_f(src[(4 * q + i) * ld + c]);
-        gstore4(dst + aoff(c, b0 + 4 * q, Kf), v);
-      }
-    };
+      for (int i = 0; i < 4; ++i) v[i] = to_f(src[(4 * q + i) * ld + c]);
+      gstore4(dst + aoff(c, b0 + 4 * q, Kf), v);
+    }
+  };
+  // slow path only: the condition and x tiles (the fast path stored them from its prologue)
+  if (TRAIN && !fast && !CVAE_DIAG_NOSTORE) {
     copy_T(Cin, P.scin, 2, (T*)net.L[lC0(net)].xT, net.L[lC0(net)].Kp);
     copy_T(Xin, P.sx, I, (T*)net.L[lE(net, 0)].xT, net.L[lE(net, 0)].Kp);
+  }
+  if (net.n_cls) {  // cfg4: the one-hot class input of the class-embedding step
+    set_classes();
+    lds_barrier();
+    if (TRAIN && !CVAE_DIAG_NOSTORE) copy_T(Cls, P.scls, net.n_cls, (T*)net.L[lCE(net)].xT, net.L[lCE(net)].Kp);
   }
 
   const float Bf = (float)a.batch;
@@ -807,7 +836,7 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
     const int nKp = (int)(sgpr(n1.z) & 0x3FFFFFFFu), nNp = (int)sgpr(n1.w);
     const int xbuf = code & 15, kind = (code >> 4) & 15;
     const int dst1 = (int)((code >> 8) & 15) - 1, dst2 = (int)((code >> 12) & 15) - 1;
-    const bool concat = (code >> 16) & 1, hc_o = (code >> 17) & 1;
+    const bool concat = (code >> 16) & 1, hc_o = (code >> 17) & 1, linear = (code >> 18) & 1;
     const int mask_out = (int)((code >> 20) & 63) - 1, mask_in = (int)((code >> 26) & 63) - 1;
     T* const d1 = dst1 >= 0 ? buf(dst1) : nullptr;
     T* const d2 = dst2 >= 0 ? buf(dst2) : nullptr;
@@ -854,10 +883,12 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
       uint32_t nib = 0;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        y[i] = live ? fmaxf(v[i] + b4[i], 0.f) : 0.f;  // zero-padded bias: pad features come out 0
+        const float u = v[i] + b4[i];
+        y[i] = live ? (linear ? u : fmaxf(u, 0.f)) : 0.f;  // zero-padded bias: pad features come out 0
         nib |= (y[i] > 0.f ? 1u : 0u) << i;
       }
-      if (!CVAE_DIAG_NOLDSW) mko[row * mw + (f0 >> 2)] = (uint8_t)nib;  // this lane owns (row, f0..f0+3): no atomics
+      // this lane owns (row, f0..f0+3): no atomics; the class-embedding step (linear) has no mask
+      if (!CVAE_DIAG_NOLDSW && !linear) mko[row * mw + (f0 >> 2)] = (uint8_t)nib;
       if (concat && f0 >= N) return;  // part of a concatenation: never write its pads
       if (!CVAE_DIAG_NOLDSW) put4(d1 + row * ld1 + off1 + f0, y);
       if (d2 && !CVAE_DIAG_NOLDSW) put4(d2 + row * ld2 + off2 + f0, y);
@@ -948,6 +979,8 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
         f32x4 y = v;
         if (a.ext && a.d_hc && row < nrows) y += gld<f32x4>(a.d_hc + (size_t)(b0 + row) * H + f0 - Z);  // H % 4 == 0
         *(f32x4*)(Dhc2 + row * H + f0 - Z) = y;
+      } else if (f0 < Z + H + net.cls_dim) {  // cfg4: the decoder's share of de (cls_dim % 4 == 0)
+        *(f32x4*)(Dce + row * net.cls_dim + f0 - Z - H) = v;
       }
     };
     // dh = G_fc·W_fc → [dh_traj ‖ dh_c(fc share)]   (H % 4 == 0: no straddle)
@@ -968,6 +1001,11 @@ __global__ __launch_bounds__(RC_THREADS) void rowchain_kernel(NetDev net, RowArg
         for (int i = 0; i < 4; ++i) y[i] = (nib >> i) & 1u ? v[i] + dh2[i] : 0.f;
         put4(Q + row * P.shc + c, y);
         put4Tq(g2, kf2, c, b0 + row, y);
+      } else if (f0 < 2 * H + net.cls_dim) {  // cfg4: de = fc share + decoder share (no activation)
+        const int c = f0 - 2 * H;
+        const f32x4 y2 = v + *(const f32x4*)(Dce + row * net.cls_dim + c);
+        const LayerDev& LC = net.L[lCE(net)];
+        put4Tq((T*)LC.gT, LC.Np, c, b0 + row, y2);
       }
     };
     switch (kind) {

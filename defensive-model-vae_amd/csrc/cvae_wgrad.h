@@ -115,6 +115,7 @@ template <int EPT>
 struct PreN {
   float p[EPT], m[EPT], v[EPT];
   int64_t base;
+  int64_t stride;  // flat distance of consecutive inputs i (1; N for a [K][N]-stored table)
   int nv;    // valid elements (0: padding)
   bool vec;  // whole aligned vector runs (layer-uniform)
 };
@@ -129,10 +130,11 @@ __device__ __forceinline__ PreN<EPT> loadn(const LayerDev& L, int o, int i, cons
   // wave-uniform: every run of the layer is an aligned EPT-vector (K % EPT == 0, segment offsets
   // % EPT == 0).  The choice must not be per lane: divergent scalar and vector paths share
   // destination registers, and the vector path then waits (vmcnt(0)) for every load in flight
-  s.vec = (L.K % EPT) == 0 && ((L.pw[0] | L.pw[1]) % EPT) == 0;
+  s.vec = !L.wt && (L.K % EPT) == 0 && ((L.pw[0] | L.pw[1]) % EPT) == 0;
+  s.stride = L.wt ? L.N : 1;
   if (o >= L.N || i >= L.K) return s;
   const int seg = (L.nseg == 2 && o >= L.seg_rows0) ? 1 : 0;
-  s.base = L.pw[seg] + (int64_t)(seg ? o - L.seg_rows0 : o) * L.K + i;
+  s.base = L.wt ? L.pw[0] + (int64_t)i * L.N + o : L.pw[seg] + (int64_t)(seg ? o - L.seg_rows0 : o) * L.K + i;
   s.nv = min(EPT, L.K - i);
   if (MODE == PM_GRAD) return s;
   if (s.vec) {
@@ -152,10 +154,10 @@ __device__ __forceinline__ PreN<EPT> loadn(const LayerDev& L, int o, int i, cons
 #pragma unroll
   for (int c = 0; c < EPT; ++c) {
     if (c < s.nv) {
-      s.p[c] = a.params[s.base + c];
+      s.p[c] = a.params[s.base + c * s.stride];
       if (MODE == PM_ADAM) {
-        s.m[c] = a.m[s.base + c];
-        s.v[c] = a.v[s.base + c];
+        s.m[c] = a.m[s.base + c * s.stride];
+        s.v[c] = a.v[s.base + c * s.stride];
       }
     }
   }
@@ -171,7 +173,7 @@ __device__ __forceinline__ typename VecF<EPT>::T applyn(PreN<EPT> s, typename Ve
   if (MODE == PM_GRAD) {
 #pragma unroll
     for (int c = 0; c < EPT; ++c)
-      if (c < s.nv) a.grads[s.base + c] = g[c];
+      if (c < s.nv) a.grads[s.base + c * s.stride] = g[c];
     return w;
   }
   if (MODE == PM_ADAM) {
@@ -194,9 +196,9 @@ __device__ __forceinline__ typename VecF<EPT>::T applyn(PreN<EPT> s, typename Ve
 #pragma unroll
       for (int c = 0; c < EPT; ++c) {
         if (c < s.nv) {
-          a.params[s.base + c] = s.p[c];
-          a.m[s.base + c] = s.m[c];
-          a.v[s.base + c] = s.v[c];
+          a.params[s.base + c * s.stride] = s.p[c];
+          a.m[s.base + c * s.stride] = s.m[c];
+          a.v[s.base + c * s.stride] = s.v[c];
         }
       }
     }
@@ -214,7 +216,7 @@ struct PreB {
 template <int MODE>
 __device__ __forceinline__ PreB loadb(const LayerDev& L, int o, const AdamArgs& a) {
   PreB b{0.f, 0.f, 0.f, -1};
-  if (o >= L.N) return b;
+  if (o >= L.N || !L.has_bias) return b;
   const int seg = (L.nseg == 2 && o >= L.seg_rows0) ? 1 : 0;
   b.idx = L.pb[seg] + (seg ? o - L.seg_rows0 : o);
   if (MODE == PM_GRAD) return b;
@@ -509,7 +511,7 @@ __device__ __forceinline__ void param_body(const LayerDev& L, const TileDesc& td
 #pragma unroll
     for (int c = 0; c < 4; ++c) g4[c] = c < st.nv ? aa.grads[st.base + c] * aa.grad_scale : 0.f;
     const int ob = td.o0 + tid;
-    if (td.i0 == 0 && tid < 32 && ob < L.N) {
+    if (td.i0 == 0 && tid < 32 && ob < L.N && L.has_bias) {
       const int seg = (L.nseg == 2 && ob >= L.seg_rows0) ? 1 : 0;
       db = aa.grads[L.pb[seg] + (seg ? ob - L.seg_rows0 : ob)] * aa.grad_scale;
     }
@@ -537,7 +539,8 @@ __global__ __launch_bounds__(CVAE_THREADS) void f8_scale_kernel(NetDev net, cons
   for (int j = threadIdx.x; j < n; j += CVAE_THREADS) {
     const int o = j / L.K, i = j - o * L.K;
     const int seg = (L.nseg == 2 && o >= L.seg_rows0) ? 1 : 0;
-    m = fmaxf(m, fabsf(params[L.pw[seg] + (int64_t)(seg ? o - L.seg_rows0 : o) * L.K + i]));
+    m = fmaxf(m, fabsf(params[L.wt ? L.pw[0] + (int64_t)i * L.N + o
+                                   : L.pw[seg] + (int64_t)(seg ? o - L.seg_rows0 : o) * L.K + i]));
   }
   __shared__ float red[CVAE_THREADS];
   red[threadIdx.x] = m;

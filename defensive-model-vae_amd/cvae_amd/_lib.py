@@ -16,7 +16,8 @@ c_i64p = C.POINTER(C.c_int64)
 
 class CvaeConfig(C.Structure):
     _fields_ = [("seq_len", C.c_int), ("dim", C.c_int), ("latent_dim", C.c_int), ("hidden_dim", C.c_int),
-                ("n_enc", C.c_int), ("n_dec", C.c_int), ("dtype", C.c_int), ("max_batch", C.c_int)]
+                ("n_enc", C.c_int), ("n_dec", C.c_int), ("dtype", C.c_int), ("max_batch", C.c_int),
+                ("n_classes", C.c_int), ("class_dim", C.c_int)]
 
 
 class CvaeLossWeights(C.Structure):
@@ -43,22 +44,24 @@ _SIGS = {
     "cvae_workspace_bytes": (_i, [_v, c_i64p]),
     "cvae_bucket_split": (_i, [_v, c_i64p]),
     "cvae_pack_weights": (_i, [_v, _v, _v]),
-    # h, x, idx, batch, xflags, start, eps, seed, offset, eps_row0, recon, mu, logvar, hc, eps_out, stream
-    "cvae_forward": (_i, [_v, _v, _v, _i, _i, _v, _v, _u64, _u64, _i64, _v, _v, _v, _v, _v, _v]),
+    # h, x, idx, classes, batch, xflags, start, eps, seed, offset, eps_row0, recon, mu, logvar, hc, eps_out, stream
+    "cvae_forward": (_i, [_v, _v, _v, _v, _i, _i, _v, _v, _u64, _u64, _i64, _v, _v, _v, _v, _v, _v]),
     "cvae_condition": (_i, [_v, _v, _i, _v, _v]),
-    "cvae_decode": (_i, [_v, _v, _v, _v, _i, _v, _v]),
-    # h, x, idx, batch, xflags, eps, seed, offset, eps_row0, w, grads, loss_out, loss_accum, counters, adam,
-    # parts, stream
-    "cvae_train_fwd_bwd": (_i, [_v, _v, _v, _i, _i, _v, _u64, _u64, _i64, _W, _v, _v, _v, _v, _A, _i, _v]),
-    # h, x, idx, batch, xflags, start, eps, seed, offset, eps_row0, d_recon, d_mu, d_logvar, d_hc, grads, stream
-    "cvae_backward": (_i, [_v, _v, _v, _i, _i, _v, _v, _u64, _u64, _i64, _v, _v, _v, _v, _v, _v]),
+    "cvae_decode": (_i, [_v, _v, _v, _v, _v, _i, _v, _v]),  # h, z, start, hc, classes, batch, out, stream
+    # h, x, idx, classes, batch, xflags, eps, seed, offset, eps_row0, w, grads, loss_out, loss_accum, counters,
+    # adam, parts, stream
+    "cvae_train_fwd_bwd": (_i, [_v, _v, _v, _v, _i, _i, _v, _u64, _u64, _i64, _W, _v, _v, _v, _v, _A, _i, _v]),
+    # h, x, idx, classes, batch, xflags, start, eps, seed, offset, eps_row0, d_recon, d_mu, d_logvar, d_hc, grads,
+    # stream
+    "cvae_backward": (_i, [_v, _v, _v, _v, _i, _i, _v, _v, _u64, _u64, _i64, _v, _v, _v, _v, _v, _v]),
     # h, params, grads, m, v, step, adam, grad_scale, counters, stream
     "cvae_adam": (_i, [_v, _v, _v, _v, _v, _i64, _A, _f, _v, _v]),
-    # h, x, idx, batch, xflags, eps, seed, offset, eps_row0, w, params, m, v, step, adam, loss_out, loss_accum,
-    # counters, stream
-    "cvae_train_step": (_i, [_v, _v, _v, _i, _i, _v, _u64, _u64, _i64, _W, _v, _v, _v, _i64, _A, _v, _v, _v, _v]),
-    "cvae_train_steps": (_i, [_v, _v, _v, _i, _i, _i, _v, _u64, _u64, _i64, _W, _v, _v, _v, _i64, _A, _v, _v, _v,
-                              _v]),
+    # h, x, idx, classes, batch, xflags, eps, seed, offset, eps_row0, w, params, m, v, step, adam, loss_out,
+    # loss_accum, counters, stream
+    "cvae_train_step": (_i, [_v, _v, _v, _v, _i, _i, _v, _u64, _u64, _i64, _W, _v, _v, _v, _i64, _A, _v, _v, _v,
+                             _v]),
+    "cvae_train_steps": (_i, [_v, _v, _v, _v, _i, _i, _i, _v, _u64, _u64, _i64, _W, _v, _v, _v, _i64, _A, _v, _v,
+                              _v, _v]),
     "cvae_bench_kernels": (_i, [_v, _v, _v, _i, _i, _v, _v, _v, _i64, C.POINTER(_f), _v]),
     "cvae_sync_words": (_i, [_v, C.POINTER(C.c_uint)]),
     "cvae_loss": (_i, [_v, _v, _v, _v, _i, _i, _i, _i, _W, _v, _v, _v]),

@@ -93,7 +93,7 @@ class DataParallelStep:
             dist.broadcast(self.engine.params, src, group=self.group)
             self.engine.pack()
 
-    def step(self, x, idx=None, eps=None, batch=None, global_batch=None, weights=None, row0=None):
+    def step(self, x, idx=None, eps=None, batch=None, global_batch=None, weights=None, row0=None, classes=None):
         """One data-parallel training step; ``batch`` = this rank's rows, ``global_batch`` = Σ over
         ranks, ``row0`` = this rank's first row in the global batch (default: rank · batch)."""
         eng = self.engine
@@ -106,12 +106,14 @@ class DataParallelStep:
             row0 = self.rank * batch
         if not self.split:
             if batch > 0:
-                eng.train_step(x, idx=idx, eps=eps, batch=batch, weights=weights, row0=row0)
+                eng.train_step(x, idx=idx, eps=eps, batch=batch, weights=weights, row0=row0,
+                               **({"classes": classes} if classes is not None else {}))
             return eng.loss
         two = self.buckets == 2  # every rank issues the same collectives, empty shares included
         if batch > 0:
             parts = 3 if two else 7  # CVAE_PART_CHAIN | DW_DEC, or CVAE_PART_ALL
-            eng.forward_backward(x, idx=idx, eps=eps, batch=batch, weights=weights, row0=row0, parts=parts)
+            eng.forward_backward(x, idx=idx, eps=eps, batch=batch, weights=weights, row0=row0, parts=parts,
+                                 **({"classes": classes} if classes is not None else {}))
             ragged = batch * self.world_size != global_batch
             scale = 1.0 if ragged else 1.0 / self.world_size
         else:  # an empty share of a ragged last batch still joins the collectives

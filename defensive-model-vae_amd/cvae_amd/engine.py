@@ -33,9 +33,11 @@ DTYPES = {"fp32": (CVAE_F32, torch.float32), "bf16": (CVAE_BF16, torch.bfloat16)
 DEFAULT_WEIGHTS = (0.1, 0.1, 1.0, 1.0)  # Training_VAE.py:300-306
 
 
-def config_info(seq_len, dim, latent_dim, hidden_dim=128, n_enc=4, n_dec=4, dtype="fp32", max_batch=1):
+def config_info(seq_len, dim, latent_dim, hidden_dim=128, n_enc=4, n_dec=4, dtype="fp32", max_batch=1,
+                n_classes=0, class_dim=0):
     """Host-only query: (n_params, n_tensors, lds_bytes) — works without a GPU."""
-    cfg = CvaeConfig(seq_len, dim, latent_dim, hidden_dim, n_enc, n_dec, DTYPES[dtype][0], max_batch)
+    cfg = CvaeConfig(seq_len, dim, latent_dim, hidden_dim, n_enc, n_dec, DTYPES[dtype][0], max_batch, n_classes,
+                     class_dim)
     n = C.c_int64()
     nt = C.c_int()
     lds = C.c_int()
@@ -45,7 +47,7 @@ def config_info(seq_len, dim, latent_dim, hidden_dim=128, n_enc=4, n_dec=4, dtyp
 
 class CVAEEngine:
     def __init__(self, seq_len, dim, latent_dim, hidden_dim=128, n_enc=4, n_dec=4, dtype="fp32",
-                 max_batch=1024, device=None, seed=0):
+                 max_batch=1024, device=None, seed=0, n_classes=0, class_dim=0):
         if not torch.cuda.is_available():
             raise RuntimeError("CVAEEngine needs a HIP device (MI355X); there is no CPU fallback")
         self.device = torch.device(device if device is not None else "cuda")
@@ -54,8 +56,10 @@ class CVAEEngine:
         self.dtype_name = dtype
         self.cdtype, self.tdtype = DTYPES[dtype]
         self.shape = (seq_len, dim, latent_dim, hidden_dim, n_enc, n_dec)
+        self.n_classes, self.class_dim = int(n_classes), int(class_dim)
         self.max_batch = max_batch
-        cfg = CvaeConfig(seq_len, dim, latent_dim, hidden_dim, n_enc, n_dec, self.cdtype, max_batch)
+        cfg = CvaeConfig(seq_len, dim, latent_dim, hidden_dim, n_enc, n_dec, self.cdtype, max_batch, self.n_classes,
+                         self.class_dim)
         h = C.c_void_p()
         with torch.cuda.device(self.device):
             check(lib().cvae_create(C.byref(cfg), self.device.index, C.byref(h)), "cvae_create")
@@ -236,6 +240,21 @@ class CVAEEngine:
             raise ValueError(f"eps must be ({batch},{self.shape[2]})")
         return eps
 
+    def _classes(self, classes, n_rows):
+        """int32 class ids per row of x on the device (cfg4); None for the reference model."""
+        if not self.n_classes:
+            if classes is not None:
+                raise ValueError("this model has no class embedding (n_classes=0)")
+            return None
+        if classes is None:
+            raise ValueError(f"a class-embedding model (n_classes={self.n_classes}) needs class ids per row")
+        c = torch.as_tensor(classes)
+        if c.device.type == "cpu" and c.numel() and (int(c.min()) < 0 or int(c.max()) >= self.n_classes):
+            raise IndexError(f"class id out of range [0, {self.n_classes})")
+        if c.numel() < n_rows:
+            raise ValueError(f"{c.numel()} class ids for {n_rows} rows")
+        return c.to(device=self.device, dtype=torch.int32).contiguous()
+
     def _weights(self, weights):
         w = self.weights if weights is None else weights
         return CvaeLossWeights(*[float(v) for v in w])
@@ -248,7 +267,7 @@ class CVAEEngine:
         return x, idx, B
 
     # ------------------------------------------------------------------ training
-    def train_step(self, x, idx=None, eps=None, batch=None, weights=None, accumulate=True, row0=0):
+    def train_step(self, x, idx=None, eps=None, batch=None, weights=None, accumulate=True, row0=0, classes=None):
         """Fused step (fwd + loss + bwd + Adam) — Training_VAE.py:345-370 for one batch.
 
         ``x``: (B,S,D) absolute trajectories, or the whole dataset with ``idx`` the rows.
@@ -257,18 +276,20 @@ class CVAEEngine:
         """
         x, idx, B = self._prep(x, idx, batch)
         e = self._eps(eps, B)
+        cl = self._classes(classes, x.shape[0])
         self.ensure_packed()
         w = self._weights(weights)
         a = self._adam()
         check(lib().cvae_train_step(
-            self._h, ptr(x), ptr(idx), B, self._xflags(x), ptr(e), self.seed, 0, int(row0), C.byref(w),
+            self._h, ptr(x), ptr(idx), ptr(cl), B, self._xflags(x), ptr(e), self.seed, 0, int(row0), C.byref(w),
             ptr(self.params), ptr(self.m), ptr(self.v), 0, C.byref(a), ptr(self.loss),
             ptr(self.loss_accum) if accumulate else None, ptr(self.counters), self._stream()), "cvae_train_step")
         self._ctr[0] += 1
         self._ctr[1] += 1
         return self.loss
 
-    def train_steps(self, x, n_steps, idx=None, eps=None, batch=None, weights=None, accumulate=True, row0=0):
+    def train_steps(self, x, n_steps, idx=None, eps=None, batch=None, weights=None, accumulate=True, row0=0,
+                    classes=None):
         """``n_steps`` fused steps in one C call (cvae_train_steps): the loop body of
         Training_VAE.py:340-370 over a run of equal-size batches, with no host work per step.
 
@@ -290,11 +311,12 @@ class CVAEEngine:
             e = torch.as_tensor(eps).to(device=self.device, dtype=torch.float32).contiguous()
             if e.shape != (n_steps * B, self.shape[2]):
                 raise ValueError(f"eps must be ({n_steps * B},{self.shape[2]})")
+        cl = self._classes(classes, x.shape[0])
         self.ensure_packed()
         w = self._weights(weights)
         a = self._adam()
         check(lib().cvae_train_steps(
-            self._h, ptr(x), ptr(idx), B, n_steps, self._xflags(x), ptr(e), self.seed, 0, int(row0), C.byref(w),
+            self._h, ptr(x), ptr(idx), ptr(cl), B, n_steps, self._xflags(x), ptr(e), self.seed, 0, int(row0), C.byref(w),
             ptr(self.params), ptr(self.m), ptr(self.v), 0, C.byref(a), ptr(self.loss),
             ptr(self.loss_accum) if accumulate else None, ptr(self.counters), self._stream()), "cvae_train_steps")
         self._ctr[0] += n_steps
@@ -302,18 +324,19 @@ class CVAEEngine:
         return self.loss
 
     def forward_backward(self, x, idx=None, eps=None, batch=None, weights=None, accumulate=True, row0=0,
-                         parts=CVAE_PART_ALL):
+                         parts=CVAE_PART_ALL, classes=None):
         """fwd + loss + bwd into ``self.grads`` (means over this batch) — the DP half-step.
 
         ``parts``: CVAE_PART_ALL, or CHAIN|DW_DEC then (separately) ``wgrad_rest()`` — the two-bucket
         split that lets the decoder bucket's all-reduce run beside the rest of the dW GEMMs."""
         x, idx, B = self._prep(x, idx, batch)
         e = self._eps(eps, B)
+        cl = self._classes(classes, x.shape[0])
         self.ensure_packed()
         w = self._weights(weights)
         a = self._adam()
         check(lib().cvae_train_fwd_bwd(
-            self._h, ptr(x), ptr(idx), B, self._xflags(x), ptr(e), self.seed, 0, int(row0), C.byref(w),
+            self._h, ptr(x), ptr(idx), ptr(cl), B, self._xflags(x), ptr(e), self.seed, 0, int(row0), C.byref(w),
             ptr(self.grads), ptr(self.loss), ptr(self.loss_accum) if accumulate else None, ptr(self.counters),
             C.byref(a), int(parts), self._stream()), "cvae_train_fwd_bwd")
         self._ctr[0] += 1
@@ -326,7 +349,7 @@ class CVAEEngine:
         ``forward_backward(parts=CHAIN|DW_DEC)`` ran."""
         B = int(batch if batch is not None else self._last_batch)
         check(lib().cvae_train_fwd_bwd(
-            self._h, None, None, B, 0, None, 0, 0, 0, None, ptr(self.grads), None, None, None, None,
+            self._h, None, None, None, B, 0, None, 0, 0, 0, None, ptr(self.grads), None, None, None, None,
             CVAE_PART_DW_REST, self._stream()), "cvae_train_fwd_bwd(rest)")
 
     def adam_step(self, grad_scale=1.0):
@@ -345,12 +368,13 @@ class CVAEEngine:
 
     # ------------------------------------------------------------------ inference / autograd
     def forward(self, x, start=None, idx=None, eps=None, batch=None, outputs=("recon", "mu", "logvar", "hc"),
-                row0=0, offset=None):
+                row0=0, offset=None, classes=None):
         """Training_VAE.py:217-226.  start=None: x absolute (transform in-kernel); else x relative.
         eps None: in-kernel Philox at ``offset`` (default: the next host offset, then advanced)."""
         S, D, Z, H = self.shape[:4]
         x, idx, B = self._prep(x, idx, batch)
         e = self._eps(eps, B)
+        cl = self._classes(classes, x.shape[0])
         self.ensure_packed()
         st = None
         if start is not None:
@@ -364,14 +388,15 @@ class CVAEEngine:
                "logvar": torch.empty(B, Z, **kw) if "logvar" in outputs else None,
                "hc": torch.empty(B, H, **kw) if "hc" in outputs else None,
                "eps": torch.empty(B, Z, **kw) if "eps" in outputs else None}
-        check(lib().cvae_forward(self._h, ptr(x), ptr(idx), B, self._xflags(x), ptr(st), ptr(e), self.seed,
+        check(lib().cvae_forward(self._h, ptr(x), ptr(idx), ptr(cl), B, self._xflags(x), ptr(st), ptr(e), self.seed,
                                  int(offset), int(row0), ptr(out["recon"]), ptr(out["mu"]), ptr(out["logvar"]),
                                  ptr(out["hc"]), ptr(out["eps"]), self._stream()), "cvae_forward")
         if "eps" in outputs:
             return out["recon"], out["mu"], out["logvar"], out["hc"], out["eps"]
         return out["recon"], out["mu"], out["logvar"], out["hc"]
 
-    def backward(self, x, start, eps, offset, d_recon, d_mu=None, d_logvar=None, d_hc=None, row0=0, grads=None):
+    def backward(self, x, start, eps, offset, d_recon, d_mu=None, d_logvar=None, d_hc=None, row0=0, grads=None,
+                 classes=None):
         """Gradient of the forward (x relative, start, eps / Philox offset) w.r.t. every parameter from
         the output gradients (cvae_backward: recompute + backward).  Writes ``grads`` (default a
         fresh flat buffer) and returns it."""
@@ -379,11 +404,12 @@ class CVAEEngine:
         st = None if start is None else torch.as_tensor(start).to(device=self.device,
                                                                     dtype=torch.float32).contiguous()
         e = self._eps(eps, B)
+        cl = self._classes(classes, B)
         f = lambda t: None if t is None else t.to(device=self.device, dtype=torch.float32).contiguous()  # noqa: E731
         out = torch.empty(self.n_params, device=self.device, dtype=torch.float32) if grads is None else grads
         self.ensure_packed()
         dr, dm, dl, dh = f(d_recon), f(d_mu), f(d_logvar), f(d_hc)
-        check(lib().cvae_backward(self._h, ptr(x), None, B, self._xflags(x), ptr(st), ptr(e), self.seed, int(offset),
+        check(lib().cvae_backward(self._h, ptr(x), None, ptr(cl), B, self._xflags(x), ptr(st), ptr(e), self.seed, int(offset),
                                   int(row0), ptr(dr), ptr(dm), ptr(dl), ptr(dh), ptr(out), self._stream()),
               "cvae_backward")
         return out
@@ -397,16 +423,17 @@ class CVAEEngine:
         check(lib().cvae_condition(self._h, ptr(st), B, ptr(hc), self._stream()), "cvae_condition")
         return hc
 
-    def decode(self, z, start=None, hc=None):
+    def decode(self, z, start=None, hc=None, classes=None):
         """decode(z, h_c) (Training_VAE.py:208-215) or decode from absolute start points."""
         S, D, Z, H = self.shape[:4]
         z = torch.as_tensor(z).to(device=self.device, dtype=torch.float32).contiguous()
         B = z.shape[0]
         st = None if start is None else torch.as_tensor(start).to(device=self.device, dtype=torch.float32).contiguous()
         h = None if hc is None else torch.as_tensor(hc).to(device=self.device, dtype=torch.float32).contiguous()
+        cl = self._classes(classes, B)
         out = torch.empty(B, S, D, device=self.device, dtype=torch.float32)
         self.ensure_packed()
-        check(lib().cvae_decode(self._h, ptr(z), ptr(st), ptr(h), B, ptr(out), self._stream()), "cvae_decode")
+        check(lib().cvae_decode(self._h, ptr(z), ptr(st), ptr(h), ptr(cl), B, ptr(out), self._stream()), "cvae_decode")
         return out
 
     # ------------------------------------------------------------------ timing
@@ -428,6 +455,8 @@ class CVAEEngine:
         """{'rowchain', 'wgrad_adam', 'step'}: average device ms of ``reps`` back-to-back launches
         (cvae_bench_kernels; synchronises; updates params like training steps)."""
         x, idx, B = self._prep(x, idx, batch)
+        if self.n_classes:
+            raise ValueError("bench_kernels measures the reference model (n_classes=0)")
         ms = (C.c_float * 3)()
         check(lib().cvae_bench_kernels(self._h, ptr(x), ptr(idx), B, int(reps), ptr(self.params), ptr(self.m),
                                        ptr(self.v), self.step_count + 1, ms, self._stream()), "cvae_bench_kernels")

@@ -41,18 +41,18 @@ class _ForwardFn(torch.autograd.Function):
     output gradients to every parameter (cvae_backward)."""
 
     @staticmethod
-    def forward(ctx, eng, x, start, eps, offset, *params):
-        recon, mu, lv, hc = eng.forward(x, start=start, eps=eps, offset=offset)
+    def forward(ctx, eng, x, start, eps, offset, classes, *params):
+        recon, mu, lv, hc = eng.forward(x, start=start, eps=eps, offset=offset, classes=classes)
         ctx.eng, ctx.offset = eng, offset
-        ctx.save_for_backward(x, start, eps)
+        ctx.save_for_backward(x, start, eps, classes)
         return recon, mu, lv, hc
 
     @staticmethod
     def backward(ctx, d_recon, d_mu, d_lv, d_hc):
-        x, start, eps = ctx.saved_tensors
+        x, start, eps, classes = ctx.saved_tensors
         eng = ctx.eng
-        flat = eng.backward(x, start, eps, ctx.offset, d_recon, d_mu, d_lv, d_hc)
-        return (None, None, None, None, None, *eng.views(flat))
+        flat = eng.backward(x, start, eps, ctx.offset, d_recon, d_mu, d_lv, d_hc, classes=classes)
+        return (None, None, None, None, None, None, *eng.views(flat))
 
 
 class _LossFn(torch.autograd.Function):
@@ -111,24 +111,35 @@ class _ConditionEncoder(nn.Sequential):
 
 
 class ConditionalTrajectoryVAE(nn.Module):
-    def __init__(self, seq_len, dim, latent_dim, hidden_dim=128, n_enc=4, n_dec=4):
+    """Training_VAE.py:118-226.  n_enc/n_dec generalise the 4+4 depth (BASELINE cfg5).
+
+    n_classes > 0 (BASELINE cfg4, a build-side extension the reference does not have): a scenario
+    class embedding ``class_embedding = nn.Embedding(n_classes, class_dim)`` whose row e joins both
+    concatenations beside h_c — fc input [h_traj ‖ h_c ‖ e] (:193) and decoder input
+    [z ‖ h_c ‖ e] (:214).  It is registered last, so the reference's 24 keys and init stream come
+    first; its parity is pinned to the extended oracle, not to the reference."""
+
+    def __init__(self, seq_len, dim, latent_dim, hidden_dim=128, n_enc=4, n_dec=4, n_classes=0, class_dim=16):
         super().__init__()
         self.seq_len, self.dim, self.latent_dim, self.hidden_dim = seq_len, dim, latent_dim, hidden_dim
         self.n_enc, self.n_dec = n_enc, n_dec
-        H, I, Z = hidden_dim, seq_len * dim, latent_dim
+        self.n_classes, self.class_dim = int(n_classes), (int(class_dim) if n_classes else 0)
+        H, I, Z, E = hidden_dim, seq_len * dim, latent_dim, self.class_dim
         # module order = reference order (init RNG stream and state_dict keys)
         self.condition_encoder = _ConditionEncoder(nn.Linear(2, H), nn.ReLU(), nn.Linear(H, H), nn.ReLU())
         enc = [nn.Flatten()]
         for i in range(n_enc):
             enc += [nn.Linear(I if i == 0 else H, H), nn.ReLU()]
         self.encoder = nn.Sequential(*enc)
-        self.fc_mu = nn.Linear(H + H, Z)
-        self.fc_logvar = nn.Linear(H + H, Z)
+        self.fc_mu = nn.Linear(H + H + E, Z)
+        self.fc_logvar = nn.Linear(H + H + E, Z)
         dec = []
         for i in range(n_dec - 1):
-            dec += [nn.Linear(Z + H if i == 0 else H, H), nn.ReLU()]
+            dec += [nn.Linear(Z + H + E if i == 0 else H, H), nn.ReLU()]
         dec += [nn.Linear(H, I), nn.Unflatten(1, (seq_len, dim))]
         self.decoder = nn.Sequential(*dec)
+        if self.n_classes:
+            self.class_embedding = nn.Embedding(self.n_classes, E)
         self.__dict__["_engine"] = None
         self.condition_encoder.__dict__["_owner"] = weakref.ref(self)
 
@@ -136,7 +147,8 @@ class ConditionalTrajectoryVAE(nn.Module):
     def attach(self, dtype="fp32", max_batch=1024, device=None, seed=0):
         """Create the HIP engine and make the parameters views of its flat buffer."""
         eng = CVAEEngine(self.seq_len, self.dim, self.latent_dim, self.hidden_dim, self.n_enc, self.n_dec,
-                         dtype=dtype, max_batch=max_batch, device=device, seed=seed)
+                         dtype=dtype, max_batch=max_batch, device=device, seed=seed, n_classes=self.n_classes,
+                         class_dim=self.class_dim)
         eng.bind(self)
         self.__dict__["_engine"] = eng
         return eng
@@ -157,18 +169,19 @@ class ConditionalTrajectoryVAE(nn.Module):
     def get_start_points(self, x):  # Training_VAE.py:169-178
         return x[:, 0, 1:3]
 
-    def encode(self, x, start_points):  # :180-197
-        _, mu, logvar, hc = _need(self).forward(x, start=start_points, outputs=("mu", "logvar", "hc"))
+    def encode(self, x, start_points, classes=None):  # :180-197
+        _, mu, logvar, hc = _need(self).forward(x, start=start_points, outputs=("mu", "logvar", "hc"),
+                                                classes=classes)
         return mu, logvar, hc
 
     def reparameterize(self, mu, logvar):  # :199-206 (elementwise helper; the training path fuses it)
         std = torch.exp(0.5 * logvar)
         return mu + torch.randn_like(std) * std
 
-    def decode(self, z, condition):  # :208-215 — condition = h_c features
-        return _need(self).decode(z, hc=condition)
+    def decode(self, z, condition, classes=None):  # :208-215 — condition = h_c features
+        return _need(self).decode(z, hc=condition, classes=classes)
 
-    def forward(self, x, start_points, eps=None):  # :217-226 (x relative, start absolute)
+    def forward(self, x, start_points, eps=None, classes=None):  # :217-226 (x relative, start absolute)
         """model(batch_rel, start_points) → (recon, mu, logvar, h_c), autograd-tracked.
 
         eps (the reparameterisation noise, :205): None draws ``torch.randn(B, Z)`` from the global
@@ -189,15 +202,16 @@ class ConditionalTrajectoryVAE(nn.Module):
             eps = torch.as_tensor(eps).to(device=eng.device, dtype=torch.float32).contiguous()
         x = eng.as_input(x, keep_f32=True).detach()
         start = torch.as_tensor(start_points).to(device=eng.device, dtype=torch.float32).contiguous().detach()
-        return _ForwardFn.apply(eng, x, start, eps, offset, *self.parameters())
+        cl = eng._classes(classes, B)
+        return _ForwardFn.apply(eng, x, start, eps, offset, cl, *self.parameters())
 
-    def generate(self, start_points, z=None, generator=None):
+    def generate(self, start_points, z=None, generator=None, classes=None):
         """Batched sampling (Tools.py:18-65): z ~ N(0,I); returns (relative, absolute) trajectories."""
         eng = _need(self)
         st = torch.as_tensor(start_points, dtype=torch.float32, device=eng.device).reshape(-1, 2)
         if z is None:
             z = torch.randn(st.shape[0], self.latent_dim, device=eng.device, generator=generator)
-        rel = eng.decode(z, start=st)
+        rel = eng.decode(z, start=st, classes=classes)
         ab = rel.clone()
         ab[:, :, 1:3] += st[:, None, :]
         return rel, ab

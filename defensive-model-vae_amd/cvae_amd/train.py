@@ -105,10 +105,13 @@ def save_checkpoint(path, model, eng, epoch, loss_history):
 def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidden_dim=128,
           weights=(0.1, 0.1, 1.0, 1.0), model_save_path=None, loss_save_path=None, dtype="fp32",
           eps="host", device=None, seed=None, engine_seed=0, log=print, model=None, buckets=1,
-          checkpoint_path=None, resume=None):
+          checkpoint_path=None, resume=None, classes=None, class_dim=16):
     """Train like ``python Training_VAE.py`` (mode='training').
 
-    data: path to the (N, seq_len, dim) ``.npy`` (TrajectoryDataset, :105-115) or an array.
+    data: path to the (N, seq_len, dim) ``.npy`` (TrajectoryDataset, :105-115) or an array; or a
+    LIST of paths (scenes) — their rows are concatenated and, with ``class_dim`` > 0, each row's
+    class is its file's index (BASELINE cfg4: one model over the Town04/Town05 scenes).
+    classes: per-row class ids (cfg4 class embedding, ``class_dim`` wide); None = the reference model.
     weights: (recon, kld, start, time) — the values of :300-306.
     seed: if given, ``torch.manual_seed(seed)`` first (the reference leaves it unseeded).
     Under ``torch.distributed`` every rank runs this with the same arguments; batch_size is
@@ -124,7 +127,12 @@ def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidd
     if seed is not None:
         torch.manual_seed(seed)
     rank, world_size = dp.world()
-    if isinstance(data, (str, os.PathLike)):
+    if isinstance(data, (list, tuple)) and data and isinstance(data[0], (str, os.PathLike)):
+        parts = [TrajectoryDataset(p).data for p in data]
+        arr = np.ascontiguousarray(np.concatenate(parts, 0))
+        if classes is None and class_dim:
+            classes = np.concatenate([np.full(len(a), i, np.int32) for i, a in enumerate(parts)])
+    elif isinstance(data, (str, os.PathLike)):
         arr = TrajectoryDataset(data).data
     else:
         arr = np.ascontiguousarray(np.asarray(data, dtype=np.float32))
@@ -132,8 +140,15 @@ def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidd
     if rank == 0 and log:
         log(f"Training parameters: seq_len={seq_len}, latent_dim={latent_dim}, batch_size={batch_size}, lr={lr}")
         log(f"Dataset size: {n} trajectories")
-    if model is None:
-        model = ConditionalTrajectoryVAE(seq_len, dim, latent_dim, hidden_dim)  # init from the global RNG
+    n_classes = 0
+    if classes is not None:
+        classes = np.ascontiguousarray(np.asarray(classes, dtype=np.int32))
+        if classes.shape != (n,):
+            raise ValueError(f"classes must hold one id per trajectory ({n}), got {classes.shape}")
+        n_classes = int(classes.max()) + 1
+    if model is None:  # init from the global RNG
+        model = ConditionalTrajectoryVAE(seq_len, dim, latent_dim, hidden_dim, n_classes=n_classes,
+                                         class_dim=class_dim)
     eng = model.__dict__.get("_engine") or model.attach(dtype=dtype, max_batch=batch_size, device=device,
                                                         seed=engine_seed)
     if eng.max_batch < batch_size:
@@ -144,6 +159,7 @@ def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidd
     step = dp.DataParallelStep(eng, buckets=buckets)
     step.broadcast_params()
     x_dev = eng.as_input(torch.from_numpy(arr), keep_f32=True)  # resident for the whole run
+    cls_dev = None if classes is None else torch.from_numpy(classes).to(x_dev.device)
     Z = latent_dim
     gb = batch_size * world_size
     loader = torch.utils.data.DataLoader(_Rows(n), batch_size=gb, shuffle=True)
@@ -171,7 +187,7 @@ def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidd
                 e = e_all[lo:hi]
             elif eps != "philox":
                 raise ValueError("eps must be 'host' or 'philox'")
-            step.step(x_dev, idx=rows[lo:hi], eps=e, batch=hi - lo, global_batch=g, row0=lo)
+            step.step(x_dev, idx=rows[lo:hi], eps=e, batch=hi - lo, global_batch=g, row0=lo, classes=cls_dev)
         sums = step.epoch_loss_sums().double().cpu().numpy()  # the only host sync of the epoch
         means = sums / n
         for k, v in zip(LOSS_KEYS, means):
@@ -211,7 +227,11 @@ def main(argv=None):
     0.1/0.1/1.0/1.0).  Under ``torch.distributed.run`` every rank trains its share over RCCL."""
     import argparse
     ap = argparse.ArgumentParser(description=main.__doc__)
-    ap.add_argument("--data", required=True, help="(N, seq_len, dim) .npy (Traj_Data_Process output)")
+    ap.add_argument("--data", required=True, nargs="+",
+                    help="(N, seq_len, dim) .npy (Traj_Data_Process output); several = several scenes")
+    ap.add_argument("--class-dim", type=int, default=0,
+                    help="BASELINE cfg4: with several --data files, a scene-class embedding this wide (the "
+                         "file index is the class)")
     ap.add_argument("--seq-len", type=int, default=10)
     ap.add_argument("--dim", type=int, default=3)
     ap.add_argument("--latent", type=int, default=8)
@@ -230,7 +250,7 @@ def main(argv=None):
     ap.add_argument("--resume", default=None, help="continue from a --checkpoint file (--epochs = total)")
     ap.add_argument("--loss-out", default=None)
     a = ap.parse_args(argv)
-    model_out, loss_out = default_paths(a.data, a.latent, a.epochs)
+    model_out, loss_out = default_paths(a.data[0], a.latent, a.epochs)
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     device = None
     if world_size > 1:
@@ -241,10 +261,11 @@ def main(argv=None):
         device = torch.device("cuda", local)
         tdist.init_process_group("nccl", device_id=device)
     try:
-        train(a.data, a.seq_len, a.dim, a.latent, batch_size=a.batch_size, lr=a.lr, epochs=a.epochs,
+        data = a.data if len(a.data) > 1 else a.data[0]
+        train(data, a.seq_len, a.dim, a.latent, batch_size=a.batch_size, lr=a.lr, epochs=a.epochs,
               hidden_dim=a.hidden, weights=tuple(a.weights), model_save_path=a.model_out or model_out,
               loss_save_path=a.loss_out or loss_out, dtype=a.dtype, eps=a.eps, device=device, seed=a.seed,
-              checkpoint_path=a.checkpoint, resume=a.resume)
+              checkpoint_path=a.checkpoint, resume=a.resume, class_dim=a.class_dim if len(a.data) > 1 else 0)
     finally:
         if world_size > 1:
             torch.distributed.destroy_process_group()

@@ -79,6 +79,10 @@ typedef struct cvae_config {
   int n_dec;       /* Linear layers in `decoder`  (reference: 4) */
   int dtype;       /* cvae_dtype: GEMM operand / activation type; master weights, Adam and loss are fp32 */
   int max_batch;   /* rows per call the workspace is sized for */
+  int n_classes;   /* BASELINE cfg4: scenario classes of the class embedding (0 = the reference model) */
+  int class_dim;   /* width of the class embedding (a multiple of 4), concatenated beside h_c in the fc
+                      input [h_traj ‖ h_c ‖ e] and the decoder input [z ‖ h_c ‖ e] (Training_VAE.py:193, :214);
+                      its table is the LAST parameter tensor, nn.Embedding layout (n_classes, class_dim) */
 } cvae_config;
 
 typedef struct cvae_handle cvae_handle;
@@ -143,13 +147,14 @@ int cvae_pack_weights(cvae_handle* h, const float* params, void* stream);
  *          model(batch_rel, start_points) at :352) and start fp32 (batch,2) is
  *          the condition.
  *   idx    optional int64[batch] row gather into x (NULL = rows 0..batch-1)
+ *   classes cfg4 only: int32 class id per row of x (gathered by idx like x; NULL = class 0)
  *   eps    optional fp32 (batch,Z); NULL = in-kernel Philox(seed, offset) keyed by the global
  *          row eps_row0 + b (a data-parallel rank passes its first global row, so the ranks of
  *          a global batch draw what one process with that batch draws)
  *   recon  fp32 (batch,S,D) relative trajectories; mu, logvar fp32 (batch,Z);
  *   hc     fp32 (batch,H) condition features; eps_out fp32 (batch,Z) the eps each row used
  *          (any output may be NULL).                                                           */
-int cvae_forward(cvae_handle* h, const void* x, const int64_t* idx, int batch, int xflags,
+int cvae_forward(cvae_handle* h, const void* x, const int64_t* idx, const int32_t* classes, int batch, int xflags,
                  const float* start, const float* eps, uint64_t seed, uint64_t offset, int64_t eps_row0,
                  float* recon, float* mu, float* logvar, float* hc, float* eps_out, void* stream);
 
@@ -163,9 +168,10 @@ int cvae_condition(cvae_handle* h, const float* start, int batch, float* hc, voi
  *   z fp32 (batch,Z); exactly the condition given:
  *     hc    fp32 (batch,H) condition features (decode(z, h_c) semantics), or
  *     start fp32 (batch,2) absolute start points (condition encoder fused in);
+ *   classes (cfg4) int32 (batch) class ids;
  *   out fp32 (batch,S,D) relative trajectories (caller adds start for global). */
-int cvae_decode(cvae_handle* h, const float* z, const float* start, const float* hc, int batch,
-                float* out, void* stream);
+int cvae_decode(cvae_handle* h, const float* z, const float* start, const float* hc, const int32_t* classes,
+                int batch, float* out, void* stream);
 
 /* Forward + conditional_vae_loss + full backward for one batch, gradients into
  * the flat fp32 `grads` (overwritten, same layout as params).  Replaces
@@ -179,7 +185,8 @@ int cvae_decode(cvae_handle* h, const float* z, const float* start, const float*
  * on the same batch (the two-bucket overlap; loss and counters advance in the first call).
  * counters + adam (nullable): the step this call begins, with its Adam scalars precomputed for the
  * cvae_adam(counters) that completes it — a data-parallel step is capturable as one graph. */
-int cvae_train_fwd_bwd(cvae_handle* h, const void* x, const int64_t* idx, int batch, int xflags,
+int cvae_train_fwd_bwd(cvae_handle* h, const void* x, const int64_t* idx, const int32_t* classes, int batch,
+                       int xflags,
                        const float* eps, uint64_t seed, uint64_t offset, int64_t eps_row0,
                        const cvae_loss_weights* w, float* grads, float* loss_out, double* loss_accum,
                        uint64_t* counters, const cvae_adam_config* adam, int parts, void* stream);
@@ -190,7 +197,7 @@ int cvae_train_fwd_bwd(cvae_handle* h, const void* x, const int64_t* idx, int ba
  * Philox(seed, offset, eps_row0)) — bit-identical to the cvae_forward that produced the
  * outputs — and back-propagates d_recon fp32 (batch,S,D), d_mu / d_logvar fp32 (batch,Z) and
  * d_hc fp32 (batch,H) (any may be NULL = zero) into the flat fp32 `grads` (overwritten). */
-int cvae_backward(cvae_handle* h, const void* x, const int64_t* idx, int batch, int xflags,
+int cvae_backward(cvae_handle* h, const void* x, const int64_t* idx, const int32_t* classes, int batch, int xflags,
                   const float* start, const float* eps, uint64_t seed, uint64_t offset, int64_t eps_row0,
                   const float* d_recon, const float* d_mu, const float* d_logvar, const float* d_hc,
                   float* grads, void* stream);
@@ -206,7 +213,7 @@ int cvae_adam(cvae_handle* h, float* params, const float* grads, float* m, float
 /* Fused single-device step: cvae_train_fwd_bwd + cvae_adam with the weight
  * gradient GEMMs and Adam in one kernel (the gradient never round-trips HBM).
  * Replaces the whole body of Training_VAE.py:345-370 for one batch. */
-int cvae_train_step(cvae_handle* h, const void* x, const int64_t* idx, int batch, int xflags,
+int cvae_train_step(cvae_handle* h, const void* x, const int64_t* idx, const int32_t* classes, int batch, int xflags,
                     const float* eps, uint64_t seed, uint64_t offset, int64_t eps_row0,
                     const cvae_loss_weights* w, float* params, float* m, float* v, int64_t step,
                     const cvae_adam_config* adam, float* loss_out, double* loss_accum,
@@ -219,7 +226,8 @@ int cvae_train_step(cvae_handle* h, const void* x, const int64_t* idx, int batch
  * Training_VAE.py:340-370 for a run of equal-size batches (an epoch's permutation uploaded
  * once); loss_out = the last step's losses, loss_accum += every step's loss * batch.  No host
  * work per step beyond the two kernel launches. */
-int cvae_train_steps(cvae_handle* h, const void* x, const int64_t* idx, int batch, int n_steps, int xflags,
+int cvae_train_steps(cvae_handle* h, const void* x, const int64_t* idx, const int32_t* classes, int batch,
+                     int n_steps, int xflags,
                      const float* eps, uint64_t seed, uint64_t offset, int64_t eps_row0,
                      const cvae_loss_weights* w, float* params, float* m, float* v, int64_t step0,
                      const cvae_adam_config* adam, float* loss_out, double* loss_accum,

@@ -51,14 +51,16 @@ class OracleEngine:
                 p.copy_(self.params[o:o + p.numel()].view_as(p))
                 o += p.numel()
 
-    def forward_backward(self, x, idx=None, eps=None, batch=None, weights=None, accumulate=True, row0=0, parts=7):
+    def forward_backward(self, x, idx=None, eps=None, batch=None, weights=None, accumulate=True, row0=0, parts=7,
+                         classes=None):
         self.calls.append(("fb", None if idx is None else idx.clone(), batch, row0, parts))
         rows = x[idx] if idx is not None else x[:batch]
+        cls = None if classes is None else (classes[idx] if idx is not None else classes[:batch]).long()
         rel, start = relative(rows)
         for p in self.plist:
             p.grad = None
-        mu, lv, hc = self.model.encode(rel, start)
-        recon = self.model.decode(self.model.reparameterize(mu, lv, eps), hc)
+        mu, lv, hc = self.model.encode(rel, start, cls)
+        recon = self.model.decode(self.model.reparameterize(mu, lv, eps), hc, cls)
         w = dict(zip(("recon_weight", "kld_weight", "start_weight", "time_weight"), weights or self.weights))
         ls = oracle_loss(recon, rel, mu, lv, hc, **w)
         ls[0].backward()
@@ -83,8 +85,9 @@ class OracleEngine:
         self.params.addcdiv_(self.m, denom, value=-(self.lr / bc1))
         self.pack()
 
-    def train_step(self, x, idx=None, eps=None, batch=None, weights=None, accumulate=True, row0=0):
-        self.forward_backward(x, idx=idx, eps=eps, batch=batch, weights=weights, accumulate=accumulate)
+    def train_step(self, x, idx=None, eps=None, batch=None, weights=None, accumulate=True, row0=0, classes=None):
+        self.forward_backward(x, idx=idx, eps=eps, batch=batch, weights=weights, accumulate=accumulate,
+                              classes=classes)
         self.adam_step()
         return self.loss
 

@@ -111,3 +111,22 @@ def test_fp8_emulation_rounding_and_layer_choice():
     f85 = cvae_np.fp8_layers(p5, 200, 6, 512, 128, 8, 8)
     assert "encoder.1" in f85 and "decoder.0" in f85 and "condition_encoder.0" not in f85
 
+
+
+def test_class_embedding_layout(cl):
+    """BASELINE cfg4: the scenario-class embedding adds one parameter tensor, LAST (nn.Embedding
+    layout), and widens fc (2H+E inputs) and decoder.0 (Z+H+E inputs); the reference's 24 keys
+    keep their order."""
+    from cvae_amd import ConditionalTrajectoryVAE, config_info
+    n, nt, lds = config_info(10, 3, 8, 128, n_classes=4, class_dim=16)
+    m = ConditionalTrajectoryVAE(10, 3, 8, n_classes=4, class_dim=16)
+    ref = OracleCVAE(10, 3, 8, n_classes=4, class_dim=16)
+    keys = list(m.state_dict().keys())
+    assert keys == list(ref.state_dict().keys()) and nt == 25 == len(keys)
+    assert keys[:24] == list(OracleCVAE(10, 3, 8).state_dict().keys())
+    assert keys[-1] == "class_embedding.weight" and tuple(m.state_dict()[keys[-1]].shape) == (4, 16)
+    assert n == sum(p.numel() for p in m.parameters()) and 0 < lds <= 160 * 1024
+    assert m.fc_mu.weight.shape == (8, 2 * 128 + 16) and m.decoder[0].weight.shape == (128, 8 + 128 + 16)
+    from cvae_amd._lib import CvaeError
+    with pytest.raises(CvaeError, match="class_dim"):
+        config_info(10, 3, 8, 128, n_classes=4, class_dim=6)
