@@ -509,7 +509,7 @@ __device__ __forceinline__ void param_body(const LayerDev& L, const TileDesc& td
   float db = 0.f;
   if (MODE == PM_ADAM) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) g4[c] = c < st.nv ? aa.grads[st.base + c] * aa.grad_scale : 0.f;
+    for (int c = 0; c < 4; ++c) g4[c] = c < st.nv ? aa.grads[st.base + c * st.stride] * aa.grad_scale : 0.f;
     const int ob = td.o0 + tid;
     if (td.i0 == 0 && tid < 32 && ob < L.N && L.has_bias) {
       const int seg = (L.nseg == 2 && ob >= L.seg_rows0) ? 1 : 0;

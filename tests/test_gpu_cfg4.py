@@ -111,6 +111,7 @@ def test_cfg4_bf16_benchmark_shape(cvae):
     want = np.array([float(v) for v in oracle_loss(r, rel, mu, lv, hc, **WD)])
     np.testing.assert_allclose(loss, want, rtol=2e-2, atol=1e-5)
     xd, cd = eng.as_input(x), cls.cuda()
+    eng.rng_offset, eng.step_count = 0, 0  # the loss check above began a step: both engines restart at 0
     for _ in range(3):
         eng.train_step(xd, classes=cd)
         e2.forward_backward(xd, classes=cd)
