@@ -57,6 +57,10 @@ struct cvae_handle {
   std::vector<TileDesc> tiles_part[2];
   TileDesc* d_tiles_part[2] = {nullptr, nullptr};
   int64_t bucket_split = 0;   // flat index of decoder.0.weight
+  // split-K of the dW launch for large batches (cvae_wgrad.h SplitK): partial workspace + tickets
+  int splitk_max = 1;
+  float* splitk_ws = nullptr;
+  unsigned* splitk_tickets = nullptr;
   char* arena = nullptr;    // weight copies + activations
   unsigned* d_sync = nullptr;  // fused launch hand-off words (fchain::FusedArgs::sync), zero between launches
   bool fused = false;          // training steps run as one fused_step_kernel launch
@@ -358,6 +362,11 @@ int alloc_arena(cvae_handle* h) {
   const int64_t zb_off = take((int64_t)maxnp * 4);
   const int64_t part_off = take((int64_t)h->max_row_tiles * 8 * 4);
   const int64_t sync_off = take(256);
+  // split-K for batches of >= 8192 rows: up to 16 splits of >= 2048 rows (cvae_wgrad.h SplitK)
+  h->splitk_max = std::max(1, std::min(16, rup_i(h->cfg.max_batch, 32) / 2048));
+  if (rup_i(h->cfg.max_batch, 32) < 8192) h->splitk_max = 1;
+  const int64_t skw_off = h->splitk_max > 1 ? take((int64_t)h->tiles.size() * h->splitk_max * (32 * 32 + 32) * 4) : 0;
+  const int64_t skt_off = h->splitk_max > 1 ? take((int64_t)h->tiles.size() * 4) : 0;
   const int64_t tile_off = take((int64_t)h->tiles.size() * sizeof(TileDesc));
   const int64_t tp_off0 = take((int64_t)h->tiles_part[0].size() * sizeof(TileDesc));
   const int64_t tp_off1 = take((int64_t)h->tiles_part[1].size() * sizeof(TileDesc));
@@ -378,6 +387,10 @@ int alloc_arena(cvae_handle* h) {
   n.bias_all = (const float*)(h->arena + bias_base);
   h->d_partials = (float*)(h->arena + part_off);
   h->d_sync = (unsigned*)(h->arena + sync_off);
+  if (h->splitk_max > 1) {  // tickets start at zero (the arena memset) and return to zero after every launch
+    h->splitk_ws = (float*)(h->arena + skw_off);
+    h->splitk_tickets = (unsigned*)(h->arena + skt_off);
+  }
   h->d_tiles = (TileDesc*)(h->arena + tile_off);
   HIPCK(hipMemcpy(h->d_tiles, h->tiles.data(), h->tiles.size() * sizeof(TileDesc), hipMemcpyHostToDevice));
   const int64_t tp_off[2] = {tp_off0, tp_off1};
@@ -663,29 +676,39 @@ int bk_of(cvae_handle*, int batch) { return rup_i(batch, 32); }
 
 // the dW (⊕ Adam) launch of a training step: the fast kernel for the fast configuration, the
 // generic kernel over a bucket's tile list for a split (two-bucket) step
+// splits of the dW launch's K (= batch) range: 1 below 8192 rows, else >= 2048 rows per split
+int splits_of(const cvae_handle* h, int batch) {
+  const int Bk = rup_i(batch, 32);
+  if (h->splitk_max <= 1 || Bk < 8192) return 1;
+  const char* env = std::getenv("CVAE_SPLITK");  // A/B measurements: force a split count
+  const int want = env ? std::atoi(env) : Bk / 2048;
+  return std::max(1, std::min(h->splitk_max, want));
+}
+
 template <int MODE>
 int launch_wgrad(cvae_handle* h, int batch, const AdamArgs& aa, const LossArgs& la, hipStream_t s,
                  int parts = CVAE_PART_DW_DEC | CVAE_PART_DW_REST) {
   const int dw = parts & (CVAE_PART_DW_DEC | CVAE_PART_DW_REST);
+  SplitK sk{splits_of(h, batch), 0, h->splitk_ws, h->splitk_tickets, 0};
   if (dw != (CVAE_PART_DW_DEC | CVAE_PART_DW_REST)) {
     const int k = dw == CVAE_PART_DW_DEC ? 0 : 1;
     const int nt = (int)h->tiles_part[k].size();
     if (is16(h))
-      return klaunch(h, wgrad_kernel<__bf16, MODE>, dim3(nt), dim3(WG_THREADS), 0, s, h->net,
-                     (const TileDesc*)h->d_tiles_part[k], bk_of(h, batch), aa, la);
-    return klaunch(h, wgrad_kernel<float, MODE>, dim3(nt), dim3(WG_THREADS), 0, s, h->net,
-                   (const TileDesc*)h->d_tiles_part[k], bk_of(h, batch), aa, la);
+      return klaunch(h, wgrad_kernel<__bf16, MODE>, dim3(nt * sk.S), dim3(WG_THREADS), 0, s, h->net,
+                     (const TileDesc*)h->d_tiles_part[k], bk_of(h, batch), aa, la, sk);
+    return klaunch(h, wgrad_kernel<float, MODE>, dim3(nt * sk.S), dim3(WG_THREADS), 0, s, h->net,
+                   (const TileDesc*)h->d_tiles_part[k], bk_of(h, batch), aa, la, sk);
   }
   const int nt = (int)h->tiles.size();
   if (h->fast_nki == 19)
-    return klaunch(h, fchain::fastwgrad_kernel<19, MODE>, dim3(fchain::Tiles<19>::total() + 1), dim3(WG_THREADS),
-                   0, s, h->arena, aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), h->net.S, h->net.D, h->net.I,
-                   aa, la);
+    return klaunch(h, fchain::fastwgrad_kernel<19, MODE>, dim3(fchain::Tiles<19>::total() * sk.S + 1),
+                   dim3(WG_THREADS), 0, s, h->arena, aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), h->net.S,
+                   h->net.D, h->net.I, aa, la, sk);
   if (is16(h))
-    return klaunch(h, wgrad_kernel<__bf16, MODE>, dim3(nt), dim3(WG_THREADS), 0, s, h->net,
-                   (const TileDesc*)h->d_tiles, bk_of(h, batch), aa, la);
-  return klaunch(h, wgrad_kernel<float, MODE>, dim3(nt), dim3(WG_THREADS), 0, s, h->net,
-                 (const TileDesc*)h->d_tiles, bk_of(h, batch), aa, la);
+    return klaunch(h, wgrad_kernel<__bf16, MODE>, dim3(nt * sk.S), dim3(WG_THREADS), 0, s, h->net,
+                   (const TileDesc*)h->d_tiles, bk_of(h, batch), aa, la, sk);
+  return klaunch(h, wgrad_kernel<float, MODE>, dim3(nt * sk.S), dim3(WG_THREADS), 0, s, h->net,
+                 (const TileDesc*)h->d_tiles, bk_of(h, batch), aa, la, sk);
 }
 
 // device counters, fused launch: its chain blocks do not bump the step (its dW tiles read it in the

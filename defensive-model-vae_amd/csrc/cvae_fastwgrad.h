@@ -132,26 +132,30 @@ __host__ __device__ inline LayerDev fast_layer(int l, char* arena, int Bp, int I
 
 // Scalars first (SGPR-preloaded at wave launch, as fastchain_kernel's): the arena and master-state
 // pointers every first load needs.
+// grid = total tiles × sk.S + 1 (split-major; the last block finishes the loss)
 template <int NKI, int MODE>
 __global__ __launch_bounds__(WG_THREADS) void fastwgrad_kernel(char* arena, float* params, float* mst, float* vst,
                                                                 int Bp, int Bk, int S, int D, int I, AdamArgs a,
-                                                                LossArgs la) {
+                                                                LossArgs la, SplitK sk) {
   const FastNet fn{arena, Bp, S, D, I};
   AdamArgs aa = a;
   aa.params = params;
   aa.m = mst;
   aa.v = vst;
-  if ((int)blockIdx.x == Tiles<NKI>::total()) {  // one extra block finishes the loss beside the tiles
+  constexpr int NTL = Tiles<NKI>::total();
+  if ((int)blockIdx.x == NTL * sk.S) {  // one extra block finishes the loss beside the tiles
     if (threadIdx.x < 64 && la.partials) finish_loss(la, fn.S, fn.D, Z);
     return;
   }
   __shared__ __attribute__((aligned(16))) WgradLds<Tiles<NKI>::ni_max()> sh;
-  const TileDesc td = Tiles<NKI>::at(blockIdx.x);
+  sk.s = blockIdx.x / NTL;
+  sk.tile = blockIdx.x - sk.s * NTL;
+  const TileDesc td = Tiles<NKI>::at(sk.tile);
   const LayerDev L = fast_layer<NKI>(td.layer, fn.arena, fn.Bp, fn.I);
   if (Tiles<NKI>::ni(td.layer) == 2)  // block-uniform
-    wgrad_body<__bf16, MODE, false, 2>(L, td, Bk, aa, la, false, fn.S, fn.D, Z, sh.red, sh.dbp);
+    wgrad_body<__bf16, MODE, false, 2>(L, td, Bk, aa, la, false, fn.S, fn.D, Z, sh.red, sh.dbp, sk);
   else
-    wgrad_body<__bf16, MODE, false, 1>(L, td, Bk, aa, la, false, fn.S, fn.D, Z, sh.red, sh.dbp);
+    wgrad_body<__bf16, MODE, false, 1>(L, td, Bk, aa, la, false, fn.S, fn.D, Z, sh.red, sh.dbp, sk);
 }
 
 // ---------------------------------------------------------------- the fused training step

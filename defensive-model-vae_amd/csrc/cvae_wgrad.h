@@ -354,6 +354,19 @@ struct WgradLds {
   float dbp[WG_NW * 32];                  // per-wave bias partials
 };
 
+// Split-K over the batch (large batches): split sk.s of sk.S computes the tile's partial dW/db over
+// its K range, writes it (fp32, write-through) to sk.ws, and adds to the tile's ticket; the block
+// whose add returns S-1 sums the S partials in split order (deterministic, independent of arrival
+// order) and runs the epilogue, then zeroes the ticket for the next launch (MI355X_MICROARCH.md,
+// inter-workgroup hand-off: sc1 stores drained before one lane's agent-scope add; the last adder
+// reads with sc1 loads after a workgroup barrier).  S = 1: the whole batch in one block.
+struct SplitK {
+  int S, s;
+  float* ws;          // [tile][S][32·TW + 32] fp32 partials (dW then db)
+  unsigned* tickets;  // [tile], zero between launches
+  int tile;
+};
+
 // One workgroup = tile td of layer L: 32 outputs × 32·NI inputs (NI = 2: two 32-wide input tiles
 // sharing the G rows).  loss_block: this workgroup also finishes the loss (S, D, Z: its shape).
 // SC1: the arena rows were handed over inside the launch (fused_step_kernel): every load of them
@@ -361,7 +374,7 @@ struct WgradLds {
 template <typename T, int MODE, bool SC1 = false, int NI = 1>
 __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td, int Bk, AdamArgs aa,
                                            const LossArgs& la, bool loss_block, int S, int D, int Z,
-                                           float* red, float* dbp) {
+                                           float* red, float* dbp, SplitK sk = SplitK{1, 0, nullptr, nullptr, 0}) {
   using V = typename Op<T>::V;
   constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC;
   constexpr int NX = 2 * NI, TW = 32 * NI, LD = TW + 4;  // X fragments per chunk, tile width, image stride
@@ -393,8 +406,10 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
   for (int m = 0; m < 2; ++m) gp[m] = G + aoff(td.o0 + m * 16 + r16, kq, Kg);
 #pragma unroll
   for (int n = 0; n < NX; ++n) xp[n] = X + aoff(td.i0 + n * 16 + r16, kq, Kx);
-  // this wave's chunks: c = wave + WG_NW*j; PF chunks of loads kept in flight
-  const int nk = Bk / KC;
+  // this split's chunk range [c0, c0 + nk) (split-K; the whole batch when S == 1); this wave's
+  // chunks: c0 + wave + WG_NW*j; PF chunks of loads kept in flight
+  const int nk_all = Bk / KC, per = (nk_all + sk.S - 1) / sk.S;
+  const int c0 = sk.s * per, nk = max(0, min(per, nk_all - c0));
   const int nmine = nk > wave ? (nk - wave + WG_NW - 1) / WG_NW : 0;
   constexpr int PF = 4;
   V ga[PF][2], xb[PF][NX];
@@ -404,7 +419,7 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
     rx = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, 0x7fffffff, 0x00020000);
   }
   auto load = [&](int u, int j) {  // unconditional, clamped to this wave's last chunk
-    const size_t ct = (size_t)(wave + WG_NW * min(j, nmine > 0 ? nmine - 1 : 0)) * (KC / 16) * 16;
+    const size_t ct = (size_t)(c0 + wave + WG_NW * min(j, nmine > 0 ? nmine - 1 : 0)) * (KC / 16) * 16;
     if (SC1) {
 #pragma unroll
       for (int m = 0; m < 2; ++m)
@@ -480,6 +495,52 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
 #pragma unroll
     for (int w = 0; w < WG_NW; ++w) db += dbp[w * 32 + tid];
   }
+  if (sk.S > 1) {  // split-K: publish this split's partial; the last of the S blocks finishes the tile
+    constexpr int PW = 32 * TW + 32;
+    static_assert(EPT == 2 || EPT == 4, "partial vectors of 8 or 16 B");
+    float* mine = sk.ws + ((size_t)sk.tile * sk.S + sk.s) * PW;
+    if (tid < 32 * TPR) {
+      if constexpr (EPT == 2)
+        __hip_atomic_store((uint64_t*)(mine + o * TW + iv), __builtin_bit_cast(uint64_t, g4), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      else
+        for (int c = 0; c < EPT; c += 2)
+          __hip_atomic_store((uint64_t*)(mine + o * TW + iv + c),
+                             __builtin_bit_cast(uint64_t, VecF<2>::T{g4[c], g4[c + 1]}), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (bias_tile && tid < 32)
+      __hip_atomic_store((unsigned*)(mine + 32 * TW + tid), __builtin_bit_cast(unsigned, db), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned old = __hip_atomic_fetch_add(sk.tickets + sk.tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      dbp[0] = __builtin_bit_cast(float, old);
+    }
+    __syncthreads();
+    if (__builtin_bit_cast(unsigned, dbp[0]) != (unsigned)(sk.S - 1)) return;  // block-uniform
+    // the last arriver: Σ of the S partials in split order
+    g4 = VE{};
+    db = 0.f;
+    for (int k = 0; k < sk.S; ++k) {
+      const float* pk = sk.ws + ((size_t)sk.tile * sk.S + k) * PW;
+      if (tid < 32 * TPR) {
+#pragma unroll
+        for (int c = 0; c < EPT; c += 2) {
+          const uint64_t u = __hip_atomic_load((const uint64_t*)(pk + o * TW + iv + c), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+          const typename VecF<2>::T v2 = __builtin_bit_cast(typename VecF<2>::T, u);
+          g4[c] += v2[0];
+          g4[c + 1] += v2[1];
+        }
+      }
+      if (bias_tile && tid < 32)
+        db += __builtin_bit_cast(float, __hip_atomic_load((const unsigned*)(pk + 32 * TW + tid), __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT));
+    }
+    if (tid == 0) sk.tickets[sk.tile] = 0u;  // every split has added: reset for the next launch
+  }
   __syncthreads();  // red becomes the image of the new weights
   tile_epilogue<T, MODE, WG_THREADS, EPT, NI>(L, td.o0, td.i0, st, sb, g4, db, aa, red);
 #if CVAE_DIAG_STAMPS
@@ -489,12 +550,16 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
 }
 
 // generic configurations: tile descriptors and layer records from memory
+// grid = ntiles × sk.S (split-major: split s owns blocks [s·ntiles, (s+1)·ntiles))
 template <typename T, int MODE>
 __global__ __launch_bounds__(WG_THREADS) void wgrad_kernel(NetDev net, const TileDesc* __restrict__ tiles,
-                                                           int Bk, AdamArgs aa, LossArgs la) {
+                                                           int Bk, AdamArgs aa, LossArgs la, SplitK sk) {
   __shared__ __attribute__((aligned(16))) WgradLds<1> sh;
-  const TileDesc td = tiles[blockIdx.x];
-  wgrad_body<T, MODE>(net.L[td.layer], td, Bk, aa, la, blockIdx.x == 0, net.S, net.D, net.Z, sh.red, sh.dbp);
+  const int ntiles = gridDim.x / sk.S;
+  sk.s = blockIdx.x / ntiles;
+  sk.tile = blockIdx.x - sk.s * ntiles;
+  const TileDesc td = tiles[sk.tile];
+  wgrad_body<T, MODE>(net.L[td.layer], td, Bk, aa, la, blockIdx.x == 0, net.S, net.D, net.Z, sh.red, sh.dbp, sk);
 }
 
 // Adam from a (reduced) gradient buffer, or repack of the operand copies.

@@ -350,3 +350,35 @@ def test_train_resume_equals_uninterrupted(cvae, golden, tmp_path, eps):
         assert torch.equal(v, m22.state_dict()[k]), k
     e4, e22 = m4.engine, m22.engine
     assert torch.equal(e4.m, e22.m) and torch.equal(e4.v, e22.v) and torch.equal(e4.counters, e22.counters)
+
+
+@pytest.mark.parametrize("dtype,S,D,B", [("bf16", 100, 6, 8192), ("fp32", 10, 3, 12288)])
+def test_splitk_dw_matches_single_split_and_is_deterministic(cvae, monkeypatch, dtype, S, D, B):
+    """Large batches split the dW launch's K (= batch) range over S blocks per tile (split-K; the
+    last arriver sums the partials in split order): the gradient equals the one-block-per-tile
+    reduction up to fp32 summation order, and repeated launches are bit-identical."""
+    torch.manual_seed(0)
+    ref = OracleCVAE(S, D, 8)
+    m, eng = _model(cvae, S, D, 8, sd=ref.state_dict(), dtype=dtype, max_batch=B)
+    x = eng.as_input(torch.randn(B, S, D, generator=torch.Generator().manual_seed(11)))
+    eps = torch.randn(B, 8, generator=torch.Generator().manual_seed(12)).cuda()
+    monkeypatch.setenv("CVAE_SPLITK", "1")
+    eng.forward_backward(x, eps=eps, accumulate=False)
+    g1 = eng.grads.clone()
+    monkeypatch.delenv("CVAE_SPLITK")
+    outs = []
+    for _ in range(2):
+        eng.forward_backward(x, eps=eps, accumulate=False)
+        outs.append(eng.grads.clone())
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    err = float((outs[0] - g1).norm() / g1.norm())
+    assert err < 1e-5, err
+    # and the fused dW ⊕ Adam path with split-K equals the split path (fwd_bwd → Adam) bit for bit
+    m2, e2 = _model(cvae, S, D, 8, sd=ref.state_dict(), dtype=dtype, max_batch=B)
+    m3, e3 = _model(cvae, S, D, 8, sd=ref.state_dict(), dtype=dtype, max_batch=B)
+    e2.train_step(x, eps=eps)
+    e3.forward_backward(x, eps=eps)
+    e3.adam_step()
+    torch.cuda.synchronize()
+    assert torch.equal(e2.params, e3.params) and torch.equal(e2.m, e3.m)
