@@ -19,6 +19,7 @@
 #include "cvae_wgrad.h"
 #include "cvae_loss.h"
 #include "cvae_fastwgrad.h"
+#include "cvae_extract.h"
 
 namespace {
 
@@ -1091,6 +1092,20 @@ int cvae_adam_scalars(const cvae_adam_config* adam, int64_t n, float* out, void*
   const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(adam_scalars_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, adam->lr, adam->beta1,
                      adam->beta2, n, out);
+  HIPCK(hipGetLastError());
+  return CVAE_OK;
+}
+
+int cvae_extract_trajectories(const double* cols, int64_t n_rows, const int64_t* file_offsets, int n_files,
+                              int scene, int target_points, int point_mode, double time_interval, double* out,
+                              int32_t* valid, void* stream) {
+  if (n_files < 0 || n_rows < 0) return fail(CVAE_E_INVALID, "bad size");
+  if (n_files == 0) return CVAE_OK;
+  if (!cols || !file_offsets || !out || !valid) return fail(CVAE_E_INVALID, "null argument");
+  if (scene < CVAE_SCENE_STATIC || scene > CVAE_SCENE_UNPREDICTABLE) return fail(CVAE_E_INVALID, "bad scene");
+  if (target_points < 2 || (point_mode != 0 && point_mode != 1)) return fail(CVAE_E_INVALID, "bad resampling");
+  hipLaunchKernelGGL(extract_kernel, dim3(n_files), dim3(EX_THREADS), 0, (hipStream_t)stream, cols, n_rows,
+                     file_offsets, scene, target_points, point_mode, time_interval, out, (int*)valid);
   HIPCK(hipGetLastError());
   return CVAE_OK;
 }

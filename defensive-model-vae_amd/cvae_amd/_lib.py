@@ -67,6 +67,8 @@ _SIGS = {
     "cvae_loss": (_i, [_v, _v, _v, _v, _i, _i, _i, _i, _W, _v, _v, _v]),
     "cvae_loss_backward": (_i, [_v, _v, _v, _v, _i, _i, _i, _i, _W, _v, _v, _v, _v, _v]),
     "cvae_adam_scalars": (_i, [_A, _i64, _v, _v]),
+    # cols, n_rows, file_offsets, n_files, scene, target_points, point_mode, time_interval, out, valid, stream
+    "cvae_extract_trajectories": (_i, [_v, _i64, _v, _i, _i, _i, _i, _d, _v, _v, _v]),
     "cvae_set_timing": (_i, [_v, _i]),
     "cvae_kernel_times": (_i, [_v, C.c_char_p, _i, C.POINTER(_f), _i]),
     "cvae_last_error": (C.c_char_p, []),

@@ -122,21 +122,89 @@ def process_csv(csv_path, scene, action=None, target_points=5, point_mode="norma
     return process_frame(read_columns(csv_path), scene, target_points, point_mode, time_interval)
 
 
-def collect_trajectories(data_root, scenes, actions, target_points=5, point_mode="normal", time_interval=0.015):
+# scene → (id of the device kernel's predicate pair, columns its predicates read)
+_SCENE_ID = {
+    "StaticBlindTown05": (0, ("ego_y", "sv2_vx", "sv2_vy")),
+    "DynamicBlindTown05": (1, ("sv1_yaw", "ego_x")),
+    "PredictableMovementTown05": (2, ("sv1_vx", "sv1_vy", "ego_y")),
+    "UnpredictableMovementTown04": (3, ("ego_x", "sv1_x", "ego_y", "sv1_y", "sv1_yaw")),
+}
+
+
+def process_frames_device(frames, scene, target_points=5, point_mode="normal", time_interval=0.015,
+                          device="cuda"):
+    """``process_frame`` for many parsed CSVs in ONE launch of the HIP extraction kernel
+    (csrc/cvae_extract.h; C-ABI ``cvae_extract_trajectories``): the columns of all files are
+    stacked into one float64 [9][rows] device array, one workgroup per file finds the start row
+    and the end row, resamples the track and forms the time column.  Same results as
+    ``process_frame`` bit for bit (list of (target_points, 3) arrays or None, in input order).
+    Fails loudly without the HIP extension (no host fallback)."""
+    import ctypes as C
+    import torch
+    from ._lib import check, lib
+    if point_mode not in ("normal", "extend_mid"):
+        raise ValueError(f"unknown point_mode {point_mode!r}")
+    if target_points < 2:
+        raise ValueError("target_points must be >= 2")
+    sid, needed = _SCENE_ID[scene]
+    lens, usable = [], []
+    for cols in frames:
+        for k in needed:  # the host predicates raise KeyError on a missing column: so do we
+            if k not in cols:
+                raise KeyError(k)
+        n = len(next(iter(cols.values()))) if cols else 0
+        lens.append(n)
+        usable.append("ego_x" in cols and "ego_y" in cols)
+    n_rows = int(sum(lens))
+    host = np.zeros((len(COLUMNS), n_rows), np.float64)
+    r = 0
+    for cols, n in zip(frames, lens):
+        for c, name in enumerate(COLUMNS):
+            if name in cols:
+                host[c, r:r + n] = np.asarray(cols[name], dtype=np.float64)
+        r += n
+    off = np.zeros(len(frames) + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    dev = torch.device(device)
+    d_cols = torch.from_numpy(host).to(dev)
+    d_off = torch.from_numpy(off).to(dev)
+    d_out = torch.empty((len(frames), target_points, 3), dtype=torch.float64, device=dev)
+    d_valid = torch.empty(len(frames), dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    check(lib().cvae_extract_trajectories(C.c_void_p(d_cols.data_ptr()), n_rows, C.c_void_p(d_off.data_ptr()),
+                                          len(frames), sid, int(target_points), int(point_mode == "extend_mid"),
+                                          float(time_interval), C.c_void_p(d_out.data_ptr()),
+                                          C.c_void_p(d_valid.data_ptr()), C.c_void_p(stream)),
+          "cvae_extract_trajectories")
+    out, valid = d_out.cpu().numpy(), d_valid.cpu().numpy()
+    return [out[f] if valid[f] and usable[f] else None for f in range(len(frames))]
+
+
+def _scene_files(data_root, scene, actions):
+    for action in actions:
+        path = os.path.join(data_root, scene, action)
+        if not os.path.exists(path):
+            continue
+        for fname in os.listdir(path):
+            if fname.endswith(".csv"):
+                yield action, os.path.join(path, fname)
+
+
+def collect_trajectories(data_root, scenes, actions, target_points=5, point_mode="normal", time_interval=0.015,
+                         device=None):
     """Traj_Data_Process.collect_trajectories (`:125-141`): every CSV under root/scene/action, in
-    ``os.listdir`` order; trajectories that fail extraction are skipped."""
+    ``os.listdir`` order; trajectories that fail extraction are skipped.  ``device`` (e.g.
+    "cuda"): parse on the host, extract every file of a scene in one kernel launch
+    (``process_frames_device``)."""
     out = []
     for scene in scenes:
-        for action in actions:
-            path = os.path.join(data_root, scene, action)
-            if not os.path.exists(path):
-                continue
-            for fname in os.listdir(path):
-                if fname.endswith(".csv"):
-                    t = process_csv(os.path.join(path, fname), scene, action, target_points, point_mode,
-                                    time_interval)
-                    if t is not None and len(t) == target_points:
-                        out.append(t)
+        files = list(_scene_files(data_root, scene, actions))
+        if device is not None:
+            ts = process_frames_device([read_columns(p) for _, p in files], scene, target_points, point_mode,
+                                       time_interval, device)
+        else:
+            ts = (process_csv(p, scene, a, target_points, point_mode, time_interval) for a, p in files)
+        out.extend(t for t in ts if t is not None and len(t) == target_points)
     return out
 
 
@@ -176,8 +244,9 @@ def main(argv=None):
     ap.add_argument("--interval", type=float, default=0.02)
     ap.add_argument("--mode", default="normal", choices=["normal", "extend_mid"])
     ap.add_argument("--out", required=True)
+    ap.add_argument("--device", default=None, help="e.g. cuda: extract on the GPU (one launch per scene)")
     a = ap.parse_args(argv)
-    trajs = collect_trajectories(a.root, a.scene, a.action or ACTIONS, a.points, a.mode, a.interval)
+    trajs = collect_trajectories(a.root, a.scene, a.action or ACTIONS, a.points, a.mode, a.interval, a.device)
     if not trajs:
         raise SystemExit("no trajectory extracted")
     arr = pad_and_save(trajs, a.out)

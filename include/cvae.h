@@ -280,6 +280,19 @@ int cvae_sync_words(cvae_handle* h, unsigned* out);
  * device-counter path (the host path computes them on the host). */
 int cvae_adam_scalars(const cvae_adam_config* adam, int64_t n, float* out, void* stream);
 
+/* Trajectory extraction (Traj_Data_Process.process_csv :72-122) for n_files parsed
+ * CSV logs at once, handle-free.  cols: float64 [9][n_rows] on the device, the columns
+ * (ego_x, ego_y, sv1_x, sv1_y, sv1_vx, sv1_vy, sv1_yaw, sv2_vx, sv2_vy) of all files stacked,
+ * file f owning rows [file_offsets[f], file_offsets[f+1]) (int64 [n_files+1], device).
+ * scene: CVAE_SCENE_* (SCENE_CONFIG :8-25); point_mode 0 = 'normal', 1 = 'extend_mid'.
+ * Writes out float64 [n_files][target_points][3] (time, ego_x, ego_y) and valid int32 [n_files]
+ * (0 where process_csv returns None: no start row, or fewer than target_points rows). */
+enum cvae_scene { CVAE_SCENE_STATIC = 0, CVAE_SCENE_DYNAMIC = 1, CVAE_SCENE_PREDICTABLE = 2,
+                  CVAE_SCENE_UNPREDICTABLE = 3 };
+int cvae_extract_trajectories(const double* cols, int64_t n_rows, const int64_t* file_offsets, int n_files,
+                              int scene, int target_points, int point_mode, double time_interval,
+                              double* out, int32_t* valid, void* stream);
+
 const char* cvae_last_error(void);
 int cvae_abi_version(void);
 
