@@ -20,6 +20,7 @@
 #include "cvae_loss.h"
 #include "cvae_fastwgrad.h"
 #include "cvae_extract.h"
+#include "cvae_mpc.h"
 
 namespace {
 
@@ -1109,6 +1110,93 @@ int cvae_extract_trajectories(const double* cols, int64_t n_rows, const int64_t*
   HIPCK(hipGetLastError());
   return CVAE_OK;
 }
+
+int cvae_mpc_default_config(cvae_mpc_config* cfg) {
+  if (!cfg) return fail(CVAE_E_INVALID, "null argument");
+  cfg->wheelbase = 2.8; cfg->max_steer = 0.5; cfg->max_accel = 7.0; cfg->dt = 0.01;
+  cfg->q_theta = 20.0; cfg->q_v = 5.0; cfg->qf_theta = 20.0; cfg->qf_v = 5.0; cfg->r_accel = 1.0; cfg->r_steer = 50.0;
+  cfg->tol = 1e-10;
+  cfg->prediction_horizon = 10; cfg->control_horizon = 5; cfg->max_iter = 50; cfg->reserved = 0;
+  return CVAE_OK;
+}
+
+static int mpc_cfg(const cvae_mpc_config* in, MpcCfg* c) {
+  if (!in) return fail(CVAE_E_INVALID, "null config");
+  if (in->prediction_horizon < 1 || in->prediction_horizon > MPC_MAXH)
+    return fail(CVAE_E_INVALID, "prediction_horizon must be in [1, 63]");
+  if (in->control_horizon < 1 || in->control_horizon > MPC_MAXCH || in->control_horizon > in->prediction_horizon)
+    return fail(CVAE_E_INVALID, "control_horizon must be in [1, min(prediction_horizon, 32)]");
+  if (!(in->dt > 0.0) || !(in->wheelbase > 0.0) || !(in->max_steer >= 0.0) || !(in->max_accel >= 0.0) ||
+      in->max_iter < 0 || !(in->tol >= 0.0))
+    return fail(CVAE_E_INVALID, "bad MPC parameter");
+  c->L = in->wheelbase; c->max_steer = in->max_steer; c->max_accel = in->max_accel; c->dt = in->dt;
+  c->q_th = in->q_theta; c->q_v = in->q_v; c->qf_th = in->qf_theta; c->qf_v = in->qf_v;
+  c->r_a = in->r_accel; c->r_d = in->r_steer; c->tol = in->tol;
+  c->N = in->prediction_horizon; c->CH = in->control_horizon; c->max_iter = in->max_iter; c->pad_ = 0;
+  return CVAE_OK;
+}
+
+static size_t mpc_spline_bytes() { return (sizeof(MpcSpline) + 7) / 8 * 8; }
+
+int cvae_mpc_track(const cvae_mpc_config* cfg, int n_paths, const double* waypoints, const int32_t* wp_offsets,
+                   const double* initial_states, const int32_t* n_steps, const int64_t* step_offsets,
+                   double* states, double* controls, int32_t* iters, void* stream) {
+  MpcCfg c;
+  int rc = mpc_cfg(cfg, &c);
+  if (rc) return rc;
+  if (n_paths < 0) return fail(CVAE_E_INVALID, "bad size");
+  if (n_paths == 0) return CVAE_OK;
+  if (!waypoints || !wp_offsets || !initial_states || !n_steps || !step_offsets || !states || !controls)
+    return fail(CVAE_E_INVALID, "null argument");
+  const size_t lds = mpc_spline_bytes() + mpc_ws_doubles(c.N, c.CH) * 8;
+  HIPCK(hipFuncSetAttribute((const void*)mpc_track_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(mpc_track_kernel, dim3(n_paths), dim3(64), lds, (hipStream_t)stream, c, waypoints, wp_offsets,
+                     initial_states, n_steps, step_offsets, states, controls, iters);
+  HIPCK(hipGetLastError());
+  return CVAE_OK;
+}
+
+int cvae_mpc_solve(const cvae_mpc_config* cfg, int n, const double* state, const double* ref, const double* last,
+                   double* u, double* cost, int32_t* iters, void* stream) {
+  MpcCfg c;
+  int rc = mpc_cfg(cfg, &c);
+  if (rc) return rc;
+  if (n < 0) return fail(CVAE_E_INVALID, "bad size");
+  if (n == 0) return CVAE_OK;
+  if (!state || !ref || !last || !u || !cost) return fail(CVAE_E_INVALID, "null argument");
+  const size_t lds = mpc_ws_doubles(c.N, c.CH) * 8;
+  HIPCK(hipFuncSetAttribute((const void*)mpc_solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(mpc_solve_kernel, dim3(n), dim3(64), lds, (hipStream_t)stream, c, state, ref, last, u, cost,
+                     iters);
+  HIPCK(hipGetLastError());
+  return CVAE_OK;
+}
+
+int cvae_mpc_reference(int n_paths, const double* waypoints, const int32_t* wp_offsets,
+                       const double* initial_states, const double* t, int n_t, double* out, double* scalars,
+                       void* stream) {
+  if (n_paths < 0 || n_t < 0) return fail(CVAE_E_INVALID, "bad size");
+  if (n_paths == 0) return CVAE_OK;
+  if (!waypoints || !wp_offsets || !initial_states || (n_t && (!t || !out)) || !scalars)
+    return fail(CVAE_E_INVALID, "null argument");
+  const size_t lds = mpc_spline_bytes() + (size_t)4 * 5 * MPC_MAXWP * 8;
+  HIPCK(hipFuncSetAttribute((const void*)mpc_reference_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds));
+  hipLaunchKernelGGL(mpc_reference_kernel, dim3(n_paths), dim3(64), lds, (hipStream_t)stream, waypoints, wp_offsets,
+                     initial_states, t, n_t, out, scalars);
+  HIPCK(hipGetLastError());
+  return CVAE_OK;
+}
+
+#if CVAE_DIAG_MPC
+int cvae_diag_mpc_prof(unsigned long long* host8) {
+  HIPCK(hipDeviceSynchronize());
+  HIPCK(hipMemcpyFromSymbol(host8, HIP_SYMBOL(mpc_prof), 8 * sizeof(unsigned long long)));
+  unsigned long long z[8] = {0};
+  HIPCK(hipMemcpyToSymbol(HIP_SYMBOL(mpc_prof), z, sizeof(z)));
+  return CVAE_OK;
+}
+#endif
 
 #if CVAE_DIAG_SUB
 int cvae_diag_set_sub(unsigned long long* dev_buf) {

@@ -24,6 +24,12 @@ class CvaeLossWeights(C.Structure):
     _fields_ = [("recon", C.c_float), ("kld", C.c_float), ("start", C.c_float), ("time", C.c_float)]
 
 
+class CvaeMpcConfig(C.Structure):
+    _fields_ = [(k, C.c_double) for k in ("wheelbase", "max_steer", "max_accel", "dt", "q_theta", "q_v", "qf_theta",
+                                          "qf_v", "r_accel", "r_steer", "tol")] + \
+               [(k, C.c_int) for k in ("prediction_horizon", "control_horizon", "max_iter", "reserved")]
+
+
 class CvaeAdamConfig(C.Structure):
     _fields_ = [("lr", C.c_double), ("beta1", C.c_double), ("beta2", C.c_double), ("eps", C.c_double)]
 
@@ -69,6 +75,13 @@ _SIGS = {
     "cvae_adam_scalars": (_i, [_A, _i64, _v, _v]),
     # cols, n_rows, file_offsets, n_files, scene, target_points, point_mode, time_interval, out, valid, stream
     "cvae_extract_trajectories": (_i, [_v, _i64, _v, _i, _i, _i, _i, _d, _v, _v, _v]),
+    "cvae_mpc_default_config": (_i, [C.POINTER(CvaeMpcConfig)]),
+    # cfg, n_paths, waypoints, wp_offsets, initial_states, n_steps, step_offsets, states, controls, iters, stream
+    "cvae_mpc_track": (_i, [C.POINTER(CvaeMpcConfig), _i, _v, _v, _v, _v, _v, _v, _v, _v, _v]),
+    # cfg, n, state, ref, last, u, cost, iters, stream
+    "cvae_mpc_solve": (_i, [C.POINTER(CvaeMpcConfig), _i, _v, _v, _v, _v, _v, _v, _v]),
+    # n_paths, waypoints, wp_offsets, initial_states, t, n_t, out, scalars, stream
+    "cvae_mpc_reference": (_i, [_i, _v, _v, _v, _v, _i, _v, _v, _v]),
     "cvae_set_timing": (_i, [_v, _i]),
     "cvae_kernel_times": (_i, [_v, C.c_char_p, _i, C.POINTER(_f), _i]),
     "cvae_last_error": (C.c_char_p, []),

@@ -293,6 +293,44 @@ int cvae_extract_trajectories(const double* cols, int64_t n_rows, const int64_t*
                               int scene, int target_points, int point_mode, double time_interval,
                               double* out, int32_t* valid, void* stream);
 
+/* Batched MPC path tracking (MPC/MPC_Tracking.py), handle-free, float64 throughout.
+ * The configuration mirrors PathTracker / MPCController / VehicleModel's parameters
+ * (MPC_Tracking.py:26, :283-306, :421-423); cvae_mpc_default_config fills the reference's values
+ * (wheelbase 2.8, max_steer 0.5, max_accel 7, dt 0.01, N 10, control horizon 5,
+ * Q = Qf = diag(20, 5), R = diag(1, 50)).  Limits: 1 <= control_horizon <= min(N, 32), N <= 63,
+ * 2..64 waypoints per path with strictly increasing times. */
+typedef struct cvae_mpc_config {
+  double wheelbase, max_steer, max_accel, dt;
+  double q_theta, q_v, qf_theta, qf_v, r_accel, r_steer;
+  double tol;            /* projected-gradient stationarity of the sub-problem solve */
+  int prediction_horizon, control_horizon, max_iter, reserved;
+} cvae_mpc_config;
+int cvae_mpc_default_config(cvae_mpc_config* cfg);
+
+/* PathTracker(waypoints, initial_state).run_simulation for n_paths paths at once (MPC_Tracking.py
+ * :418-523).  Device arrays: waypoints float64 [sum n_wp][3] (x, y, t), wp_offsets int32 [n_paths+1],
+ * initial_states float64 [n_paths][5] (x, y, theta, vx, vy; theta already wrapped as :435-436 does),
+ * n_steps int32 [n_paths] (= int(total_time / dt)), step_offsets int64 [n_paths+1] (prefix sums of
+ * n_steps).  Writes states float64 rows [step_offsets[p] + p .. + n_steps[p]] x 4 (x, y, theta, v;
+ * row 0 = the initial state), controls float64 rows [step_offsets[p] ..) x 2 (accel, steer) and,
+ * if non-null, iters int32 [sum n_steps] (Newton iterations of each sub-problem). */
+int cvae_mpc_track(const cvae_mpc_config* cfg, int n_paths, const double* waypoints, const int32_t* wp_offsets,
+                   const double* initial_states, const int32_t* n_steps, const int64_t* step_offsets,
+                   double* states, double* controls, int32_t* iters, void* stream);
+
+/* MPCController.solve_mpc (:311-415) for n independent sub-problems: state [n][4], ref [n][N+1][2]
+ * (theta_ref, v_ref), last [n][2] (previous control, NaN = none).  Writes the control sequence
+ * u [n][control_horizon][2], its cost [n] and (if non-null) iters [n]. */
+int cvae_mpc_solve(const cvae_mpc_config* cfg, int n, const double* state, const double* ref, const double* last,
+                   double* u, double* cost, int32_t* iters, void* stream);
+
+/* PathInterpolator (:89-277) queries: out [n_paths][n_t][5] = get_reference(t) (x, y, vx, vy) and
+ * get_reference_heading(t); scalars [n_paths][6] = start_theta, end_vx, end_vy, end_theta, end_x,
+ * end_y.  Same waypoint/initial-state layout as cvae_mpc_track; t float64 [n_t]. */
+int cvae_mpc_reference(int n_paths, const double* waypoints, const int32_t* wp_offsets,
+                       const double* initial_states, const double* t, int n_t, double* out, double* scalars,
+                       void* stream);
+
 const char* cvae_last_error(void);
 int cvae_abi_version(void);
 
