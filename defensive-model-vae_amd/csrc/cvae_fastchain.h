@@ -755,7 +755,16 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(char* arena, const void* 
   ra.x = x;
   ra.idx = idx;
   ra.batch = batch;
+#if CVAE_DIAG_TWICE  // diagnostic builds only: the same code runs twice, the second pass on warm caches
+  const int reps = Bp > 0 ? 2 : 1;
+#pragma nounroll
+  for (int it = 0; it < reps; ++it) {
+    chain_body<NKI>(FastNet{arena, Bp, S, D, I}, ra, smem, nullptr, blockIdx.x);
+    __syncthreads();
+  }
+#else
   chain_body<NKI>(FastNet{arena, Bp, S, D, I}, ra, smem, nullptr, blockIdx.x);
+#endif
 }
 
 }  // namespace fchain

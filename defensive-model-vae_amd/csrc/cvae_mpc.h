@@ -571,6 +571,8 @@ __device__ int mpc_solve(const MpcCfg& c, const MpcWs& w, double th0, double v0,
     const double eps = fmin(pg, 1e-3);
     const bool act = lane < NV && ((uj <= -b + eps && g > 0.0) || (uj >= b - eps && g < 0.0));
     const unsigned long long amask = __ballot(act);
+    // held variables take a diagonally scaled gradient step (onto their bound after projection)
+    const double hjj = lane < NV ? w.H[lane * w.ldh + lane] : 1.0;
     if (lane < NV) {
       for (int m = 0; m < NV; ++m) {
         const bool am = (amask >> m) & 1ull;
@@ -586,7 +588,7 @@ __device__ int mpc_solve(const MpcCfg& c, const MpcWs& w, double th0, double v0,
       else lambda = lambda == 0.0 ? 1e-10 : lambda * 100.0;
       continue;
     }
-    const double d = mpc_chol_solve(w, NV, lane, act || lane >= NV ? 0.0 : -g);
+    const double d = mpc_chol_solve(w, NV, lane, lane >= NV ? 0.0 : act ? -g / fmax(hjj, 1e-12) : -g);
     MPC_TOC(4);
     double alpha = 1.0;
     bool accepted = false;
@@ -606,14 +608,21 @@ __device__ int mpc_solve(const MpcCfg& c, const MpcWs& w, double th0, double v0,
       alpha *= 0.5;
     }
     MPC_TOC(1);
-    if (!accepted) break;
+    if (!accepted) {
+      if (exact) {  // the Newton model misled the search: retry from here with Gauss-Newton
+        exact = false;
+        continue;
+      }
+      break;
+    }
     if (lane < NV) w.u[lane] = uj;
     mpc_sync();
     const bool stalled = !(e.J - et.J > 1e-15 * fabs(e.J));  // no representable progress left
     e = et;
-    exact = true;
     lambda = 0.0;
-    if (stalled) break;
+    const bool full = alpha == 1.0;
+    if (stalled && (full || !exact)) break;  // converged (or Gauss-Newton cannot progress either)
+    exact = full;  // after a backtracked step take the Gauss-Newton model once
   }
   J = e.J;
   return it;

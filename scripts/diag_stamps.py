@@ -33,7 +33,10 @@ for _ in range(30):
 torch.cuda.synchronize()
 L.cvae_diag_set_stamps(eng._h, C.c_void_p(dbuf.data_ptr()))
 L.cvae_diag_set_wstamps(C.c_void_p(wbuf.data_ptr()))
-eng.train_step(x)  # the measured step: both kernels stamp their blocks
+if os.environ.get("MODE") == "split":
+    eng.forward_backward(x)  # the separate row-chain launch (fastchain_kernel) and dW launch
+else:
+    eng.train_step(x)  # the measured step: both kernels stamp their blocks
 torch.cuda.synchronize()
 L.cvae_diag_set_wstamps(C.c_void_p(0))
 st = dbuf.view(nb, 64).cpu().numpy().astype(np.int64)
