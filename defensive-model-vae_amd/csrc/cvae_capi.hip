@@ -19,6 +19,7 @@
 #include "cvae_wgrad.h"
 #include "cvae_loss.h"
 #include "cvae_fastwgrad.h"
+#include "cvae_widechain.h"
 #include "cvae_extract.h"
 #include "cvae_mpc.h"
 
@@ -77,6 +78,8 @@ struct cvae_handle {
   int lds_bytes = 0;
   int fast_nki = 0;         // > 0: bf16 training runs fchain::fastchain_kernel<fast_nki>
   int fast_lds = 0;
+  bool wide = false;        // bf16 training at BASELINE cfg5's shape runs wchain::widechain_kernel<Cfg5>
+  int wide_lds = 0;
   bool timing = false;
   // timing: per call, a chain of events on the caller's stream; segment i of a
   // call spans ev[i] → ev[i+1] and is named by the kernel launched after ev[i]
@@ -612,6 +615,45 @@ int plan_fast(cvae_handle* h) {
   return CVAE_OK;
 }
 
+// The specialised wide chain (cvae_widechain.h) covers exactly BASELINE cfg5's shape in bf16:
+// S=200, D=6, latent 512, 8+8 layers, hidden 128.  Its compile-time arena offsets are checked
+// against the handle's layout before it is enabled (as fast_layout_matches).
+template <class A>
+bool wide_layout_matches(const cvae_handle* h) {
+  const NetDev& n = h->net;
+  if (n.n_layers != A::NL || n.nbias != A::nbias || n.Bp % 32 != 0 ||
+      (const char*)n.bias_all != h->arena + A::bias_base)
+    return false;
+  const int64_t Bp2 = 2 * (int64_t)n.Bp;
+  for (int l = 0; l < A::NL; ++l) {
+    const LayerDev& L = n.L[l];
+    if (L.Kp != A::Kp(l) || L.Np != A::Np(l) || n.bias_off[l] != A::bias_off(l) || L.f8 ||
+        (char*)L.Wf != h->arena + A::wf(l) || (char*)L.Wb != h->arena + A::wb(l) ||
+        (char*)L.xT != h->arena + A::act0 + Bp2 * A::xrows(l) ||
+        (char*)L.gT != h->arena + A::act0 + Bp2 * A::grows(l))
+      return false;
+    const bool relu = !(l == A::LFC || l == A::LDL);
+    if (L.relu != (relu ? 1 : 0)) return false;
+  }
+  return true;
+}
+
+int plan_wide(cvae_handle* h) {
+  using A = wchain::Cfg5;
+  const cvae_config& c = h->cfg;
+  h->wide = false;
+  const char* env = std::getenv("CVAE_GENERIC");
+  if ((env && env[0] == '1') || c.dtype != CVAE_BF16 || c.n_classes > 0 || c.hidden_dim != wchain::H ||
+      c.seq_len != A::S || c.dim != A::D || c.latent_dim != A::Z || c.n_enc != A::NE || c.n_dec != A::ND)
+    return CVAE_OK;
+  if (!wide_layout_matches<A>(h)) return CVAE_OK;
+  HIPCK(hipFuncSetAttribute((const void*)wchain::widechain_kernel<A>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            A::L_TOTAL));
+  h->wide = true;
+  h->wide_lds = A::L_TOTAL;
+  return CVAE_OK;
+}
+
 // What every training / inference call hands the row chain.
 struct CallX {
   const void* x;
@@ -646,6 +688,16 @@ RowArgs row_args(cvae_handle* h, const CallX& c) {
 bool fast_ok(const cvae_handle* h, const RowArgs& ra) {
   return h->fast_nki > 0 && (((uintptr_t)ra.x) & 15) == 0 && !ra.x_f32 && !ra.ext && !ra.x_relative;
 }
+bool wide_ok(const cvae_handle* h, const RowArgs& ra) {
+  return h->wide && (((uintptr_t)ra.x) & 15) == 0 && (((uintptr_t)ra.eps) & 15) == 0 && !ra.x_f32 && !ra.ext &&
+         !ra.x_relative;
+}
+// rows per workgroup of the training row chain a call runs (its loss partials are per workgroup)
+int chain_rows(const cvae_handle* h, const RowArgs& ra) {
+  if (fast_ok(h, ra)) return fchain::R;
+  if (wide_ok(h, ra)) return wchain::R;
+  return h->R;
+}
 
 // the training row chain (forward + loss + every dX): the specialised bf16 chain where it applies
 template <typename T>
@@ -660,13 +712,18 @@ int launch_train_chain(cvae_handle* h, RowArgs ra, hipStream_t s) {
     return klaunch(h, fchain::fastchain_kernel<19>, dim3(grid), dim3(fchain::NT), h->fast_lds, s, h->arena, ra.x,
                    ra.idx, h->net.Bp, ra.batch, h->net.S, h->net.D, h->net.I, ra);
   }
+  if (std::is_same<T, __bf16>::value && wide_ok(h, ra)) {
+    const int grid = rup_i(ra.batch, 32) / wchain::R;
+    return klaunch(h, wchain::widechain_kernel<wchain::Cfg5>, dim3(grid), dim3(wchain::NT), h->wide_lds, s,
+                   h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra);
+  }
   return launch_rowchain<T, RC_TRAIN>(h, ra, s);
 }
 
 LossArgs make_loss(cvae_handle* h, const RowArgs& ra, float* loss_out, double* loss_accum) {
   LossArgs la{};
   la.partials = h->d_partials;
-  la.ntiles = rup_i(ra.batch, 32) / h->R;
+  la.ntiles = rup_i(ra.batch, 32) / chain_rows(h, ra);
   la.batch = ra.batch;
   la.w_recon = ra.w_recon; la.w_kld = ra.w_kld; la.w_start = ra.w_start; la.w_time = ra.w_time;
   la.loss_out = loss_out; la.loss_accum = loss_accum;
@@ -810,6 +867,7 @@ int cvae_create(const cvae_config* cfg, int device, cvae_handle** out) {
   rc = alloc_arena(h);
   if (!rc) rc = is16(h) ? set_lds_attrs<__bf16>(h) : set_lds_attrs<float>(h);
   if (!rc) rc = plan_fast(h);
+  if (!rc) rc = plan_wide(h);
   if (rc) { cvae_destroy(h); return rc; }
   *out = h;
   return CVAE_OK;
@@ -854,6 +912,12 @@ int cvae_config_info(const cvae_config* cfg, int64_t* total_params, int* n_tenso
 int cvae_workspace_bytes(const cvae_handle* h, int64_t* bytes) {
   if (!h || !bytes) return fail(CVAE_E_INVALID, "null argument");
   *bytes = h->arena_bytes;
+  return CVAE_OK;
+}
+
+int cvae_train_kernel(const cvae_handle* h, int* kind) {
+  if (!h || !kind) return fail(CVAE_E_INVALID, "null argument");
+  *kind = h->fast_nki > 0 ? CVAE_KERNEL_FAST : h->wide ? CVAE_KERNEL_WIDE : CVAE_KERNEL_GENERIC;
   return CVAE_OK;
 }
 

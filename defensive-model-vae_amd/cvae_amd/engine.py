@@ -470,6 +470,14 @@ class CVAEEngine:
         check(lib().cvae_sync_words(self._h, out), "cvae_sync_words")
         return list(out)
 
+    @property
+    def train_kernel(self):
+        """'generic', 'fast' (reference architecture, bf16) or 'wide' (BASELINE cfg5 shape, bf16):
+        the training row chain this engine runs (cvae_train_kernel)."""
+        k = C.c_int()
+        check(lib().cvae_train_kernel(self._h, C.byref(k)))
+        return ("generic", "fast", "wide")[k.value]
+
     def workspace_bytes(self):
         b = C.c_int64()
         check(lib().cvae_workspace_bytes(self._h, C.byref(b)))

@@ -132,6 +132,14 @@ int cvae_workspace_bytes(const cvae_handle* h, int64_t* bytes);
  * [split, total), CVAE_PART_DW_REST is [0, split). */
 int cvae_bucket_split(const cvae_handle* h, int64_t* split);
 
+/* Which training row chain this handle runs for the usual call (16-B aligned operand-dtype x, no
+ * external gradients): CVAE_KERNEL_GENERIC (the step interpreter, any shape), CVAE_KERNEL_FAST
+ * (bf16, the reference architecture: hidden 128, latent 8, 4+4 layers, seq_len*dim 600) or
+ * CVAE_KERNEL_WIDE (bf16, BASELINE cfg5's shape: seq_len 200, dim 6, latent 512, 8+8 layers).
+ * Introspection only (no reference counterpart); CVAE_GENERIC=1 at creation forces the generic. */
+enum cvae_train_kernel_kind { CVAE_KERNEL_GENERIC = 0, CVAE_KERNEL_FAST = 1, CVAE_KERNEL_WIDE = 2 };
+int cvae_train_kernel(const cvae_handle* h, int* kind);
+
 /* Rebuild the device copies of the weights (padded operand-dtype W and Wᵀ,
  * padded fp32 biases) from the flat fp32 master `params`.  Call after the
  * caller writes parameters (init, load_state_dict, an optimizer outside this

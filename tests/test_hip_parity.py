@@ -553,6 +553,80 @@ def test_wide_cfg5_generate(cvae):
     assert rel_l2(rel.cpu().numpy(), want.numpy()) < 1e-5
 
 
+def _wide_pair(cvae, monkeypatch, B, seed=0):
+    """Two bf16 engines at the cfg5 shape on the same weights: the specialised wide chain
+    (cvae_widechain.h) and the generic interpreter (CVAE_GENERIC=1 at creation)."""
+    ref, m, eng, x, eps = _wide(cvae, "bf16", B, seed)
+    monkeypatch.setenv("CVAE_GENERIC", "1")
+    m2 = cvae.ConditionalTrajectoryVAE(WIDE["S"], WIDE["D"], WIDE["Z"], 128, WIDE["n_enc"], WIDE["n_dec"])
+    m2.load_state_dict(ref.state_dict())
+    e2 = m2.attach(dtype="bf16", max_batch=max(B, 32), device="cuda:0")
+    monkeypatch.delenv("CVAE_GENERIC")
+    assert eng.train_kernel == "wide" and e2.train_kernel == "generic"
+    return ref, m, eng, m2, e2, x, eps
+
+
+@pytest.mark.parametrize("B", [37, 200])
+def test_wide_chain_matches_generic_and_emulation(cvae, monkeypatch, B):
+    """The specialised cfg5 row chain against the generic interpreter (same rounding points, fp32
+    summation order aside) and against the CPU emulation of those rounding points, ragged last
+    tile (B=37) and a gathered batch (B=200 rows of 300 by index)."""
+    ref, m, eng, m2, e2, x, eps = _wide_pair(cvae, monkeypatch, B)
+    x = x.to(torch.bfloat16).float()
+    if B == 200:
+        pool = torch.randn(300, WIDE["S"], WIDE["D"], generator=torch.Generator().manual_seed(9)).to(torch.bfloat16)
+        idx = torch.randperm(300, generator=torch.Generator().manual_seed(3))[:B]
+        x = pool[idx].float()
+        lw = eng.forward_backward(pool.cuda(), idx=idx.cuda(), eps=eps).cpu().numpy()
+    else:
+        lw = eng.forward_backward(x, eps=eps).cpu().numpy()
+    lg = e2.forward_backward(x, eps=eps).cpu().numpy()
+    np.testing.assert_allclose(lw, lg, rtol=2e-3, atol=1e-6)
+    gw, gg = _grads(m, eng), _grads(m2, e2)
+    for k in gw:
+        assert rel_l2(gw[k], gg[k]) < 1e-2, (k, rel_l2(gw[k], gg[k]))
+    p = {k: v.numpy() for k, v in ref.state_dict().items()}
+    ne, nd = WIDE["n_enc"], WIDE["n_dec"]
+    r, mu, lv, hc, c = cvae_np.forward(p, x.numpy(), eps.numpy(), n_enc=ne, n_dec=nd, q=cvae_np.bf16)
+    np.testing.assert_allclose(lw, cvae_np.losses(r, c["rel"], mu, lv), rtol=3e-3, atol=1e-6)
+    ge = cvae_np.backward(p, c, r, mu, lv, n_enc=ne, n_dec=nd)
+    for k in cvae_np.param_keys(ne, nd):
+        assert rel_l2(gw[k], ge[k]) < 3e-2, (k, rel_l2(gw[k], ge[k]))
+
+
+def test_wide_chain_philox_and_training_match_generic(cvae, monkeypatch):
+    """In-kernel Philox eps (keyed by the global row: eps_row0) draws the same noise in the wide
+    chain as in the generic interpreter; three full training steps (dW ⊕ Adam behind each chain)
+    stay within the bf16 summation-order distance of the generic run; and the wide chain is
+    deterministic (two identical runs are bit-equal)."""
+    B = 96
+    ref, m, eng, m2, e2, x, _ = _wide_pair(cvae, monkeypatch, B)
+    xd = x.to("cuda", torch.bfloat16)
+    lw = eng.forward_backward(xd, row0=640).cpu().numpy()
+    lg = e2.forward_backward(xd, row0=640).cpu().numpy()
+    np.testing.assert_allclose(lw, lg, rtol=2e-3, atol=1e-6)
+    gw, gg = _grads(m, eng), _grads(m2, e2)
+    for k in gw:
+        assert rel_l2(gw[k], gg[k]) < 1e-2, (k, rel_l2(gw[k], gg[k]))
+    p0 = eng.params.clone()
+    for _ in range(3):
+        eng.train_step(xd)
+        e2.train_step(xd)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(eng.loss.cpu().numpy(), e2.loss.cpu().numpy(), rtol=3e-3, atol=1e-6)
+    dp = (eng.params - e2.params).norm() / (eng.params - p0).norm()
+    assert float(dp) < 2e-2, float(dp)
+    # determinism: a second wide engine from the same state replays bit for bit
+    m3 = cvae.ConditionalTrajectoryVAE(WIDE["S"], WIDE["D"], WIDE["Z"], 128, WIDE["n_enc"], WIDE["n_dec"])
+    m3.load_state_dict(ref.state_dict())
+    e3 = m3.attach(dtype="bf16", max_batch=B, device="cuda:0")
+    e3.forward_backward(xd, row0=640)
+    for _ in range(3):
+        e3.train_step(xd)
+    torch.cuda.synchronize()
+    assert torch.equal(e3.params, eng.params) and torch.equal(e3.loss, eng.loss)
+
+
 def test_train_cli_end_to_end(cvae, golden, tmp_path):
     """python -m cvae_amd.train (the reference __main__ as a CLI): two epochs on the sce1 rows,
     checkpoint with the 24 reference keys and the loss CSV written."""
