@@ -713,6 +713,7 @@ int launch_train_chain(cvae_handle* h, RowArgs ra, hipStream_t s) {
                    ra.idx, h->net.Bp, ra.batch, h->net.S, h->net.D, h->net.I, ra);
   }
   if (std::is_same<T, __bf16>::value && wide_ok(h, ra)) {
+    ra.stamps = h->d_stamps;
     const int grid = rup_i(ra.batch, 32) / wchain::R;
     return klaunch(h, wchain::widechain_kernel<wchain::Cfg5>, dim3(grid), dim3(wchain::NT), h->wide_lds, s,
                    h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra);

@@ -34,7 +34,6 @@ using fchain::H;
 using fchain::NT;
 using fchain::NW;
 using fchain::R;
-using fchain::arena4;
 using fchain::bf16x4;
 using fchain::from_bf4;
 using fchain::ioff;
@@ -98,15 +97,19 @@ struct Arch {
   static constexpr int L_HCAT = L_U, L_DCAT = L_HCAT + 2 * H * 32, L_RCH0 = L_DCAT + ZH * 32,
                        L_GD0 = L_RCH0 + S * R * 4, L_UEND = L_GD0 + S * R * 4, L_GFC = L_U;
   static_assert(2 * Z * 32 <= L_UEND - L_U, "the fc-backward image fits in the dead forward buffers");
-  static constexpr int L_BIAS = L_UEND, L_PART = L_BIAS + nbias * 4, L_TOTAL = L_PART + NW * 8 * 4;
+  static constexpr int L_BIAS = L_UEND, L_PART = L_BIAS + nbias * 4, L_STAMPS = L_PART + NW * 8 * 4,
+                       L_TOTAL = L_STAMPS + (CVAE_DIAG_STAMPS ? 64 * 8 : 0);
   static_assert(L_TOTAL <= 160 * 1024, "LDS");
 };
 
 // One GEMM of the chain as its weight stream sees it: the operand (layer, forward Wf / backward
 // Wb), its K chunks KC, the n-tiles of the output (NTL) and this wave's share (TS slots: tile
 // wave + 8·slot; a slot past NTL reloads the last tile and its result is dropped).
+// GRP > 0: the slots run in TS/GRP groups of GRP (group p = slots p, p + TS/GRP, ..), each group's
+// whole K before the next (its epilogue then overlaps the next group's stream; the X operand, KC
+// chunks, is read once and held); GRP = 0: K-chunk-major over all slots (X streamed).
 struct StepInfo {
-  int layer, bwd, KC, TS, NTL;
+  int layer, bwd, KC, TS, NTL, GRP;
 };
 
 template <class A>
@@ -118,11 +121,11 @@ struct Plan {
     if (s == k++) return {A::LC1, 0, H / 32, 1, H / 16};
     for (int i = 1; i < A::NE; ++i)
       if (s == k++) return {A::LE(i), 0, H / 32, 1, H / 16};
-    if (s == k++) return {A::LFC, 0, 2 * H / 32, A::Z / 64, A::Z / 8};
+    if (s == k++) return {A::LFC, 0, 2 * H / 32, A::Z / 64, A::Z / 8, 2};
     if (s == k++) return {A::LD0, 0, A::ZH / 32, 1, H / 16};
     for (int i = 1; i < A::ND - 1; ++i)
       if (s == k++) return {A::LD(i), 0, H / 32, 1, H / 16};
-    if (s == k++) return {A::LDL, 0, H / 32, (A::Ip / 16 + NW - 1) / NW, A::Ip / 16};
+    if (s == k++) return {A::LDL, 0, H / 32, (A::Ip / 16 + NW - 1) / NW, A::Ip / 16, 1};
     if (s == k++) return {A::LDL, 1, A::NKI, 1, H / 16};
     for (int i = A::ND - 2; i >= 1; --i)
       if (s == k++) return {A::LD(i), 1, H / 32, 1, H / 16};
@@ -131,7 +134,7 @@ struct Plan {
     for (int i = A::NE - 1; i >= 1; --i)
       if (s == k++) return {A::LE(i), 1, H / 32, 1, H / 16};
     if (s == k++) return {A::LC1, 1, H / 32, 1, H / 16};
-    return {-1, 0, 0, 0, 0};
+    return {-1, 0, 0, 0, 0, 0};
   }
   static constexpr int nsteps() {
     int s = 0;
@@ -171,7 +174,9 @@ __device__ __forceinline__ void ring_load(Ring<P>& ring, const char* AR, int wav
   if constexpr (G < PL::total) {
     constexpr int s = PL::step_of(G);
     constexpr StepInfo st = PL::step(s);
-    constexpr int j = G - PL::start(s), kc = j / st.TS, slot = j % st.TS;
+    constexpr int j = G - PL::start(s);
+    constexpr int NGR = st.GRP ? st.TS / st.GRP : 1, GS = st.GRP ? st.GRP : st.TS;  // groups, slots per group
+    constexpr int grp = j / (st.KC * GS), kc = (j / GS) % st.KC, slot = grp + NGR * (j % GS);
     constexpr int64_t base = st.bwd ? A::wb(st.layer) : A::wf(st.layer);
     int w = wave;
     asm volatile("" : "+s"(w));  // recomputed per item: hoisted, ~400 item addresses would be live SGPRs
@@ -184,12 +189,17 @@ __device__ __forceinline__ void ring_load(Ring<P>& ring, const char* AR, int wav
 
 // acc[slot] = X·Wᵀ for this wave's n-tiles of step S: X chunk kc read once (two transposed LDS
 // reads), multiplied by every slot's fragment; each consumed ring slot is refilled P items ahead
-template <class A, int P, int S, int TS>
+struct NoSide {
+  template <class C>
+  __device__ void operator()(C) const {}
+};
+// side(integral_constant<c>) runs after chunk c: VALU work placed inside a stream-bound GEMM
+template <class A, int P, int S, int TS, class Side = NoSide>
 __device__ __forceinline__ void gemm(Ring<P>& ring, const __bf16* img, f32x4 (&acc)[TS], const char* AR, int wave,
-                                     int lane) {
+                                     int lane, Side&& side = Side{}) {
   using PL = Plan<A>;
   constexpr StepInfo st = PL::step(S);
-  static_assert(st.TS == TS, "accumulator slots");
+  static_assert(st.TS == TS && st.GRP == 0, "accumulator slots");
   constexpr int G0 = PL::start(S);
   sfor<0, TS>([&](auto t) { acc[decltype(t)::value] = f32x4{0.f, 0.f, 0.f, 0.f}; });
   bf16x8 xf = xfrag(img, 0);
@@ -207,7 +217,37 @@ __device__ __forceinline__ void gemm(Ring<P>& ring, const __bf16* img, f32x4 (&a
       asm volatile("" : "+v"(acc[u]));
       ring_load<A, P, g + P>(ring, AR, wave, lane);
     });
+    side(kc);
     xf = xn;
+  });
+}
+
+// The grouped form (StepInfo::GRP > 0): all KC X chunks read first, then per group p its GRP
+// accumulators over the whole K and epi(integral_constant<p>, acc) — the group's epilogue issues
+// while the next group's fragments stream in.
+template <class A, int P, int S, class Epi>
+__device__ __forceinline__ void gemm_grouped(Ring<P>& ring, const __bf16* img, const char* AR, int wave, int lane,
+                                             Epi&& epi) {
+  using PL = Plan<A>;
+  constexpr StepInfo st = PL::step(S);
+  static_assert(st.GRP > 0 && st.TS % st.GRP == 0, "grouped step");
+  constexpr int G0 = PL::start(S), GS = st.GRP, NGR = st.TS / st.GRP, KC = st.KC;
+  bf16x8 xf[KC];
+  sfor<0, KC>([&](auto kc) { xf[decltype(kc)::value] = xfrag(img, decltype(kc)::value); });
+  sfor<0, NGR>([&](auto pp) {
+    constexpr int p = decltype(pp)::value;
+    f32x4 acc[GS];
+    sfor<0, GS>([&](auto i) { acc[decltype(i)::value] = f32x4{0.f, 0.f, 0.f, 0.f}; });
+    sfor<0, KC>([&](auto kc) {
+      constexpr int c = decltype(kc)::value;
+      sfor<0, GS>([&](auto i) {
+        constexpr int u = decltype(i)::value, g = G0 + (p * KC + c) * GS + u;
+        acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[c], ring.r[g % P], acc[u], 0, 0, 0);
+        asm volatile("" : "+v"(acc[u]));  // MFMA(g) before refill(g + P), as in gemm
+        ring_load<A, P, g + P>(ring, AR, wave, lane);
+      });
+    });
+    epi(pp, acc);
   });
 }
 
@@ -215,6 +255,45 @@ __device__ __forceinline__ void gemm(Ring<P>& ring, const __bf16* img, f32x4 (&a
 template <class A, int P>
 __device__ __forceinline__ void ring_fill(Ring<P>& ring, const char* AR, int wave, int lane) {
   sfor<0, P>([&](auto g) { ring_load<A, P, decltype(g)::value>(ring, AR, wave, lane); });
+}
+
+// Arena stores.  An epilogue only writes LDS; the arena copy of each LDS image (the layer's
+// feature-major [Kf][16 rows] slab of this row tile, exactly the image's content) is issued in the
+// NEXT step, while the image is still intact, as 16-B stores: per-CU store ISSUE bounds these
+// (MI355X_MICROARCH.md, store tail: 16-B stores halve it against the 8-B-per-lane epilogue
+// stores of a lane's 4 rows), and they leave the epilogue's critical path.  Write-through (sc1):
+// the lines leave L2 now, for the dW kernel behind, not at the kernel-end writeback.
+#ifndef CVAE_WIDE_SC1
+#define CVAE_WIDE_SC1 1
+#endif
+__device__ __forceinline__ void st16(void* p, u32x4 v) {
+  if (CVAE_DIAG_NOSTORE) return;
+  if (CVAE_WIDE_SC1)
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  else
+    gst<u32x4>(p, v);
+}
+
+// rounds [R0, R1) of the 16-B copy of features [0, NF) of an LDS image (ioff layout) to the arena
+// matrix `mat` (Kf feature rows) at feature offset goff: task k = feature k / 2, rows 8(k & 1)..+7.
+// In the image, row quad q of feature f sits at slot q ^ x (x = (f >> 2) & 3), so a task's two
+// quads are the slot pair 2(h ^ (x >> 1)), +1, in swapped order when x is odd.
+// Threads T0.. take the tasks (T0 = 256: a 128-feature image on waves 4-7, beside another on 0-3).
+template <int NF, int R0, int R1, int T0 = 0>
+__device__ __forceinline__ void img_copy(const __bf16* img, void* mat, int Kf, int goff, int b0) {
+#pragma unroll
+  for (int r = R0; r < R1; ++r) {
+    if (r * NT - T0 >= 2 * NF) break;
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));  // per-round addresses: hoisted, every round's would stay live
+    const int k = r * NT + t - T0;
+    if ((T0 == 0 && 2 * NF % NT == 0) || (k >= 0 && k < 2 * NF)) {
+      const int f = k >> 1, h = k & 1, x = (f >> 2) & 3;
+      u32x4 v = *(const u32x4*)(img + f * 16 + 8 * (h ^ (x >> 1)));
+      if (x & 1) v = u32x4{v[2], v[3], v[0], v[1]};
+      st16((__bf16*)mat + aoff(goff + f, b0 + 8 * h, Kf), v);
+    }
+  }
 }
 
 template <class A, int P>
@@ -236,6 +315,20 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   float* const GD0 = (float*)(smem + A::L_GD0);
   float* const BIAS = (float*)(smem + A::L_BIAS);
   float* const PART = (float*)(smem + A::L_PART);
+  // diagnostic builds only: thread 0's time at every step barrier, kept in LDS, written at the end
+  unsigned long long* const STAMPS = (unsigned long long*)(smem + A::L_STAMPS);
+  int stamp_i = 0;
+  auto bar = [&]() {
+    lbar();
+    if (CVAE_DIAG_STAMPS && threadIdx.x == 0 && stamp_i < 64) STAMPS[stamp_i] = __builtin_amdgcn_s_memrealtime();
+    ++stamp_i;
+  };
+  if (CVAE_DIAG_STAMPS && threadIdx.x == 0) STAMPS[stamp_i++] = __builtin_amdgcn_s_memrealtime();
+  // a stamp inside a step (CVAE_DIAG_STAMPS == 2 only)
+  auto sub = [&]() {
+    if (CVAE_DIAG_STAMPS == 2 && threadIdx.x == 0 && stamp_i < 64) STAMPS[stamp_i] = __builtin_amdgcn_s_memrealtime();
+    if (CVAE_DIAG_STAMPS == 2) ++stamp_i;
+  };
   // arena matrices: recomputed at each use from Bp (one SGPR) — kept, the ~36 64-bit pointers of
   // the chain would be live scalar registers for the whole kernel (SGPR spills)
   auto XT = [&](int l) {
@@ -250,6 +343,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   };
   auto bias = [&](int l, int f) { return BIAS[A::bias_off(l) + f]; };
   const int n = 16 * wave + n16;  // this lane's feature in the 128-wide layers (n-tile = wave)
+  auto img = [&](__bf16* im, int f, bf16x4 v) { *(bf16x4*)(im + ioff(f, q)) = v; };
 
   // ReLU masks: nibble m of this lane (feature n, rows 4q..4q+3) at bits 4(m % 8) of mk[m / 8]
   uint32_t mk[A::NMW];
@@ -278,14 +372,11 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     for (int i = 0; i < 4; ++i) y[i] = (nib >> i) & 1u ? acc[i] : 0.f;
     return to_bf4(y);
   };
-  // one round (one (feature, row quad) task per thread) of the arena copy of the XIN image
-  auto copy_round = [&](int k, void* mat, int Kf) {
-    int t = tid;
-    asm volatile("" : "+v"(t));  // per-round addresses: hoisted, every round's would stay live
-    const int e = k * NT + t;
-    if (e < Ip * 4) arena4(mat, Kf, e >> 2, b0, e & 3, *(const bf16x4*)(XIN + ioff(e >> 2, e & 3)));
-  };
-  constexpr int NCOPY = (Ip * 4 + NT - 1) / NT;  // rounds of one XIN copy
+  using std::integral_constant;
+
+  // the Philox offset of this launch: a scalar load before anything else (a vector load here, under
+  // the counter-pointer branch, made the compiler drain every in-flight load at the fc step)
+  const uint64_t rng_off = a.ctr ? *(const __attribute__((address_space(4))) uint64_t*)a.ctr : a.offset;
 
   Ring<P> ring;
   float s_recon = 0.f, s_kl = 0.f, s_start = 0.f, s_t0 = 0.f, s_relu = 0.f;
@@ -321,13 +412,12 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     for (int k = 0; k < UB; ++k) bv[k] = gld<f32x4>((const float*)(AR + A::bias_base) + 4 * min(k * NT + tid, NB4 - 1));
     // the weight stream queues behind the x tile and the biases (vmcnt retires in order)
     ring_fill<A, P>(ring, AR, wave, lane);
-    if (a.ctr && blk == 0 && tid == 0) adam_precompute(a.ctr, a.lr, a.beta1, a.beta2, a.adam_pre);
+    sub();
     if (tid < 28 * 4) *(uint64_t*)(CIN + (4 + tid / 4) * 16 + 4 * (tid & 3)) = 0ull;
     if (tid < (Ip - I) * 4) *(uint64_t*)(XIN + (I + tid / 4) * 16 + 4 * (tid & 3)) = 0ull;
 #pragma unroll
     for (int k = 0; k < UB; ++k)
       if (k * NT + tid < NB4) ((f32x4*)BIAS)[k * NT + tid] = bv[k];
-    void* const xc0 = XT(A::LC0);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int v = u * NT + tid;
@@ -355,131 +445,131 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
         }
         *(bf16x4*)(XIN + ioff(fl, rq)) = to_bf4(rl);
         *(bf16x4*)(XIN + ioff(fh, rq)) = to_bf4(rh);
-        if (c == 0) {
-          const bf16x4 cs = to_bf4(cv);
-          *(bf16x4*)(CIN + ioff(qd, rq)) = cs;
-          arena4(xc0, A::Kp(A::LC0), qd, b0, rq, cs);
-        }
+        if (c == 0) *(bf16x4*)(CIN + ioff(qd, rq)) = to_bf4(cv);
       }
     }
   }
-  lbar();
+  sub();
+  bar();
 
   const float Bf = (float)a.batch;
   const float inv_BSD = 1.f / (Bf * (float)(S * D)), inv_2B = 1.f / (2.f * Bf), inv_B = 1.f / Bf;
   const float inv_BS1 = S > 1 ? 1.f / (Bf * (float)(S - 1)) : 0.f, inv_BZ = 1.f / (Bf * (float)Z);
   const bool use_start = a.w_start > 0.f, use_time = a.w_time > 0.f;  // Training_VAE.py:247, :256
+  // the x_rel image → xT(E0): rounds of its 16-B copy, over the first encoder steps (done before
+  // the loss epilogue overwrites XIN)
+  constexpr int XR = (2 * Ip + NT - 1) / NT;
+  static_assert(XR <= 5 && NE >= 4, "the x_rel copy runs over C0|E0, C1|E1, E2, E3");
+
+  // eps of the reparameterisation (:199-206), per mu tile k of this lane (latent j, rows 4q..4q+3):
+  // host-given (loaded unconditionally — rows clamped into the batch, any valid address when eps
+  // is drawn in-kernel — a load under a branch drains the weight stream) or Philox keyed by the
+  // global row (data parallelism: eps_row0 = the rank's first row).  The Philox draws (integer
+  // multiplies, ~1 us of VALU per wave) run inside the stream-bound encoder-L1 GEMM.
+  constexpr int NZT = Z / 128;
+  f32x4 ep[NZT];
+  const int rowq = 4 * q + (n16 & 3);  // the row this lane draws (4 latents) before the quad transpose
+  auto draw_eps = [&](auto kk) {
+    constexpr int k = decltype(kk)::value;
+    const int j0 = 16 * (wave + NW * k) + 4 * (n16 >> 2);
+    const float* const ebase = a.eps ? a.eps : (const float*)(AR + A::bias_base);  // global memory either way
+    const int erow = a.eps ? min(b0 + rowq, max(a.batch - 1, 0)) : 0;
+    const f32x4 eh = gld<f32x4>(ebase + (a.eps ? (size_t)erow * Z + j0 : 0));
+    f32x4 e = a.eps ? eh : philox_normal4(a.seed, rng_off, (uint32_t)(a.eps_row0 + b0 + rowq), (uint32_t)j0);
+    if (rowq >= nrows) e = f32x4{0.f, 0.f, 0.f, 0.f};
+    ep[k] = quad_t(e);
+  };
+  auto eps_side = [&](auto cc) {
+    constexpr int c = decltype(cc)::value;
+    if constexpr (c % 8 == 2 && c / 8 < NZT) draw_eps(integral_constant<int, c / 8>{});
+  };
+  static_assert(8 * (NZT - 1) + 2 < A::NKI, "the eps draws fit in the encoder-L1 GEMM");
 
   // ================================================================ forward
   {  // C0 ‖ E0
     f32x4 acc[1];
     gemm<A, P, 0>(ring, CIN, acc, AR, wave, lane);
-    const bf16x4 hc = relu(acc[0], bias(A::LC0, n), std::integral_constant<int, A::MC0>{});
-    *(bf16x4*)(CB + ioff(n, q)) = hc;
-    arena4(XT(A::LC1), A::Kp(A::LC1), n, b0, q, hc);
-    gemm<A, P, PL::sE0>(ring, XIN, acc, AR, wave, lane);
-    const bf16x4 he = relu(acc[0], bias(A::LE0, n), std::integral_constant<int, A::ME(0)>{});
-    *(bf16x4*)(A0 + ioff(n, q)) = he;
-    arena4(XT(A::LE(1)), A::Kp(A::LE(1)), n, b0, q, he);
+    img_copy<32, 0, 1>(CIN, XT(A::LC0), A::Kp(A::LC0), 0, b0);
+    img_copy<Ip, 0, 2>(XIN, XT(A::LE0), A::Kp(A::LE0), 0, b0);
+    img(CB, n, relu(acc[0], bias(A::LC0, n), integral_constant<int, A::MC0>{}));
+    sub();
+    gemm<A, P, PL::sE0>(ring, XIN, acc, AR, wave, lane, eps_side);
+    sub();
+    img(A0, n, relu(acc[0], bias(A::LE0, n), integral_constant<int, A::ME(0)>{}));
   }
-  lbar();
+  bar();
   {  // C1 ‖ E1: h_c goes to both concatenations (fc input at H+n, decoder input at Z+n)
     f32x4 acc[1];
     gemm<A, P, PL::sC1>(ring, CB, acc, AR, wave, lane);
-    const bf16x4 hc = relu(acc[0], bias(A::LC1, n), std::integral_constant<int, A::MC1>{});
-    *(bf16x4*)(HCAT + ioff(H + n, q)) = hc;
-    *(bf16x4*)(DCAT + ioff(Z + n, q)) = hc;
-    arena4(XT(A::LFC), A::Kp(A::LFC), H + n, b0, q, hc);
-    arena4(XT(A::LD0), A::Kp(A::LD0), Z + n, b0, q, hc);
+    img_copy<H, 0, 1, 2 * H>(CB, XT(A::LC1), H, 0, b0);
+    img_copy<Ip, 2, 3>(XIN, XT(A::LE0), A::Kp(A::LE0), 0, b0);
+    const bf16x4 hc = relu(acc[0], bias(A::LC1, n), integral_constant<int, A::MC1>{});
+    img(HCAT, H + n, hc);
+    img(DCAT, Z + n, hc);
   }
   // encoder layers 1 .. NE-1 (input image: E(i-1)'s output, A0 for odd i); the last → h_traj
   sfor<1, NE>([&](auto ii) {
     constexpr int i = decltype(ii)::value;
-    if constexpr (i > 1) lbar();
+    if constexpr (i > 1) bar();
+    __bf16* const in = (i & 1) ? A0 : A1;
     f32x4 acc[1];
-    gemm<A, P, PL::sC1 + i>(ring, (i & 1) ? A0 : A1, acc, AR, wave, lane);
-    const bf16x4 he = relu(acc[0], bias(A::LE(i), n), std::integral_constant<int, A::ME(i)>{});
-    if constexpr (i == NE - 1) {
-      *(bf16x4*)(HCAT + ioff(n, q)) = he;
-      arena4(XT(A::LFC), A::Kp(A::LFC), n, b0, q, he);
-    } else {
-      *(bf16x4*)(((i & 1) ? A1 : A0) + ioff(n, q)) = he;
-      arena4(XT(A::LE(i + 1)), A::Kp(A::LE(i + 1)), n, b0, q, he);
-    }
-    // the x_rel tile → xT(E0): spread over the encoder steps, done before the loss overwrites XIN
-    if constexpr (i <= 5) {
-#pragma unroll
-      for (int k = 2 * (i - 1); k < 2 * i && k < NCOPY; ++k) copy_round(k, XT(A::LE0), A::Kp(A::LE0));
-    }
+    gemm<A, P, PL::sC1 + i>(ring, in, acc, AR, wave, lane);
+    img_copy<H, 0, 1>(in, XT(A::LE(i)), H, 0, b0);
+    if constexpr (i >= 2 && i <= 3) img_copy<Ip, i + 1, i + 2>(XIN, XT(A::LE0), A::Kp(A::LE0), 0, b0);
+    const bf16x4 he = relu(acc[0], bias(A::LE(i), n), integral_constant<int, A::ME(i)>{});
+    img(i == NE - 1 ? HCAT : (i & 1) ? A1 : A0, n, he);
   });
-  static_assert(NCOPY <= 10 && NE >= 6, "the x_rel copy needs 5 encoder steps");
-  lbar();
-  // fc_mu ‖ fc_logvar (:195-196) + reparameterize (:199-206) + KL terms (:243): slot k < Z/128 is
-  // mu tile wave + 8k, slot k + Z/128 the logvar tile of the same latents
-  constexpr int NZT = Z / 128;
-  f32x4 mu[NZT], lv[NZT], ep[NZT];
-  {
-    f32x4 acc[2 * NZT];
-    gemm<A, P, PL::sFC>(ring, HCAT, acc, AR, wave, lane);
-    const uint64_t off = rng_offset(a);
-    const int rowq = 4 * q + (n16 & 3);  // the row this lane draws (4 latents) before the quad transpose
+  bar();
+  // fc_mu ‖ fc_logvar (:195-196) + reparameterize (:199-206) + KL terms (:243): group k = the mu
+  // tile wave + 8k and the logvar tile Z/16 + wave + 8k of the same latents
+  f32x4 mu[NZT], lv[NZT];
+  gemm_grouped<A, P, PL::sFC>(ring, HCAT, AR, wave, lane, [&](auto kk, f32x4(&acc)[2]) {
+    constexpr int k = decltype(kk)::value;
+    if constexpr (k == 0) img_copy<2 * H, 0, 1>(HCAT, XT(A::LFC), A::Kp(A::LFC), 0, b0);
+    const int j = 16 * (wave + NW * k) + n16;
+    const float bm = bias(A::LFC, j), bl = bias(A::LFC, Z + j);
+    f32x4 z;
 #pragma unroll
-    for (int k = 0; k < NZT; ++k) {
-      const int j = 16 * (wave + NW * k) + n16, j0 = 16 * (wave + NW * k) + 4 * (n16 >> 2);
-      f32x4 e = {0.f, 0.f, 0.f, 0.f};
-      if (rowq < nrows)  // Philox keyed by the global row (data parallelism: eps_row0 = the rank's first row)
-        e = a.eps ? gld<f32x4>(a.eps + (size_t)(b0 + rowq) * Z + j0)
-                  : philox_normal4(a.seed, off, (uint32_t)(a.eps_row0 + b0 + rowq), (uint32_t)j0);
-      ep[k] = quad_t(e);  // eps of latent j, rows 4q .. 4q+3
-      const float bm = bias(A::LFC, j), bl = bias(A::LFC, Z + j);
-      f32x4 z;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        mu[k][i] = acc[k][i] + bm;
-        lv[k][i] = acc[NZT + k][i] + bl;
-        const float sd = __expf(0.5f * lv[k][i]);
-        z[i] = mu[k][i] + ep[k][i] * sd;
-        if (4 * q + i < nrows) s_kl += 1.f + lv[k][i] - mu[k][i] * mu[k][i] - __expf(lv[k][i]);
-      }
-      const bf16x4 zh = to_bf4(z);
-      *(bf16x4*)(DCAT + ioff(j, q)) = zh;
-      arena4(XT(A::LD0), A::Kp(A::LD0), j, b0, q, zh);
+    for (int i = 0; i < 4; ++i) {
+      mu[k][i] = acc[0][i] + bm;
+      lv[k][i] = acc[1][i] + bl;
+      const float sd = __expf(0.5f * lv[k][i]);
+      z[i] = mu[k][i] + ep[k][i] * sd;
+      if (4 * q + i < nrows) s_kl += 1.f + lv[k][i] - mu[k][i] * mu[k][i] - __expf(lv[k][i]);
     }
-  }
-  lbar();
+    img(DCAT, j, to_bf4(z));
+  });
+  bar();
   {  // D0 → A0
     f32x4 acc[1];
     gemm<A, P, PL::sD0>(ring, DCAT, acc, AR, wave, lane);
-    const bf16x4 h = relu(acc[0], bias(A::LD0, n), std::integral_constant<int, A::MD(0)>{});
-    *(bf16x4*)(A0 + ioff(n, q)) = h;
-    arena4(XT(A::LD(1)), A::Kp(A::LD(1)), n, b0, q, h);
+    img_copy<A::ZH, 0, 3>(DCAT, XT(A::LD0), A::Kp(A::LD0), 0, b0);
+    img(A0, n, relu(acc[0], bias(A::LD0, n), integral_constant<int, A::MD(0)>{}));
   }
   // decoder layers 1 .. ND-2 (input: D(i-1)'s output, A0 for odd i)
   sfor<1, ND - 1>([&](auto ii) {
     constexpr int i = decltype(ii)::value;
-    lbar();
+    bar();
+    __bf16* const in = (i & 1) ? A0 : A1;
     f32x4 acc[1];
-    gemm<A, P, PL::sD0 + i>(ring, (i & 1) ? A0 : A1, acc, AR, wave, lane);
-    const bf16x4 h = relu(acc[0], bias(A::LD(i), n), std::integral_constant<int, A::MD(i)>{});
-    *(bf16x4*)(((i & 1) ? A1 : A0) + ioff(n, q)) = h;
-    arena4(XT(A::LD(i + 1)), A::Kp(A::LD(i + 1)), n, b0, q, h);
+    gemm<A, P, PL::sD0 + i>(ring, in, acc, AR, wave, lane);
+    img_copy<H, 0, 1>(in, XT(A::LD(i)), H, 0, b0);
+    img((i & 1) ? A1 : A0, n, relu(acc[0], bias(A::LD(i), n), integral_constant<int, A::MD(i)>{}));
   });
-  lbar();
+  bar();
   __bf16* const DLIN = ((ND - 2) & 1) ? A1 : A0;  // input image of the last decoder layer
-  {  // last decoder layer + conditional_vae_loss (:229-268) + dL/drecon, over x_rel in place
-    constexpr StepInfo st = PL::step(PL::sDL);
-    constexpr int G3 = st.TS, NG3 = st.NTL;
-    auto has = [&](int g) { return NW * (g + 1) <= NG3 || wave + NW * g < NG3; };
-    f32x4 accs[G3];
-    gemm<A, P, PL::sDL>(ring, DLIN, accs, AR, wave, lane);
+  {  // last decoder layer + conditional_vae_loss (:229-268) + dL/drecon, over x_rel in
+     // place; one n-tile per group, its loss epilogue beside the next tile's stream
+    constexpr int NG3 = PL::step(PL::sDL).NTL;
     typedef float f32x2 __attribute__((ext_vector_type(2)));
     const float cr = a.w_recon * 2.f;
     f32x2 sr2 = {0.f, 0.f};
-#pragma unroll
-    for (int g = 0; g < G3; ++g) {
-      if (!has(g)) continue;
+    gemm_grouped<A, P, PL::sDL>(ring, DLIN, AR, wave, lane, [&](auto gg, f32x4(&accs)[1]) {
+      constexpr int g = decltype(gg)::value;
+      if constexpr (g == 0) img_copy<H, 0, 1>(DLIN, XT(A::LDL), H, 0, b0);
+      if (!(NW * (g + 1) <= NG3 || wave + NW * g < NG3)) return;  // wave-uniform: tile past the output
       const int t = wave + NW * g;
-      const f32x4 acc = accs[g];
+      const f32x4 acc = accs[0];
       const int f = 16 * t + n16;
       f32x4 gi = {0.f, 0.f, 0.f, 0.f};
       if (f < I) {
@@ -520,10 +610,10 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
         }
       }
       *(bf16x4*)(XIN + ioff(f, q)) = to_bf4(gi);  // pad features f >= I: 0
-    }
+    });
     s_recon += sr2[0] + sr2[1];
   }
-  lbar();
+  bar();
   // time-monotonicity term relu(r_s − r_{s+1}) (:261-262, ReLU'(0) = 0) into the time channel of
   // dL/drecon: one task per (timestep, row quad)
   {
@@ -549,41 +639,36 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
       *(bf16x4*)(XIN + ioff(f, qq)) = to_bf4(gv);
     }
   }
-  lbar();
+  bar();
 
   // ================================================================ backward
+  // dL/drecon → gT(DL): rounds of its 16-B copy, over the decoder backward steps
+  static_assert(XR <= ND - 1, "the dL/drecon copy runs over the decoder backward steps");
   {  // last decoder layer ᵀ: dL/d h_D(ND-2) = GL · W_DL, ReLU mask of D(ND-2) → A0
     f32x4 acc[1];
     gemm<A, P, PL::sDLb>(ring, XIN, acc, AR, wave, lane);
-    const bf16x4 h = masked(acc[0], std::integral_constant<int, A::MD(ND - 2)>{});
-    *(bf16x4*)(A0 + ioff(n, q)) = h;
-    arena4(GT(A::LD(ND - 2)), A::Np(A::LD(ND - 2)), n, b0, q, h);
+    img_copy<Ip, 0, 1>(XIN, GT(A::LDL), A::Np(A::LDL), 0, b0);
+    img(A0, n, masked(acc[0], integral_constant<int, A::MD(ND - 2)>{}));
   }
-  // dL/drecon → gT(DL), spread over the decoder backward steps
-  copy_round(0, GT(A::LDL), A::Np(A::LDL));
-  copy_round(1, GT(A::LDL), A::Np(A::LDL));
-  static_assert(ND >= 6, "the dL/drecon copy needs 5 decoder backward steps");
-  // D(i)ᵀ for i = ND-2 .. 1: input = the gradient image of D(i)'s output, mask of D(i-1)
+  // D(i)ᵀ for i = ND-2 .. 1: input = dL/d(pre-activation of D(i)) = gT(D(i)), mask of D(i-1)
   sfor<1, ND - 1>([&](auto kk) {
     constexpr int k = decltype(kk)::value, i = ND - 1 - k;  // k-th decoder backward step after DLᵀ
-    lbar();
+    bar();
+    __bf16* const in = (k & 1) ? A0 : A1;
     f32x4 acc[1];
-    gemm<A, P, PL::sDLb + k>(ring, (k & 1) ? A0 : A1, acc, AR, wave, lane);
-    const bf16x4 h = masked(acc[0], std::integral_constant<int, A::MD(i - 1)>{});
-    *(bf16x4*)(((k & 1) ? A1 : A0) + ioff(n, q)) = h;
-    arena4(GT(A::LD(i - 1)), A::Np(A::LD(i - 1)), n, b0, q, h);
-    if constexpr (k <= 4) {
-#pragma unroll
-      for (int r = 2 * k; r < 2 * k + 2 && r < NCOPY; ++r) copy_round(r, GT(A::LDL), A::Np(A::LDL));
-    }
+    gemm<A, P, PL::sDLb + k>(ring, in, acc, AR, wave, lane);
+    img_copy<H, 0, 1>(in, GT(A::LD(i)), H, 0, b0);
+    if constexpr (k < XR) img_copy<Ip, k, k + 1>(XIN, GT(A::LDL), A::Np(A::LDL), 0, b0);
+    img((k & 1) ? A1 : A0, n, masked(acc[0], integral_constant<int, A::MD(i - 1)>{}));
   });
-  lbar();
+  bar();
   // D0ᵀ: [dz ‖ dh_c(decoder share)]; dz → KL/reparameterisation backward → dL/d[mu ‖ logvar]
-  __bf16* const D0IN = ((ND - 2) & 1) ? A1 : A0;  // gradient image of D0's output
+  __bf16* const D0IN = ((ND - 2) & 1) ? A1 : A0;  // gT(D0) image
   f32x4 dhc2;
   {
     f32x4 acc[NZT + 1];
     gemm<A, P, PL::sD0b>(ring, D0IN, acc, AR, wave, lane);
+    img_copy<H, 0, 1>(D0IN, GT(A::LD0), H, 0, b0);
 #pragma unroll
     for (int k = 0; k < NZT; ++k) {
       const int j = 16 * (wave + NW * k) + n16;
@@ -595,63 +680,70 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
         gm[i] = live ? a.w_kld * mu[k][i] * inv_BZ + acc[k][i] : 0.f;
         gl[i] = live ? a.w_kld * 0.5f * (__expf(lv[k][i]) - 1.f) * inv_BZ + acc[k][i] * ep[k][i] * 0.5f * sd : 0.f;
       }
-      const bf16x4 hm = to_bf4(gm), hl = to_bf4(gl);
-      *(bf16x4*)(GFC + ioff(j, q)) = hm;
-      *(bf16x4*)(GFC + ioff(Z + j, q)) = hl;
-      arena4(GT(A::LFC), A::Np(A::LFC), j, b0, q, hm);
-      arena4(GT(A::LFC), A::Np(A::LFC), Z + j, b0, q, hl);
+      img(GFC, j, to_bf4(gm));
+      img(GFC, Z + j, to_bf4(gl));
     }
     dhc2 = acc[NZT];  // feature n of dh_c: the lane that masks it in the fc backward
   }
-  lbar();
+  bar();
   {  // fcᵀ: dh = G_fc · W_fc → h_traj gradient (mask E(NE-1)) and h_c gradient (+ decoder share, mask C1)
     f32x4 acc[2];
     gemm<A, P, PL::sFCb>(ring, GFC, acc, AR, wave, lane);
-    const bf16x4 ht = masked(acc[0], std::integral_constant<int, A::ME(NE - 1)>{});
-    *(bf16x4*)(A0 + ioff(n, q)) = ht;
-    arena4(GT(A::LE(NE - 1)), A::Np(A::LE(NE - 1)), n, b0, q, ht);
-    const bf16x4 hc = masked(acc[1] + dhc2, std::integral_constant<int, A::MC1>{});
-    *(bf16x4*)(CB + ioff(n, q)) = hc;
-    arena4(GT(A::LC1), A::Np(A::LC1), n, b0, q, hc);
+    sub();
+    img_copy<2 * Z, 0, (4 * Z + NT - 1) / NT>(GFC, GT(A::LFC), A::Np(A::LFC), 0, b0);
+    img(A0, n, masked(acc[0], integral_constant<int, A::ME(NE - 1)>{}));
+    img(CB, n, masked(acc[1] + dhc2, integral_constant<int, A::MC1>{}));
   }
-  // E(i)ᵀ for i = NE-1 .. 2 (input: gradient image of E(i)'s output), mask of E(i-1)
+  // E(i)ᵀ for i = NE-1 .. 2 (input: gT(E(i)) image), mask of E(i-1)
   sfor<0, NE - 2>([&](auto kk) {
     constexpr int k = decltype(kk)::value, i = NE - 1 - k;
-    lbar();
+    bar();
+    __bf16* const in = (k & 1) ? A1 : A0;
     f32x4 acc[1];
-    gemm<A, P, PL::sFCb + 1 + k>(ring, (k & 1) ? A1 : A0, acc, AR, wave, lane);
-    const bf16x4 h = masked(acc[0], std::integral_constant<int, A::ME(i - 1)>{});
-    *(bf16x4*)(((k & 1) ? A0 : A1) + ioff(n, q)) = h;
-    arena4(GT(A::LE(i - 1)), A::Np(A::LE(i - 1)), n, b0, q, h);
+    gemm<A, P, PL::sFCb + 1 + k>(ring, in, acc, AR, wave, lane);
+    img_copy<H, 0, 1>(in, GT(A::LE(i)), H, 0, b0);
+    if constexpr (k == 0) img_copy<H, 0, 1, 2 * H>(CB, GT(A::LC1), H, 0, b0);
+    img((k & 1) ? A0 : A1, n, masked(acc[0], integral_constant<int, A::ME(i - 1)>{}));
   });
-  lbar();
-  {  // E1ᵀ ‖ C1ᵀ: the last two gradients only feed the dW kernel
+  bar();
+  {  // E1ᵀ ‖ C1ᵀ: the last two gradients, gT(E0) and gT(C0), only feed the dW kernel
+    __bf16* const in = ((NE - 2) & 1) ? A1 : A0;  // gT(E1) image
+    __bf16* const oE = ((NE - 2) & 1) ? A0 : A1;  // free
+    __bf16* const oC = GFC;                        // free (U region)
     f32x4 acc[1];
-    gemm<A, P, PL::sC1b - 1>(ring, ((NE - 2) & 1) ? A1 : A0, acc, AR, wave, lane);
-    arena4(GT(A::LE0), A::Np(A::LE0), n, b0, q, masked(acc[0], std::integral_constant<int, A::ME(0)>{}));
+    gemm<A, P, PL::sC1b - 1>(ring, in, acc, AR, wave, lane);
+    img_copy<H, 0, 1>(in, GT(A::LE(1)), H, 0, b0);
+    img(oE, n, masked(acc[0], integral_constant<int, A::ME(0)>{}));
     gemm<A, P, PL::sC1b>(ring, CB, acc, AR, wave, lane);
-    arena4(GT(A::LC0), A::Np(A::LC0), n, b0, q, masked(acc[0], std::integral_constant<int, A::MC0>{}));
+    img(oC, n, masked(acc[0], integral_constant<int, A::MC0>{}));
+    // ---- loss partial sums (deterministic order)
+    s_recon = wave_sum(s_recon);
+    s_kl = wave_sum(s_kl);
+    s_start = wave_sum(s_start);
+    s_t0 = wave_sum(s_t0);
+    s_relu = wave_sum(s_relu);
+    if (lane == 0) {
+      PART[wave * 8 + 0] = s_recon;
+      PART[wave * 8 + 1] = s_kl;
+      PART[wave * 8 + 2] = s_start;
+      PART[wave * 8 + 3] = s_t0;
+      PART[wave * 8 + 4] = s_relu;
+    }
+    bar();
+    img_copy<H, 0, 1>(oE, GT(A::LE0), H, 0, b0);
+    img_copy<H, 0, 1, 2 * H>(oC, GT(A::LC0), H, 0, b0);
   }
-
-  // ---- loss partial sums (deterministic order)
-  s_recon = wave_sum(s_recon);
-  s_kl = wave_sum(s_kl);
-  s_start = wave_sum(s_start);
-  s_t0 = wave_sum(s_t0);
-  s_relu = wave_sum(s_relu);
-  if (lane == 0) {
-    PART[wave * 8 + 0] = s_recon;
-    PART[wave * 8 + 1] = s_kl;
-    PART[wave * 8 + 2] = s_start;
-    PART[wave * 8 + 3] = s_t0;
-    PART[wave * 8 + 4] = s_relu;
-  }
-  lbar();
   if (tid < 5) {
     float s = 0.f;
     for (int w = 0; w < NW; ++w) s += PART[w * 8 + tid];
     gst<float>(a.partials + blk * 8 + tid, s);
   }
+  // device counters: this launch begins optimizer step ctr[1] + 1 and precomputes its Adam scalars
+  // for the dW kernel behind it — one lane of block 0, at the end (its loads and the f64 pow, under
+  // a branch, would otherwise stall the wave's weight stream)
+  if (a.ctr && blk == 0 && tid == 0) adam_precompute(a.ctr, a.lr, a.beta1, a.beta2, a.adam_pre);
+  if (CVAE_DIAG_STAMPS && a.stamps && tid < 64)
+    gst<unsigned long long>(a.stamps + blk * 64 + tid, tid < stamp_i ? STAMPS[tid] : 0ull);
 }
 
 // BASELINE cfg5: S=200, D=6, latent 512, 8 + 8 layers (hidden 128)

@@ -17,9 +17,10 @@ from cvae_amd._lib import lib  # noqa: E402
 B = int(os.environ.get("B", "1024"))
 dtype = os.environ.get("DT", "bf16")
 torch.manual_seed(0)
-m = ConditionalTrajectoryVAE(100, 6, 8)
+WIDE = os.environ.get("WIDE") == "1"  # BASELINE cfg5's shape (the wide chain)
+m = ConditionalTrajectoryVAE(200, 6, 512, 128, 8, 8) if WIDE else ConditionalTrajectoryVAE(100, 6, 8)
 eng = m.attach(dtype=dtype, max_batch=B)
-x = eng.as_input(torch.randn(B, 100, 6))
+x = eng.as_input(torch.randn(B, 200, 6) if WIDE else torch.randn(B, 100, 6))
 L = lib()
 L.cvae_diag_set_stamps.argtypes = [C.c_void_p, C.c_void_p]
 L.cvae_diag_set_wstamps.argtypes = [C.c_void_p]
@@ -45,6 +46,15 @@ d = np.diff(st[:, :k], axis=1) * 10  # ns
 t0 = st[:, 0].min()
 print(f"blocks={nb} stamps={k} kernel span={(st[:, k-1].max() - t0) * 10 / 1000:.2f} us; start skew={(st[:,0].max()-t0)*10/1000:.2f} us")
 names = ["prologue", "xT copies+C0"] + [f"step{i}" for i in range(1, 64)]
+if WIDE:
+    names = (["prologue", "C0|E0", "C1|E1"] + [f"E{i}" for i in range(2, 8)] + ["FC", "D0"]
+             + [f"D{i}" for i in range(1, 7)] + ["D7+loss", "fixup", "D7b"] + [f"D{i}b" for i in range(6, 0, -1)]
+             + ["D0b", "FCb"] + [f"E{i}b" for i in range(7, 1, -1)] + ["E1b|C1b", "partials"])
+    if os.environ.get("SUB") == "1":  # CVAE_DIAG_STAMPS=2: stamps inside some steps
+        names = (["pro:issue", "pro:transform", "pro:bar", "C0+copies", "E0 gemm", "E0 epi", "C1|E1"]
+                 + [f"E{i}" for i in range(2, 8)] + ["FC", "D0"] + [f"D{i}" for i in range(1, 7)]
+                 + ["D7+loss", "fixup", "D7b"] + [f"D{i}b" for i in range(6, 0, -1)]
+                 + ["D0b", "FCb gemm", "FCb epi"] + [f"E{i}b" for i in range(7, 1, -1)] + ["E1b|C1b", "partials"])
 for i in range(k - 1):
     print(f"{names[i]:>14s} {i:2d}: median {np.median(d[:, i]) / 1000:7.3f} us   max {d[:, i].max() / 1000:7.3f} us")
 
