@@ -80,6 +80,8 @@ struct cvae_handle {
   int fast_lds = 0;
   bool wide = false;        // bf16 training at BASELINE cfg5's shape runs wchain::widechain_kernel<Cfg5>
   int wide_lds = 0;
+  bool ring = false;        // the fast configuration's training chain runs wchain::widechain_kernel<Cfg2>
+  int ring_lds = 0;
   bool timing = false;
   // timing: per call, a chain of events on the caller's stream; segment i of a
   // call spans ev[i] → ev[i+1] and is named by the kernel launched after ev[i]
@@ -627,7 +629,7 @@ bool wide_layout_matches(const cvae_handle* h) {
   const int64_t Bp2 = 2 * (int64_t)n.Bp;
   for (int l = 0; l < A::NL; ++l) {
     const LayerDev& L = n.L[l];
-    if (L.Kp != A::Kp(l) || L.Np != A::Np(l) || n.bias_off[l] != A::bias_off(l) || L.f8 ||
+    if (L.Kp != A::Kp(l) || L.Np != A::Np(l) || n.bias_off[l] != A::bias_off(l) || (L.f8 != 0) != A::f8(l) ||
         (char*)L.Wf != h->arena + A::wf(l) || (char*)L.Wb != h->arena + A::wb(l) ||
         (char*)L.xT != h->arena + A::act0 + Bp2 * A::xrows(l) ||
         (char*)L.gT != h->arena + A::act0 + Bp2 * A::grows(l))
@@ -638,20 +640,47 @@ bool wide_layout_matches(const cvae_handle* h) {
   return true;
 }
 
-int plan_wide(cvae_handle* h) {
-  using A = wchain::Cfg5;
+// The reference architecture (the fast configuration, S=100: BASELINE cfg2) on the single-ring
+// weight-stream chain (cvae_widechain.h, small-latent form) instead of fastchain_kernel's per-step
+// register prefetch: the per-CU L2 stream stays busy across step barriers.  Opt-in (CVAE_RING=1 at
+// creation): measured equal to fastchain_kernel at B = 1024 (18.4-18.9 vs 18.5 us; both stream
+// ~1.05 MB of weight fragments per workgroup at the per-CU L2 rate).  The fused single
+// launch (CVAE_FUSE=1) is fastchain's.
+int plan_ring(cvae_handle* h) {
+  using A = wchain::Cfg2;
   const cvae_config& c = h->cfg;
-  h->wide = false;
-  const char* env = std::getenv("CVAE_GENERIC");
-  if ((env && env[0] == '1') || c.dtype != CVAE_BF16 || c.n_classes > 0 || c.hidden_dim != wchain::H ||
-      c.seq_len != A::S || c.dim != A::D || c.latent_dim != A::Z || c.n_enc != A::NE || c.n_dec != A::ND)
-    return CVAE_OK;
+  h->ring = false;
+  const char* env = std::getenv("CVAE_RING");
+  if (!(env && env[0] == '1') || h->fast_nki != 19 || c.seq_len != A::S || c.dim != A::D) return CVAE_OK;
+  if (!wide_layout_matches<A>(h)) return CVAE_OK;
+  HIPCK(hipFuncSetAttribute((const void*)wchain::widechain_kernel<A>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            A::L_TOTAL));
+  h->ring = true;
+  h->ring_lds = A::L_TOTAL;
+  return CVAE_OK;
+}
+
+template <class A>
+int plan_wide_as(cvae_handle* h) {
   if (!wide_layout_matches<A>(h)) return CVAE_OK;
   HIPCK(hipFuncSetAttribute((const void*)wchain::widechain_kernel<A>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             A::L_TOTAL));
   h->wide = true;
   h->wide_lds = A::L_TOTAL;
   return CVAE_OK;
+}
+
+// bf16 runs wchain::Cfg5, CVAE_FP8 wchain::Cfg5F8 (e4m3 forward GEMMs)
+int plan_wide(cvae_handle* h) {
+  using A = wchain::Cfg5;
+  const cvae_config& c = h->cfg;
+  h->wide = false;
+  const char* env = std::getenv("CVAE_GENERIC");
+  if ((env && env[0] == '1') || (c.dtype != CVAE_BF16 && c.dtype != CVAE_FP8) || c.n_classes > 0 ||
+      c.hidden_dim != wchain::H || c.seq_len != A::S || c.dim != A::D || c.latent_dim != A::Z || c.n_enc != A::NE ||
+      c.n_dec != A::ND)
+    return CVAE_OK;
+  return c.dtype == CVAE_FP8 ? plan_wide_as<wchain::Cfg5F8>(h) : plan_wide_as<A>(h);
 }
 
 // What every training / inference call hands the row chain.
@@ -704,6 +733,12 @@ template <typename T>
 int launch_train_chain(cvae_handle* h, RowArgs ra, hipStream_t s) {
   int rc = tmark(h, s, "rowchain");
   if (rc) return rc;
+  if (std::is_same<T, __bf16>::value && h->ring && fast_ok(h, ra)) {
+    ra.stamps = h->d_stamps;
+    const int grid = rup_i(ra.batch, 32) / wchain::R;
+    return klaunch(h, wchain::widechain_kernel<wchain::Cfg2>, dim3(grid), dim3(wchain::NT), h->ring_lds, s,
+                   h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra);
+  }
   if (std::is_same<T, __bf16>::value && fast_ok(h, ra)) {
     ra.steps = h->d_steps[cvae_handle::ST_TRAIN];
     ra.nsteps = h->n_steps[cvae_handle::ST_TRAIN];
@@ -715,6 +750,9 @@ int launch_train_chain(cvae_handle* h, RowArgs ra, hipStream_t s) {
   if (std::is_same<T, __bf16>::value && wide_ok(h, ra)) {
     ra.stamps = h->d_stamps;
     const int grid = rup_i(ra.batch, 32) / wchain::R;
+    if (h->cfg.dtype == CVAE_FP8)
+      return klaunch(h, wchain::widechain_kernel<wchain::Cfg5F8>, dim3(grid), dim3(wchain::NT), h->wide_lds, s,
+                     h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra);
     return klaunch(h, wchain::widechain_kernel<wchain::Cfg5>, dim3(grid), dim3(wchain::NT), h->wide_lds, s,
                    h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra);
   }
@@ -869,6 +907,7 @@ int cvae_create(const cvae_config* cfg, int device, cvae_handle** out) {
   if (!rc) rc = is16(h) ? set_lds_attrs<__bf16>(h) : set_lds_attrs<float>(h);
   if (!rc) rc = plan_fast(h);
   if (!rc) rc = plan_wide(h);
+  if (!rc) rc = plan_ring(h);
   if (rc) { cvae_destroy(h); return rc; }
   *out = h;
   return CVAE_OK;
@@ -918,7 +957,10 @@ int cvae_workspace_bytes(const cvae_handle* h, int64_t* bytes) {
 
 int cvae_train_kernel(const cvae_handle* h, int* kind) {
   if (!h || !kind) return fail(CVAE_E_INVALID, "null argument");
-  *kind = h->fast_nki > 0 ? CVAE_KERNEL_FAST : h->wide ? CVAE_KERNEL_WIDE : CVAE_KERNEL_GENERIC;
+  *kind = h->ring && !h->fused ? CVAE_KERNEL_RING
+           : h->fast_nki > 0      ? CVAE_KERNEL_FAST
+           : h->wide              ? CVAE_KERNEL_WIDE
+                                  : CVAE_KERNEL_GENERIC;
   return CVAE_OK;
 }
 

@@ -51,38 +51,51 @@ __device__ __forceinline__ void sfor(F&& f) {
   }
 }
 
-template <int S_, int D_, int Z_, int NE_, int ND_>
+// F8_: the CVAE_FP8 form — every forward GEMM whose padded K is a multiple of 64 multiplies e4m3
+// activations by e4m3(s·W) fragments (half the weight stream); backward GEMMs stay bf16.
+template <int S_, int D_, int Z_, int NE_, int ND_, bool F8_ = false>
 struct Arch {
   static constexpr int S = S_, D = D_, Z = Z_, NE = NE_, ND = ND_, I = S_ * D_;
+  static constexpr bool F8 = F8_;
   static constexpr int NKI = (I + 31) / 32, Ip = 32 * NKI;
   static constexpr int NL = 3 + NE + ND, ZH = Z + H;
+  // SZ: a latent of one 16-feature tile of mu ‖ logvar (the reference architecture, latent 8): fc is
+  // one n-tile, split over the waves by K; dz and dh_c of the decoder-L0 backward are not tile-aligned
+  static constexpr bool SZ = 2 * Z == 16;
+  static constexpr int r32(int v) { return (v + 31) / 32 * 32; }
   static constexpr int LC0 = 0, LC1 = 1, LE0 = 2, LFC = 2 + NE, LD0 = 3 + NE, LDL = 2 + NE + ND;
   static constexpr int LE(int i) { return 2 + i; }
   static constexpr int LD(int i) { return 3 + NE + i; }
-  static constexpr int Kp(int l) { return l == LC0 ? 32 : l == LE0 ? Ip : l == LFC ? 2 * H : l == LD0 ? ZH : H; }
-  static constexpr int Np(int l) { return l == LFC ? 2 * Z : l == LDL ? Ip : H; }
+  static constexpr int Kp(int l) { return l == LC0 ? 32 : l == LE0 ? Ip : l == LFC ? 2 * H : l == LD0 ? r32(ZH) : H; }
+  static constexpr int Np(int l) { return l == LFC ? r32(2 * Z) : l == LDL ? Ip : H; }
   // ReLU masks (forward order): C0 C1 E0..E(NE-1) D0..D(ND-2)
   static constexpr int MC0 = 0, MC1 = 1;
   static constexpr int ME(int i) { return 2 + i; }
   static constexpr int MD(int i) { return 2 + NE + i; }
   static constexpr int NMASK = 2 + NE + ND - 1, NMW = (NMASK + 7) / 8;
-  static_assert(Z % 128 == 0, "latent tiles: 8 waves x whole 16-feature tiles of mu and logvar");
+  static_assert(Z % 128 == 0 || SZ, "latent tiles: 8 waves x whole 16-feature tiles of mu and logvar, or one tile");
+  static_assert(!SZ || 2 * H / 32 == NW, "small latent: fc's K chunks split one per wave");
   static_assert(I % 8 == 0 && D >= 3, "x rows load as 16-B vectors; channels 0..2 = t, x, y");
-  // the arena as alloc_arena (cvae_capi.hip) lays it out, bf16 operands: byte offsets from its base
+  // the layers the fp8 form runs in e4m3 (cvae_capi.hip build_plan: padded K % 64 == 0)
+  static constexpr bool f8(int l) { return F8 && Kp(l) % 64 == 0; }
+  // the arena as alloc_arena (cvae_capi.hip) lays it out, bf16 operands: byte offsets from its base;
+  // an e4m3 layer's Wf region starts with its 256-B F8Scale header
   static constexpr int64_t r256(int64_t b) { return (b + 255) / 256 * 256; }
-  static constexpr int64_t wf(int l) {
+  static constexpr int64_t hdr(int l) { return f8(l) ? (int64_t)sizeof(F8Scale) : 0; }
+  static constexpr int64_t region(int l) {
     int64_t o = 0;
-    for (int k = 0; k < l; ++k) o += 2 * r256(2LL * Np(k) * Kp(k));
+    for (int k = 0; k < l; ++k) o += r256(2LL * Np(k) * Kp(k) + hdr(k)) + r256(2LL * Np(k) * Kp(k));
     return o;
   }
-  static constexpr int64_t wb(int l) { return wf(l) + r256(2LL * Np(l) * Kp(l)); }
+  static constexpr int64_t wf(int l) { return region(l) + hdr(l); }
+  static constexpr int64_t wb(int l) { return region(l) + r256(2LL * Np(l) * Kp(l) + hdr(l)); }
   static constexpr int bias_off(int l) {
     int o = 0;
     for (int k = 0; k < l; ++k) o += Np(k);
     return o;
   }
   static constexpr int nbias = bias_off(NL);
-  static constexpr int64_t bias_base = wf(NL);
+  static constexpr int64_t bias_base = region(NL);
   static constexpr int64_t act0 = bias_base + r256(4LL * nbias);
   static constexpr int64_t xrows(int l) {  // xT(l) = act0 + 2·Bp·xrows(l) (Bp % 32 == 0)
     int64_t o = 0;
@@ -94,11 +107,34 @@ struct Arch {
   // pass; dL/d[mu ‖ logvar] (the fc backward's input image) from the decoder-L0 backward on
   static constexpr int L_XIN = 0, L_CIN = L_XIN + Ip * 32, L_CB = L_CIN + 32 * 32, L_A0 = L_CB + H * 32,
                        L_A1 = L_A0 + H * 32, L_U = L_A1 + H * 32;
-  static constexpr int L_HCAT = L_U, L_DCAT = L_HCAT + 2 * H * 32, L_RCH0 = L_DCAT + ZH * 32,
+  static constexpr int L_HCAT = L_U, L_DCAT = L_HCAT + 2 * H * 32, L_RCH0 = L_DCAT + Kp(LD0) * 32,
                        L_GD0 = L_RCH0 + S * R * 4, L_UEND = L_GD0 + S * R * 4, L_GFC = L_U;
-  static_assert(2 * Z * 32 <= L_UEND - L_U, "the fc-backward image fits in the dead forward buffers");
-  static constexpr int L_BIAS = L_UEND, L_PART = L_BIAS + nbias * 4, L_STAMPS = L_PART + NW * 8 * 4,
-                       L_TOTAL = L_STAMPS + (CVAE_DIAG_STAMPS ? 64 * 8 : 0);
+  static_assert(Np(LFC) * 32 <= L_UEND - L_U, "the fc-backward image fits in the dead forward buffers");
+  // SZ only: fc's per-wave partial sums (fp32 [wave][feature][row], in A0 ‖ A1, dead at fc) and the
+  // decoder share of dh_c (fp32 [c][row], behind the fc-backward image in the dead U region)
+  static constexpr int L_PFC = L_A0, L_DHC2 = L_GFC + Np(LFC) * 32;
+  static_assert(!SZ || (NW * 16 * R * 4 <= 2 * H * 32 && L_DHC2 + H * R * 4 <= L_UEND), "SZ buffers");
+  // F8: e4m3 images (fragment order, 16 B per feature, img8) beside the bf16 ones of every input of
+  // an e4m3 GEMM: the condition h (C1's input), the hidden ping-pong pair, the fc input; the
+  // encoder-L1 input (during C0‖E0) and later the decoder input share the recon time channel's
+  // buffers (dead until the last decoder layer)
+  static constexpr int F8B = F8 ? 16 : 0;
+  static constexpr int L_CB8 = L_UEND, L_A08 = L_CB8 + H * F8B, L_A18 = L_A08 + H * F8B,
+                       L_HCAT8 = L_A18 + H * F8B, L_X8 = L_RCH0, L_DCAT8 = L_RCH0;
+  static_assert(!F8 || Kp(LD0) == ZH, "fp8: no decoder-input padding (its e4m3 twin is not zeroed)");
+  static_assert(!F8 || (Ip * 16 <= 2 * S * R * 4 && Kp(LD0) * 16 <= 2 * S * R * 4 && Ip % 64 == 0 &&
+                        Kp(LD0) % 64 == 0),
+                "fp8 images");
+  static constexpr int L_INVS = L_HCAT8 + 2 * H * F8B;  // 1/s of every layer (1 where bf16)
+  // the e4m3 twin of the bf16 image at LDS offset L (compile-time at every use: a pointer-valued
+  // mapping became a lookup table in scratch memory)
+  static constexpr int twin_off(int L) {
+    return L == L_A0 ? L_A08 : L == L_A1 ? L_A18 : L == L_CB ? L_CB8 : L == L_HCAT ? L_HCAT8
+         : L == L_DCAT ? L_DCAT8 : L == L_XIN ? L_X8 : -1;
+  }
+  static constexpr int L_BIAS = L_INVS + (F8 ? 32 * 4 : 0), L_PART = L_BIAS + nbias * 4,
+                       L_STAMPS = L_PART + NW * 8 * 4, L_TOTAL = L_STAMPS + (CVAE_DIAG_STAMPS ? 64 * 8 : 0);
+  static_assert(NL <= 32, "1/s table");
   static_assert(L_TOTAL <= 160 * 1024, "LDS");
 };
 
@@ -108,33 +144,44 @@ struct Arch {
 // GRP > 0: the slots run in TS/GRP groups of GRP (group p = slots p, p + TS/GRP, ..), each group's
 // whole K before the next (its epilogue then overlaps the next group's stream; the X operand, KC
 // chunks, is read once and held); GRP = 0: K-chunk-major over all slots (X streamed).
+// KS = 1: one n-tile whose K chunks are split over the waves (chunk = wave; one item per wave), the
+// partial sums reduced through LDS by the step's epilogue.
+// F8 = 1: an e4m3 forward GEMM — KC counts 64-wide K pairs (one 16-B fragment each).
 struct StepInfo {
-  int layer, bwd, KC, TS, NTL, GRP;
+  int layer, bwd, KC, TS, NTL, GRP, KS, F8;
 };
 
 template <class A>
 struct Plan {
   static constexpr StepInfo step(int s) {
+    StepInfo st = step0(s);
+    if (st.layer >= 0 && !st.bwd && A::f8(st.layer)) {  // e4m3: K pairs
+      st.KC = st.KS ? st.KC : st.KC / 2;
+      st.F8 = 1;
+    }
+    return st;
+  }
+  static constexpr StepInfo step0(int s) {
     int k = 0;
     if (s == k++) return {A::LC0, 0, 1, 1, H / 16};
     if (s == k++) return {A::LE0, 0, A::NKI, 1, H / 16};
     if (s == k++) return {A::LC1, 0, H / 32, 1, H / 16};
     for (int i = 1; i < A::NE; ++i)
       if (s == k++) return {A::LE(i), 0, H / 32, 1, H / 16};
-    if (s == k++) return {A::LFC, 0, 2 * H / 32, A::Z / 64, A::Z / 8, 2};
-    if (s == k++) return {A::LD0, 0, A::ZH / 32, 1, H / 16};
+    if (s == k++) return A::SZ ? StepInfo{A::LFC, 0, 1, 1, 1, 0, 1} : StepInfo{A::LFC, 0, 2 * H / 32, A::Z / 64, A::Z / 8, 2};
+    if (s == k++) return {A::LD0, 0, A::Kp(A::LD0) / 32, 1, H / 16};
     for (int i = 1; i < A::ND - 1; ++i)
       if (s == k++) return {A::LD(i), 0, H / 32, 1, H / 16};
     if (s == k++) return {A::LDL, 0, H / 32, (A::Ip / 16 + NW - 1) / NW, A::Ip / 16, 1};
     if (s == k++) return {A::LDL, 1, A::NKI, 1, H / 16};
     for (int i = A::ND - 2; i >= 1; --i)
       if (s == k++) return {A::LD(i), 1, H / 32, 1, H / 16};
-    if (s == k++) return {A::LD0, 1, H / 32, A::ZH / 128, A::ZH / 16};
-    if (s == k++) return {A::LFC, 1, 2 * A::Z / 32, 2, 2 * H / 16};
+    if (s == k++) return {A::LD0, 1, H / 32, (A::Kp(A::LD0) / 16 + NW - 1) / NW, A::Kp(A::LD0) / 16};
+    if (s == k++) return {A::LFC, 1, A::Np(A::LFC) / 32, 2, 2 * H / 16};
     for (int i = A::NE - 1; i >= 1; --i)
       if (s == k++) return {A::LE(i), 1, H / 32, 1, H / 16};
     if (s == k++) return {A::LC1, 1, H / 32, 1, H / 16};
-    return {-1, 0, 0, 0, 0, 0};
+    return {-1, 0, 0, 0, 0, 0, 0, 0};
   }
   static constexpr int nsteps() {
     int s = 0;
@@ -182,34 +229,74 @@ __device__ __forceinline__ void ring_load(Ring<P>& ring, const char* AR, int wav
     asm volatile("" : "+s"(w));  // recomputed per item: hoisted, ~400 item addresses would be live SGPRs
     int t = w + NW * slot;
     if constexpr (NW * (slot + 1) > st.NTL) t = min(t, st.NTL - 1);
-    ring.r[G % P] = CVAE_DIAG_NOWLOAD ? bf16x8{}
-                                      : gld<bf16x8>(AR + base + (int64_t)(t * st.KC + kc) * 1024 + lane * 16);
+    const int64_t frag = st.KS ? w : t * st.KC + kc;  // KS: tile 0, chunk = wave
+    ring.r[G % P] = CVAE_DIAG_NOWLOAD ? bf16x8{} : gld<bf16x8>(AR + base + frag * 1024 + lane * 16);
   }
 }
 
+// e4m3 activation images (F8): fragment order, 16 B per (64-wide K pair kp, row quad q, row r) —
+// lane (r, q) of an e4m3 X operand reads its two 32-wide chunks of pair kp (frag_k order, as the
+// e4m3 weight fragment, cvae_device.h f8_wf_off) with one ds_read_b128
+typedef long l2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ l2 x8frag(const void* img8, int kp) {
+  const int lane = threadIdx.x & 63;
+  return *(const l2*)((const uint8_t*)img8 + (((kp * 4 + (lane >> 4)) * 16 + (lane & 15)) << 4));
+}
+// rows 4q..4q+3 of feature f: e4m3 of the bf16 activation (the bf16 image holds the same values;
+// RNE, saturated at ±448 as f8x8) — four byte stores
+__device__ __forceinline__ void img8(void* im8, int f, bf16x4 h, int q) {
+  const int kc = f >> 5, kk = f & 31, qx = (kk & 15) >> 2, e = (kk & 3) + ((kk >> 4) << 2);
+  uint8_t* const p = (uint8_t*)im8 + ((((kc >> 1) * 4 + qx) * 16 + 4 * q) << 4) + (kc & 1) * 8 + e;
+  auto c = [](__bf16 x) { return fminf(fmaxf((float)x, -F8_MAX), F8_MAX); };
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(c(h[0]), c(h[1]), 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c(h[2]), c(h[3]), w, true);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) p[16 * i] = (uint8_t)(w >> (8 * i));
+}
+
 // acc[slot] = X·Wᵀ for this wave's n-tiles of step S: X chunk kc read once (two transposed LDS
-// reads), multiplied by every slot's fragment; each consumed ring slot is refilled P items ahead
+// reads; an e4m3 step: one read of the pair's e4m3 image), multiplied by every slot's fragment;
+// each consumed ring slot is refilled P items ahead.  e4m3 steps: acc · sc (= 1/s) at the end.
+template <bool F8>
+using XOp = std::conditional_t<F8, l2, bf16x8>;
+template <bool F8>
+__device__ __forceinline__ XOp<F8> xop(const void* img, int kc) {
+  if constexpr (F8) return x8frag(img, kc);
+  else return xfrag((const __bf16*)img, kc);
+}
+template <bool F8>
+__device__ __forceinline__ f32x4 xmfma(XOp<F8> x, bf16x8 w, f32x4 acc) {
+  if constexpr (F8) {
+    const l2 w8 = __builtin_bit_cast(l2, w);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(x[0], w8[0], acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(x[1], w8[1], acc, 0, 0, 0);
+  } else {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(x, w, acc, 0, 0, 0);
+  }
+}
 struct NoSide {
   template <class C>
   __device__ void operator()(C) const {}
 };
 // side(integral_constant<c>) runs after chunk c: VALU work placed inside a stream-bound GEMM
 template <class A, int P, int S, int TS, class Side = NoSide>
-__device__ __forceinline__ void gemm(Ring<P>& ring, const __bf16* img, f32x4 (&acc)[TS], const char* AR, int wave,
-                                     int lane, Side&& side = Side{}) {
+__device__ __forceinline__ void gemm(Ring<P>& ring, const void* img, f32x4 (&acc)[TS], const char* AR, int wave,
+                                     int lane, Side&& side = Side{}, float sc = 1.f) {
   using PL = Plan<A>;
   constexpr StepInfo st = PL::step(S);
+  constexpr bool F8 = st.F8;
   static_assert(st.TS == TS && st.GRP == 0, "accumulator slots");
   constexpr int G0 = PL::start(S);
   sfor<0, TS>([&](auto t) { acc[decltype(t)::value] = f32x4{0.f, 0.f, 0.f, 0.f}; });
-  bf16x8 xf = xfrag(img, 0);
+  static_assert(!st.KS || (st.KC == 1 && TS == 1 && !F8), "K split: one chunk per wave");
+  XOp<F8> xf = xop<F8>(img, st.KS ? wave : 0);
   sfor<0, st.KC>([&](auto kc) {
     constexpr int c = decltype(kc)::value;
     // the next chunk's X fragment is read one chunk ahead
-    const bf16x8 xn = c + 1 < st.KC ? xfrag(img, c + 1) : xf;
+    const XOp<F8> xn = c + 1 < st.KC ? xop<F8>(img, c + 1) : xf;
     sfor<0, TS>([&](auto t) {
       constexpr int u = decltype(t)::value, g = G0 + c * TS + u;
-      acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf, ring.r[g % P], acc[u], 0, 0, 0);
+      acc[u] = xmfma<F8>(xf, ring.r[g % P], acc[u]);
       // Program order MFMA(g) → refill(g + P): the empty volatile asm on the result is ordered
       // before the (volatile) address step of the refill.  Left alone, the scheduler issues a
       // step's refills first and sinks its MFMA chains, and every ring slot then needs a second
@@ -220,20 +307,22 @@ __device__ __forceinline__ void gemm(Ring<P>& ring, const __bf16* img, f32x4 (&a
     side(kc);
     xf = xn;
   });
+  if constexpr (F8) sfor<0, TS>([&](auto t) { acc[decltype(t)::value] *= sc; });
 }
 
 // The grouped form (StepInfo::GRP > 0): all KC X chunks read first, then per group p its GRP
 // accumulators over the whole K and epi(integral_constant<p>, acc) — the group's epilogue issues
 // while the next group's fragments stream in.
 template <class A, int P, int S, class Epi>
-__device__ __forceinline__ void gemm_grouped(Ring<P>& ring, const __bf16* img, const char* AR, int wave, int lane,
-                                             Epi&& epi) {
+__device__ __forceinline__ void gemm_grouped(Ring<P>& ring, const void* img, const char* AR, int wave, int lane,
+                                             Epi&& epi, float sc = 1.f) {
   using PL = Plan<A>;
   constexpr StepInfo st = PL::step(S);
+  constexpr bool F8 = st.F8;
   static_assert(st.GRP > 0 && st.TS % st.GRP == 0, "grouped step");
   constexpr int G0 = PL::start(S), GS = st.GRP, NGR = st.TS / st.GRP, KC = st.KC;
-  bf16x8 xf[KC];
-  sfor<0, KC>([&](auto kc) { xf[decltype(kc)::value] = xfrag(img, decltype(kc)::value); });
+  XOp<F8> xf[KC];
+  sfor<0, KC>([&](auto kc) { xf[decltype(kc)::value] = xop<F8>(img, decltype(kc)::value); });
   sfor<0, NGR>([&](auto pp) {
     constexpr int p = decltype(pp)::value;
     f32x4 acc[GS];
@@ -242,11 +331,12 @@ __device__ __forceinline__ void gemm_grouped(Ring<P>& ring, const __bf16* img, c
       constexpr int c = decltype(kc)::value;
       sfor<0, GS>([&](auto i) {
         constexpr int u = decltype(i)::value, g = G0 + (p * KC + c) * GS + u;
-        acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[c], ring.r[g % P], acc[u], 0, 0, 0);
+        acc[u] = xmfma<F8>(xf[c], ring.r[g % P], acc[u]);
         asm volatile("" : "+v"(acc[u]));  // MFMA(g) before refill(g + P), as in gemm
         ring_load<A, P, g + P>(ring, AR, wave, lane);
       });
     });
+    if constexpr (F8) sfor<0, GS>([&](auto i) { acc[decltype(i)::value] *= sc; });
     epi(pp, acc);
   });
 }
@@ -315,6 +405,19 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   float* const GD0 = (float*)(smem + A::L_GD0);
   float* const BIAS = (float*)(smem + A::L_BIAS);
   float* const PART = (float*)(smem + A::L_PART);
+  // F8 only: the e4m3 twins of the bf16 images that feed e4m3 GEMMs (A::twin_off), and 1/s per layer
+  uint8_t* const X8 = (uint8_t*)(smem + A::L_X8);
+  float* const INVS = (float*)(smem + A::L_INVS);
+  // the X operand of step S from the bf16 image at LDS offset L: its e4m3 twin for an e4m3 GEMM
+  auto opnd = [smem](auto sI, auto LI) -> const void* {
+    constexpr int L = decltype(LI)::value;
+    if constexpr (PL::step(decltype(sI)::value).F8) return smem + A::twin_off(L);
+    else return smem + L;
+  };
+  auto scl = [INVS](auto sI) -> float {
+    if constexpr (PL::step(decltype(sI)::value).F8) return INVS[PL::step(decltype(sI)::value).layer];
+    else return 1.f;
+  };
   // diagnostic builds only: thread 0's time at every step barrier, kept in LDS, written at the end
   unsigned long long* const STAMPS = (unsigned long long*)(smem + A::L_STAMPS);
   int stamp_i = 0;
@@ -344,6 +447,19 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   auto bias = [&](int l, int f) { return BIAS[A::bias_off(l) + f]; };
   const int n = 16 * wave + n16;  // this lane's feature in the 128-wide layers (n-tile = wave)
   auto img = [&](__bf16* im, int f, bf16x4 v) { *(bf16x4*)(im + ioff(f, q)) = v; };
+  // an image (LDS offset L) that feeds an e4m3 GEMM (F8): the bf16 image (the arena copy) and its
+  // e4m3 twin
+  auto img2 = [smem, q](auto LI, int f, bf16x4 v) {
+    constexpr int L = decltype(LI)::value;
+    *(bf16x4*)((__bf16*)(smem + L) + ioff(f, q)) = v;
+    if constexpr (A::F8) img8(smem + A::twin_off(L), f, v, q);
+  };
+  using std::integral_constant;
+  using IA0 = integral_constant<int, A::L_A0>;
+  using IA1 = integral_constant<int, A::L_A1>;
+  using ICB = integral_constant<int, A::L_CB>;
+  using IHC = integral_constant<int, A::L_HCAT>;
+  using IDC = integral_constant<int, A::L_DCAT>;
 
   // ReLU masks: nibble m of this lane (feature n, rows 4q..4q+3) at bits 4(m % 8) of mk[m / 8]
   uint32_t mk[A::NMW];
@@ -410,14 +526,25 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     f32x4 bv[UB];
 #pragma unroll
     for (int k = 0; k < UB; ++k) bv[k] = gld<f32x4>((const float*)(AR + A::bias_base) + 4 * min(k * NT + tid, NB4 - 1));
+    float invv = 1.f;  // F8: 1/s of layer tid (F8Scale::inv_s in front of its Wf)
+    if constexpr (A::F8) {
+      const int l = min(tid, A::NL - 1);
+      invv = gld<float>((const float*)(AR + (A::f8(l) ? A::wf(l) - (int64_t)sizeof(F8Scale) + 4 : A::bias_base)));
+    }
     // the weight stream queues behind the x tile and the biases (vmcnt retires in order)
     ring_fill<A, P>(ring, AR, wave, lane);
     sub();
     if (tid < 28 * 4) *(uint64_t*)(CIN + (4 + tid / 4) * 16 + 4 * (tid & 3)) = 0ull;
     if (tid < (Ip - I) * 4) *(uint64_t*)(XIN + (I + tid / 4) * 16 + 4 * (tid & 3)) = 0ull;
+    if constexpr (A::Kp(A::LD0) > A::ZH)  // decoder-input K padding (read by D0, copied to xT(D0))
+      if (tid < (A::Kp(A::LD0) - A::ZH) * 4) *(uint64_t*)(DCAT + (A::ZH + tid / 4) * 16 + 4 * (tid & 3)) = 0ull;
 #pragma unroll
     for (int k = 0; k < UB; ++k)
       if (k * NT + tid < NB4) ((f32x4*)BIAS)[k * NT + tid] = bv[k];
+    if constexpr (A::F8) {
+      if (tid < A::NL) INVS[tid] = A::f8(tid) ? invv : 1.f;
+      if (tid < (Ip - I) * 4) img8(X8, I + tid / 4, bf16x4{}, tid & 3);  // e4m3 K padding of x_rel
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int v = u * NT + tid;
@@ -445,6 +572,10 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
         }
         *(bf16x4*)(XIN + ioff(fl, rq)) = to_bf4(rl);
         *(bf16x4*)(XIN + ioff(fh, rq)) = to_bf4(rh);
+        if constexpr (A::F8) {
+          img8(X8, fl, to_bf4(rl), rq);
+          img8(X8, fh, to_bf4(rh), rq);
+        }
         if (c == 0) *(bf16x4*)(CIN + ioff(qd, rq)) = to_bf4(cv);
       }
     }
@@ -466,12 +597,13 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   // is drawn in-kernel — a load under a branch drains the weight stream) or Philox keyed by the
   // global row (data parallelism: eps_row0 = the rank's first row).  The Philox draws (integer
   // multiplies, ~1 us of VALU per wave) run inside the stream-bound encoder-L1 GEMM.
-  constexpr int NZT = Z / 128;
+  // SZ: one tile of latents, held by wave 0's lanes n16 < Z (every wave draws; only wave 0's count)
+  constexpr int NZT = A::SZ ? 1 : Z / 128;
   f32x4 ep[NZT];
   const int rowq = 4 * q + (n16 & 3);  // the row this lane draws (4 latents) before the quad transpose
   auto draw_eps = [&](auto kk) {
     constexpr int k = decltype(kk)::value;
-    const int j0 = 16 * (wave + NW * k) + 4 * (n16 >> 2);
+    const int j0 = A::SZ ? min(4 * (n16 >> 2), Z - 4) : 16 * (wave + NW * k) + 4 * (n16 >> 2);
     const float* const ebase = a.eps ? a.eps : (const float*)(AR + A::bias_base);  // global memory either way
     const int erow = a.eps ? min(b0 + rowq, max(a.batch - 1, 0)) : 0;
     const f32x4 eh = gld<f32x4>(ebase + (a.eps ? (size_t)erow * Z + j0 : 0));
@@ -479,11 +611,12 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     if (rowq >= nrows) e = f32x4{0.f, 0.f, 0.f, 0.f};
     ep[k] = quad_t(e);
   };
+  constexpr int ES = PL::step(PL::sE0).F8 ? 4 : 8;  // encoder-L1 K items between two draws
   auto eps_side = [&](auto cc) {
     constexpr int c = decltype(cc)::value;
-    if constexpr (c % 8 == 2 && c / 8 < NZT) draw_eps(integral_constant<int, c / 8>{});
+    if constexpr (c % ES == 2 && c / ES < NZT) draw_eps(integral_constant<int, c / ES>{});
   };
-  static_assert(8 * (NZT - 1) + 2 < A::NKI, "the eps draws fit in the encoder-L1 GEMM");
+  static_assert(ES * (NZT - 1) + 2 < PL::step(PL::sE0).KC, "the eps draws fit in the encoder-L1 GEMM");
 
   // ================================================================ forward
   {  // C0 ‖ E0
@@ -491,21 +624,23 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     gemm<A, P, 0>(ring, CIN, acc, AR, wave, lane);
     img_copy<32, 0, 1>(CIN, XT(A::LC0), A::Kp(A::LC0), 0, b0);
     img_copy<Ip, 0, 2>(XIN, XT(A::LE0), A::Kp(A::LE0), 0, b0);
-    img(CB, n, relu(acc[0], bias(A::LC0, n), integral_constant<int, A::MC0>{}));
+    img2(ICB{}, n, relu(acc[0], bias(A::LC0, n), integral_constant<int, A::MC0>{}));
     sub();
-    gemm<A, P, PL::sE0>(ring, XIN, acc, AR, wave, lane, eps_side);
+    constexpr integral_constant<int, PL::sE0> sE0{};
+    gemm<A, P, PL::sE0>(ring, opnd(sE0, integral_constant<int, A::L_XIN>{}), acc, AR, wave, lane, eps_side, scl(sE0));
     sub();
-    img(A0, n, relu(acc[0], bias(A::LE0, n), integral_constant<int, A::ME(0)>{}));
+    img2(IA0{}, n, relu(acc[0], bias(A::LE0, n), integral_constant<int, A::ME(0)>{}));
   }
   bar();
   {  // C1 ‖ E1: h_c goes to both concatenations (fc input at H+n, decoder input at Z+n)
     f32x4 acc[1];
-    gemm<A, P, PL::sC1>(ring, CB, acc, AR, wave, lane);
+    constexpr integral_constant<int, PL::sC1> sC1{};
+    gemm<A, P, PL::sC1>(ring, opnd(sC1, ICB{}), acc, AR, wave, lane, NoSide{}, scl(sC1));
     img_copy<H, 0, 1, 2 * H>(CB, XT(A::LC1), H, 0, b0);
     img_copy<Ip, 2, 3>(XIN, XT(A::LE0), A::Kp(A::LE0), 0, b0);
     const bf16x4 hc = relu(acc[0], bias(A::LC1, n), integral_constant<int, A::MC1>{});
-    img(HCAT, H + n, hc);
-    img(DCAT, Z + n, hc);
+    img2(IHC{}, H + n, hc);
+    img2(IDC{}, Z + n, hc);
   }
   // encoder layers 1 .. NE-1 (input image: E(i-1)'s output, A0 for odd i); the last → h_traj
   sfor<1, NE>([&](auto ii) {
@@ -513,17 +648,48 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     if constexpr (i > 1) bar();
     __bf16* const in = (i & 1) ? A0 : A1;
     f32x4 acc[1];
-    gemm<A, P, PL::sC1 + i>(ring, in, acc, AR, wave, lane);
+    constexpr integral_constant<int, PL::sC1 + i> sI{};
+    using IIN = std::conditional_t<(i & 1), IA0, IA1>;
+    using IOUT = std::conditional_t<i == NE - 1, IHC, std::conditional_t<(i & 1), IA1, IA0>>;
+    gemm<A, P, PL::sC1 + i>(ring, opnd(sI, IIN{}), acc, AR, wave, lane, NoSide{}, scl(sI));
     img_copy<H, 0, 1>(in, XT(A::LE(i)), H, 0, b0);
     if constexpr (i >= 2 && i <= 3) img_copy<Ip, i + 1, i + 2>(XIN, XT(A::LE0), A::Kp(A::LE0), 0, b0);
     const bf16x4 he = relu(acc[0], bias(A::LE(i), n), integral_constant<int, A::ME(i)>{});
-    img(i == NE - 1 ? HCAT : (i & 1) ? A1 : A0, n, he);
+    img2(IOUT{}, n, he);
   });
   bar();
   // fc_mu ‖ fc_logvar (:195-196) + reparameterize (:199-206) + KL terms (:243): group k = the mu
   // tile wave + 8k and the logvar tile Z/16 + wave + 8k of the same latents
   f32x4 mu[NZT], lv[NZT];
-  gemm_grouped<A, P, PL::sFC>(ring, HCAT, AR, wave, lane, [&](auto kk, f32x4(&acc)[2]) {
+  if constexpr (A::SZ) {  // one n-tile, K split over the waves; the partial sums meet in LDS
+    float* const PFC = (float*)(smem + A::L_PFC);
+    f32x4 acc[1];
+    gemm<A, P, PL::sFC>(ring, HCAT, acc, AR, wave, lane);
+    img_copy<2 * H, 0, 1>(HCAT, XT(A::LFC), A::Kp(A::LFC), 0, b0);
+    *(f32x4*)(PFC + (wave * 16 + n16) * R + 4 * q) = acc[0];
+    bar();
+    if (wave == 0 && n16 < Z) {  // latent j = n16: mu at feature j, logvar at Z + j
+      const int j = n16;
+      f32x4 sm = {0.f, 0.f, 0.f, 0.f}, sl = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {  // fixed order: deterministic
+        sm += *(const f32x4*)(PFC + (w * 16 + j) * R + 4 * q);
+        sl += *(const f32x4*)(PFC + (w * 16 + Z + j) * R + 4 * q);
+      }
+      const float bm = bias(A::LFC, j), bl = bias(A::LFC, Z + j);
+      f32x4 z;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        mu[0][i] = sm[i] + bm;
+        lv[0][i] = sl[i] + bl;
+        const float sd = __expf(0.5f * lv[0][i]);
+        z[i] = mu[0][i] + ep[0][i] * sd;
+        if (4 * q + i < nrows) s_kl += 1.f + lv[0][i] - mu[0][i] * mu[0][i] - __expf(lv[0][i]);
+      }
+      img(DCAT, j, to_bf4(z));
+    }
+  } else
+  gemm_grouped<A, P, PL::sFC>(ring, opnd(integral_constant<int, PL::sFC>{}, IHC{}), AR, wave, lane, [&](auto kk, f32x4(&acc)[2]) {
     constexpr int k = decltype(kk)::value;
     if constexpr (k == 0) img_copy<2 * H, 0, 1>(HCAT, XT(A::LFC), A::Kp(A::LFC), 0, b0);
     const int j = 16 * (wave + NW * k) + n16;
@@ -537,14 +703,15 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
       z[i] = mu[k][i] + ep[k][i] * sd;
       if (4 * q + i < nrows) s_kl += 1.f + lv[k][i] - mu[k][i] * mu[k][i] - __expf(lv[k][i]);
     }
-    img(DCAT, j, to_bf4(z));
-  });
+    img2(IDC{}, j, to_bf4(z));
+  }, scl(integral_constant<int, PL::sFC>{}));
   bar();
   {  // D0 → A0
     f32x4 acc[1];
-    gemm<A, P, PL::sD0>(ring, DCAT, acc, AR, wave, lane);
+    constexpr integral_constant<int, PL::sD0> sD0{};
+    gemm<A, P, PL::sD0>(ring, opnd(sD0, IDC{}), acc, AR, wave, lane, NoSide{}, scl(sD0));
     img_copy<A::ZH, 0, 3>(DCAT, XT(A::LD0), A::Kp(A::LD0), 0, b0);
-    img(A0, n, relu(acc[0], bias(A::LD0, n), integral_constant<int, A::MD(0)>{}));
+    img2(IA0{}, n, relu(acc[0], bias(A::LD0, n), integral_constant<int, A::MD(0)>{}));
   }
   // decoder layers 1 .. ND-2 (input: D(i-1)'s output, A0 for odd i)
   sfor<1, ND - 1>([&](auto ii) {
@@ -552,9 +719,12 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     bar();
     __bf16* const in = (i & 1) ? A0 : A1;
     f32x4 acc[1];
-    gemm<A, P, PL::sD0 + i>(ring, in, acc, AR, wave, lane);
+    constexpr integral_constant<int, PL::sD0 + i> sI{};
+    using IIN = std::conditional_t<(i & 1), IA0, IA1>;
+    using IOUT = std::conditional_t<(i & 1), IA1, IA0>;
+    gemm<A, P, PL::sD0 + i>(ring, opnd(sI, IIN{}), acc, AR, wave, lane, NoSide{}, scl(sI));
     img_copy<H, 0, 1>(in, XT(A::LD(i)), H, 0, b0);
-    img((i & 1) ? A1 : A0, n, relu(acc[0], bias(A::LD(i), n), integral_constant<int, A::MD(i)>{}));
+    img2(IOUT{}, n, relu(acc[0], bias(A::LD(i), n), integral_constant<int, A::MD(i)>{}));
   });
   bar();
   __bf16* const DLIN = ((ND - 2) & 1) ? A1 : A0;  // input image of the last decoder layer
@@ -564,7 +734,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     typedef float f32x2 __attribute__((ext_vector_type(2)));
     const float cr = a.w_recon * 2.f;
     f32x2 sr2 = {0.f, 0.f};
-    gemm_grouped<A, P, PL::sDL>(ring, DLIN, AR, wave, lane, [&](auto gg, f32x4(&accs)[1]) {
+    gemm_grouped<A, P, PL::sDL>(ring, opnd(integral_constant<int, PL::sDL>{}, std::conditional_t<((ND - 2) & 1), IA1, IA0>{}), AR, wave, lane, [&](auto gg, f32x4(&accs)[1]) {
       constexpr int g = decltype(gg)::value;
       if constexpr (g == 0) img_copy<H, 0, 1>(DLIN, XT(A::LDL), H, 0, b0);
       if (!(NW * (g + 1) <= NG3 || wave + NW * g < NG3)) return;  // wave-uniform: tile past the output
@@ -610,7 +780,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
         }
       }
       *(bf16x4*)(XIN + ioff(f, q)) = to_bf4(gi);  // pad features f >= I: 0
-    });
+    }, scl(integral_constant<int, PL::sDL>{}));
     s_recon += sr2[0] + sr2[1];
   }
   bar();
@@ -665,7 +835,35 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   // D0ᵀ: [dz ‖ dh_c(decoder share)]; dz → KL/reparameterisation backward → dL/d[mu ‖ logvar]
   __bf16* const D0IN = ((ND - 2) & 1) ? A1 : A0;  // gT(D0) image
   f32x4 dhc2;
-  {
+  float* const DHC2 = (float*)(smem + A::L_DHC2);  // SZ only
+  if constexpr (A::SZ) {  // tiles wave, wave + 8: features f < Z are dz, Z <= f < Z + H dh_c (to LDS)
+    constexpr int TS = PL::step(PL::sD0b).TS, NTL = PL::step(PL::sD0b).NTL;
+    f32x4 acc[TS];
+    gemm<A, P, PL::sD0b>(ring, D0IN, acc, AR, wave, lane);
+    img_copy<H, 0, 1>(D0IN, GT(A::LD0), H, 0, b0);
+    sfor<0, TS>([&](auto ss) {
+      constexpr int s = decltype(ss)::value;
+      const int t = wave + NW * s, f = 16 * t + n16;
+      if (NW * (s + 1) > NTL && t >= NTL) return;  // wave-uniform: a reloaded tile
+      if (f < Z) {
+        const int j = f;
+        f32x4 gm, gl;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bool live = 4 * q + i < nrows;
+          const float sd = __expf(0.5f * lv[0][i]);
+          gm[i] = live ? a.w_kld * mu[0][i] * inv_BZ + acc[s][i] : 0.f;
+          gl[i] = live ? a.w_kld * 0.5f * (__expf(lv[0][i]) - 1.f) * inv_BZ + acc[s][i] * ep[0][i] * 0.5f * sd : 0.f;
+        }
+        img(GFC, j, to_bf4(gm));
+        img(GFC, Z + j, to_bf4(gl));
+      } else if (f < A::ZH) {
+        *(f32x4*)(DHC2 + (f - Z) * R + 4 * q) = acc[s];
+      }
+    });
+    // the fc-backward image's K padding (the region held the forward fc input until now)
+    if (tid < (A::Np(A::LFC) - 2 * Z) * 4) *(uint64_t*)(GFC + (2 * Z + tid / 4) * 16 + 4 * (tid & 3)) = 0ull;
+  } else {
     f32x4 acc[NZT + 1];
     gemm<A, P, PL::sD0b>(ring, D0IN, acc, AR, wave, lane);
     img_copy<H, 0, 1>(D0IN, GT(A::LD0), H, 0, b0);
@@ -690,7 +888,8 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     f32x4 acc[2];
     gemm<A, P, PL::sFCb>(ring, GFC, acc, AR, wave, lane);
     sub();
-    img_copy<2 * Z, 0, (4 * Z + NT - 1) / NT>(GFC, GT(A::LFC), A::Np(A::LFC), 0, b0);
+    img_copy<A::Np(A::LFC), 0, (2 * A::Np(A::LFC) + NT - 1) / NT>(GFC, GT(A::LFC), A::Np(A::LFC), 0, b0);
+    if constexpr (A::SZ) dhc2 = *(const f32x4*)(DHC2 + n * R + 4 * q);
     img(A0, n, masked(acc[0], integral_constant<int, A::ME(NE - 1)>{}));
     img(CB, n, masked(acc[1] + dhc2, integral_constant<int, A::MC1>{}));
   }
@@ -748,10 +947,17 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
 
 // BASELINE cfg5: S=200, D=6, latent 512, 8 + 8 layers (hidden 128)
 using Cfg5 = Arch<200, 6, 512, 8, 8>;
+// BASELINE cfg2 / the reference architecture: S=100, D=6, latent 8, 4 + 4 layers
+using Cfg2 = Arch<100, 6, 8, 4, 4>;
+// BASELINE cfg5 in the CVAE_FP8 form (e4m3 forward GEMMs)
+using Cfg5F8 = Arch<200, 6, 512, 8, 8, true>;
 #ifndef CVAE_WIDE_RING
 #define CVAE_WIDE_RING 12
 #endif
 constexpr int RING = CVAE_WIDE_RING;
+#ifndef CVAE_RING_P
+#define CVAE_RING_P 12
+#endif
 
 template <class A>
 __global__ __launch_bounds__(NT) void widechain_kernel(char* arena, const void* x, const int64_t* idx, int Bp,
@@ -761,7 +967,7 @@ __global__ __launch_bounds__(NT) void widechain_kernel(char* arena, const void* 
   ra.x = x;
   ra.idx = idx;
   ra.batch = batch;
-  wide_body<A, RING>(arena, Bp, ra, smem, blockIdx.x);
+  wide_body<A, A::SZ ? CVAE_RING_P : RING>(arena, Bp, ra, smem, blockIdx.x);
 }
 
 }  // namespace wchain

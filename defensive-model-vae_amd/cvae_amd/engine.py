@@ -472,11 +472,12 @@ class CVAEEngine:
 
     @property
     def train_kernel(self):
-        """'generic', 'fast' (reference architecture, bf16) or 'wide' (BASELINE cfg5 shape, bf16):
+        """'generic', 'fast' / 'ring' (reference architecture, bf16; 'ring' = the single weight-stream
+        chain, S=100 D=6) or 'wide' (BASELINE cfg5 shape, bf16):
         the training row chain this engine runs (cvae_train_kernel)."""
         k = C.c_int()
         check(lib().cvae_train_kernel(self._h, C.byref(k)))
-        return ("generic", "fast", "wide")[k.value]
+        return ("generic", "fast", "wide", "ring")[k.value]
 
     def workspace_bytes(self):
         b = C.c_int64()

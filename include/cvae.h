@@ -135,9 +135,13 @@ int cvae_bucket_split(const cvae_handle* h, int64_t* split);
 /* Which training row chain this handle runs for the usual call (16-B aligned operand-dtype x, no
  * external gradients): CVAE_KERNEL_GENERIC (the step interpreter, any shape), CVAE_KERNEL_FAST
  * (bf16, the reference architecture: hidden 128, latent 8, 4+4 layers, seq_len*dim 600) or
- * CVAE_KERNEL_WIDE (bf16, BASELINE cfg5's shape: seq_len 200, dim 6, latent 512, 8+8 layers).
+ * CVAE_KERNEL_WIDE (bf16, BASELINE cfg5's shape: seq_len 200, dim 6, latent 512, 8+8 layers) or
+ * CVAE_KERNEL_RING (the fast configuration at seq_len 100, dim 6 on the single-ring weight-stream
+ * chain, opt-in: CVAE_RING=1 at creation).
  * Introspection only (no reference counterpart); CVAE_GENERIC=1 at creation forces the generic. */
-enum cvae_train_kernel_kind { CVAE_KERNEL_GENERIC = 0, CVAE_KERNEL_FAST = 1, CVAE_KERNEL_WIDE = 2 };
+enum cvae_train_kernel_kind {
+  CVAE_KERNEL_GENERIC = 0, CVAE_KERNEL_FAST = 1, CVAE_KERNEL_WIDE = 2, CVAE_KERNEL_RING = 3
+};
 int cvae_train_kernel(const cvae_handle* h, int* kind);
 
 /* Rebuild the device copies of the weights (padded operand-dtype W and Wᵀ,

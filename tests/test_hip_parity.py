@@ -392,7 +392,10 @@ def test_fused_step_equals_two_launch_step(cvae, monkeypatch):
     torch.manual_seed(0)
     ref = OracleCVAE(S, D, 8)
     monkeypatch.delenv("CVAE_FUSE", raising=False)
+    monkeypatch.setenv("CVAE_RING", "0")  # the fused launch runs fastchain's body: compare with it
     m1, e1 = _model(cvae, S, D, 8, sd=ref.state_dict(), dtype="bf16", max_batch=200)
+    monkeypatch.delenv("CVAE_RING")
+    assert e1.train_kernel == "fast"
     monkeypatch.setenv("CVAE_FUSE", "1")
     m2, e2 = _model(cvae, S, D, 8, sd=ref.state_dict(), dtype="bf16", max_batch=200)
     monkeypatch.delenv("CVAE_FUSE")
@@ -439,6 +442,82 @@ def test_fast_and_generic_kernels_agree(cvae, monkeypatch):
     np.testing.assert_allclose(lf.cpu().numpy(), lg.cpu().numpy(), rtol=2e-3, atol=1e-6)
     dp = (ef.params - eg.params).norm() / (ef.params - torch.cat([p.detach().flatten() for p in ref.parameters()]).cuda()).norm()
     assert float(dp) < 2e-2, float(dp)  # relative to the 3-step update
+
+
+def _ring_pair(cvae, monkeypatch, B, seed=0):
+    """Two bf16 engines of the reference architecture (S=100, D=6) on the same weights: the
+    single-ring chain (CVAE_RING=1 at creation, cvae_widechain.h small-latent form) and
+    fastchain_kernel (the default)."""
+    torch.manual_seed(seed)
+    ref = OracleCVAE(100, 6, 8)
+    monkeypatch.delenv("CVAE_GENERIC", raising=False)
+    monkeypatch.setenv("CVAE_RING", "1")
+    m1, e1 = _model(cvae, 100, 6, 8, sd=ref.state_dict(), dtype="bf16", max_batch=max(B, 32))
+    monkeypatch.delenv("CVAE_RING")
+    m2, e2 = _model(cvae, 100, 6, 8, sd=ref.state_dict(), dtype="bf16", max_batch=max(B, 32))
+    assert e1.train_kernel == "ring" and e2.train_kernel == "fast"
+    return ref, m1, e1, m2, e2
+
+
+@pytest.mark.parametrize("B", [37, 200, 1024])
+def test_ring_chain_matches_fast_and_emulation(cvae, monkeypatch, B):
+    """The ring chain (one weight stream per wave across every step; fc split over the waves by K)
+    against fastchain_kernel (same rounding points; fp32 summation order of fc aside) and against
+    the CPU emulation of those rounding points: ragged last tile (B=37), a gathered batch (B=200
+    rows of 300 by index), the benchmark batch (B=1024)."""
+    ref, m1, e1, m2, e2 = _ring_pair(cvae, monkeypatch, B)
+    pool = torch.randn(max(B, 300), 100, 6, generator=torch.Generator().manual_seed(B)).to(torch.bfloat16)
+    idx = torch.randperm(pool.shape[0], generator=torch.Generator().manual_seed(3))[:B]
+    eps = torch.randn(B, 8, generator=torch.Generator().manual_seed(4321))
+    l1 = e1.forward_backward(pool.cuda(), idx=idx.cuda(), eps=eps).cpu().numpy()
+    l2 = e2.forward_backward(pool.cuda(), idx=idx.cuda(), eps=eps).cpu().numpy()
+    np.testing.assert_allclose(l1, l2, rtol=1e-3, atol=1e-6)
+    g1, g2 = _grads(m1, e1), _grads(m2, e2)
+    for k in g1:
+        assert rel_l2(g1[k], g2[k]) < 1e-2, (k, rel_l2(g1[k], g2[k]))
+    x = pool[idx].float()
+    p = {k: v.numpy() for k, v in ref.state_dict().items()}
+    r, mu, lv, hc, c = cvae_np.forward(p, x.numpy(), eps.numpy(), q=cvae_np.bf16)
+    np.testing.assert_allclose(l1, cvae_np.losses(r, c["rel"], mu, lv), rtol=2e-3, atol=1e-6)
+    ge = cvae_np.backward(p, c, r, mu, lv)
+    for k in cvae_np.param_keys():
+        assert rel_l2(g1[k], ge[k]) < 2e-2, (k, rel_l2(g1[k], ge[k]))
+
+
+def test_ring_chain_philox_training_and_determinism(cvae, monkeypatch):
+    """In-kernel Philox eps keyed by the global row: the ring chain draws fastchain's noise (same
+    losses up to summation order); five training steps (device counters, dW ⊕ Adam behind each
+    chain) stay within the bf16 summation-order distance of the fastchain run; a second ring
+    engine replays the first bit for bit; the DP split path (row chain + dW without Adam, then
+    Adam) equals the fused ring step bit for bit."""
+    B = 160
+    ref, m1, e1, m2, e2 = _ring_pair(cvae, monkeypatch, B)
+    xd = torch.randn(B, 100, 6, generator=torch.Generator().manual_seed(5)).to("cuda", torch.bfloat16)
+    l1 = e1.forward_backward(xd, row0=320).cpu().numpy()
+    l2 = e2.forward_backward(xd, row0=320).cpu().numpy()
+    np.testing.assert_allclose(l1, l2, rtol=1e-3, atol=1e-6)
+    p0 = e1.params.clone()
+    for _ in range(5):
+        e1.train_step(xd)
+        e2.train_step(xd)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(e1.loss.cpu().numpy(), e2.loss.cpu().numpy(), rtol=3e-3, atol=1e-6)
+    dp = (e1.params - e2.params).norm() / (e1.params - p0).norm()
+    assert float(dp) < 2e-2, float(dp)
+    monkeypatch.setenv("CVAE_RING", "1")
+    m3, e3 = _model(cvae, 100, 6, 8, sd=ref.state_dict(), dtype="bf16", max_batch=B)
+    m4, e4 = _model(cvae, 100, 6, 8, sd=ref.state_dict(), dtype="bf16", max_batch=B)
+    monkeypatch.delenv("CVAE_RING")
+    assert e3.train_kernel == "ring" and e4.train_kernel == "ring"
+    e3.forward_backward(xd, row0=320)
+    e4.forward_backward(xd, row0=320)
+    for _ in range(5):
+        e3.train_step(xd)
+        e4.forward_backward(xd)
+        e4.adam_step(1.0)
+    torch.cuda.synchronize()
+    assert torch.equal(e3.params, e1.params) and torch.equal(e3.loss, e1.loss)
+    assert torch.equal(e3.params, e4.params) and torch.equal(e3.m, e4.m) and torch.equal(e3.v, e4.v)
 
 
 def test_misaligned_input_runs_generic_chain(cvae):
@@ -705,6 +784,44 @@ def test_fp8_matches_fp8_emulation(cvae, shape):
     dev = np.abs(loss - want32) / np.abs(want32)
     print(f"fp8 {shape}: loss rel deviation from the fp32 reference {dev}")
     assert (dev < 0.25).all(), dev
+
+
+@pytest.mark.parametrize("B", [37, 200])
+def test_wide_fp8_chain_matches_generic_fp8(cvae, monkeypatch, B):
+    """The cfg5 fp8 form of the wide chain (e4m3 activation twins written by the producing
+    epilogues, e4m3 weight pairs in the ring) against the generic interpreter's fp8 path
+    (CVAE_GENERIC=1) — the same rounding points, fp32 summation order aside — and against the CPU
+    emulation (emulation tolerances of test_fp8_matches_fp8_emulation); ragged tile (B=37) and a
+    gathered batch (B=200)."""
+    ref, m, eng, x, eps = _wide(cvae, "fp8", B)
+    monkeypatch.setenv("CVAE_GENERIC", "1")
+    m2 = cvae.ConditionalTrajectoryVAE(WIDE["S"], WIDE["D"], WIDE["Z"], 128, WIDE["n_enc"], WIDE["n_dec"])
+    m2.load_state_dict(ref.state_dict())
+    e2 = m2.attach(dtype="fp8", max_batch=max(B, 32), device="cuda:0")
+    monkeypatch.delenv("CVAE_GENERIC")
+    assert eng.train_kernel == "wide" and e2.train_kernel == "generic"
+    x = x.to(torch.bfloat16).float()
+    if B == 200:
+        pool = torch.randn(300, WIDE["S"], WIDE["D"], generator=torch.Generator().manual_seed(9)).to(torch.bfloat16)
+        idx = torch.randperm(300, generator=torch.Generator().manual_seed(3))[:B]
+        x = pool[idx].float()
+        lw = eng.forward_backward(pool.cuda(), idx=idx.cuda(), eps=eps).cpu().numpy()
+    else:
+        lw = eng.forward_backward(x, eps=eps).cpu().numpy()
+    lg = e2.forward_backward(x, eps=eps).cpu().numpy()
+    np.testing.assert_allclose(lw, lg, rtol=5e-3, atol=1e-6)
+    gw, gg = _grads(m, eng), _grads(m2, e2)
+    errs = {k: rel_l2(gw[k], gg[k]) for k in gw}
+    assert max(errs.values()) < 1e-1 and np.median(list(errs.values())) < 2e-2, errs
+    p = {k: v.numpy() for k, v in ref.state_dict().items()}
+    ne, nd = WIDE["n_enc"], WIDE["n_dec"]
+    f8 = cvae_np.fp8_layers(p, WIDE["S"], WIDE["D"], WIDE["Z"], 128, ne, nd)
+    r, mu, lv, hc, cc = cvae_np.forward(p, x.numpy(), eps.numpy(), n_enc=ne, n_dec=nd, q=cvae_np.bf16, f8=f8)
+    np.testing.assert_allclose(lw, cvae_np.losses(r, cc["rel"], mu, lv), rtol=5e-3, atol=1e-6)
+    ge = cvae_np.backward(p, cc, r, mu, lv, n_enc=ne, n_dec=nd)
+    errs = {k: rel_l2(gw[k], ge[k]) for k in cvae_np.param_keys(ne, nd)}
+    print(f"wide fp8 chain B={B}: grad rel-L2 vs emulation", {k: round(v, 4) for k, v in errs.items()})
+    assert max(errs.values()) < 1e-1 and np.median(list(errs.values())) < 2e-2, errs
 
 
 def test_fp8_training_full_batch_cfg5(cvae):
