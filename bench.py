@@ -72,6 +72,27 @@ def bytes_per_traj(S, D, Z, H, tsize, C=2, n_enc=4, n_dec=4):
 ADAM_BYTES_PER_PARAM = 28  # p, m, v read + write (24 B) + bf16/fp32 operand copies W, Wᵀ written
 
 
+def weight_stream_bytes(S, D, Z, H, dtype, C=2, n_enc=4, n_dec=4):
+    """Weight-fragment bytes ONE row-chain workgroup streams per launch: every
+    layer's padded forward operand Wf (e4m3 where CVAE_FP8 runs the layer in fp8: padded K % 64 ==
+    0) plus the padded Wᵀ of every layer whose dX the chain computes (all but the condition and
+    encoder input layers).  Every workgroup streams all of it; the chain's floor is this over the
+    per-CU L2 -> CU rate."""
+    r32 = lambda v: (v + 31) // 32 * 32  # noqa: E731
+    I = S * D
+    ks = [C, H, I] + [H] * (n_enc - 1) + [2 * H, Z + H] + [H] * (n_dec - 1)
+    ns = [H, H, H] + [H] * (n_enc - 1) + [2 * Z] + [H] * (n_dec - 1) + [I]
+    t = 4 if dtype == "fp32" else 2
+    fwd = sum(r32(n) * r32(k) * (1 if dtype == "fp8" and r32(k) % 64 == 0 else t) for k, n in zip(ks, ns))
+    bwd = sum(r32(n) * r32(k) * t for i, (k, n) in enumerate(zip(ks, ns)) if i not in (0, 2))
+    return fwd + bwd
+
+
+# highest per-CU weight-stream rate measured in a row-chain step (wide chain, fc backward: 512 KB
+# per workgroup in 4.7-4.8 us; profiles/r02k_wide_stamps.txt) — an empirical ceiling, not a spec
+CU_STREAM_MAX_GBS = 109.0
+
+
 def roofline(kernel, avg_ms, flop, nbytes, dtype, traffic=None):
     """Both ceilings of one kernel; the binding one (longer time at peak) becomes the headline."""
     t = avg_ms * 1e-3
@@ -320,6 +341,14 @@ def main():
         std = (S, D, Z, H, NE, ND) == (100, 6, 8, 128, 4, 4)
         traffic = measured_traffic(args.traffic_file, dom, B, dtype) if std else None
         roof = roofline(dom, kt[dom][0], flop[dom], nbytes[dom], dtype, traffic)
+        if "rowchain" in kt and wl != "cfg1":
+            wsb = weight_stream_bytes(S, D, Z, H, dtype, n_enc=NE, n_dec=ND)
+            ach = wsb / (kt["rowchain"][0] * 1e-3) / 1e9
+            roof["weight_stream"] = {"kernel": "rowchain", "bytes_per_workgroup": wsb,
+                                     "achieved_GBps_per_CU": round(ach, 1),
+                                     "measured_max_GBps_per_CU": CU_STREAM_MAX_GBS,
+                                     "frac": round(ach / CU_STREAM_MAX_GBS, 4),
+                                     "active_CUs": (rows_launch + 15) // 16}
         roof["kernels_ms"] = {k: round(v[0], 5) for k, v in kt.items()}
         if b2b:
             roof["kernels_back_to_back_ms"] = {k: round(v, 5) for k, v in b2b.items()}

@@ -116,12 +116,11 @@ struct Arch {
   static_assert(!SZ || (NW * 16 * R * 4 <= 2 * H * 32 && L_DHC2 + H * R * 4 <= L_UEND), "SZ buffers");
   // F8: e4m3 images (fragment order, 16 B per feature, img8) beside the bf16 ones of every input of
   // an e4m3 GEMM: the condition h (C1's input), the hidden ping-pong pair, the fc input; the
-  // encoder-L1 input (during C0‖E0) and later the decoder input share the recon time channel's
-  // buffers (dead until the last decoder layer)
+  // encoder-L1 input (converted after C0, read by E0) and later the decoder input share the recon
+  // time channel's buffers (dead until the last decoder layer)
   static constexpr int F8B = F8 ? 16 : 0;
   static constexpr int L_CB8 = L_UEND, L_A08 = L_CB8 + H * F8B, L_A18 = L_A08 + H * F8B,
                        L_HCAT8 = L_A18 + H * F8B, L_X8 = L_RCH0, L_DCAT8 = L_RCH0;
-  static_assert(!F8 || Kp(LD0) == ZH, "fp8: no decoder-input padding (its e4m3 twin is not zeroed)");
   static_assert(!F8 || (Ip * 16 <= 2 * S * R * 4 && Kp(LD0) * 16 <= 2 * S * R * 4 && Ip % 64 == 0 &&
                         Kp(LD0) % 64 == 0),
                 "fp8 images");
@@ -242,16 +241,18 @@ __device__ __forceinline__ l2 x8frag(const void* img8, int kp) {
   const int lane = threadIdx.x & 63;
   return *(const l2*)((const uint8_t*)img8 + (((kp * 4 + (lane >> 4)) * 16 + (lane & 15)) << 4));
 }
-// rows 4q..4q+3 of feature f: e4m3 of the bf16 activation (the bf16 image holds the same values;
-// RNE, saturated at ±448 as f8x8) — four byte stores
+// rows 4q..4q+3 of feature f (f & 3 == lane & 3: a quad of lanes holds 4 consecutive features):
+// e4m3 of the bf16 activation (RNE, saturated at ±448 as f8x8).  The quad's 4 x 4 block is
+// transposed (quad_t) so lane b writes row 4q + b's 4 features as one dword; byte stores of single
+// features were 16-way bank conflicts (the x_rel image cost 3.8 us of prologue that way).
 __device__ __forceinline__ void img8(void* im8, int f, bf16x4 h, int q) {
-  const int kc = f >> 5, kk = f & 31, qx = (kk & 15) >> 2, e = (kk & 3) + ((kk >> 4) << 2);
-  uint8_t* const p = (uint8_t*)im8 + ((((kc >> 1) * 4 + qx) * 16 + 4 * q) << 4) + (kc & 1) * 8 + e;
-  auto c = [](__bf16 x) { return fminf(fmaxf((float)x, -F8_MAX), F8_MAX); };
-  int w = __builtin_amdgcn_cvt_pk_fp8_f32(c(h[0]), c(h[1]), 0, false);
-  w = __builtin_amdgcn_cvt_pk_fp8_f32(c(h[2]), c(h[3]), w, true);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) p[16 * i] = (uint8_t)(w >> (8 * i));
+  const int b = threadIdx.x & 3, f0 = f - b;
+  const int kc = f0 >> 5, kk = f0 & 31, qx = (kk & 15) >> 2, e0 = (kk >> 4) << 2;
+  const f32x4 t = quad_t(from_bf4(h));  // features f0..f0+3 of row 4q + b
+  auto c = [](float x) { return fminf(fmaxf(x, -F8_MAX), F8_MAX); };
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(c(t[0]), c(t[1]), 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c(t[2]), c(t[3]), w, true);
+  *(int*)((uint8_t*)im8 + ((((kc >> 1) * 4 + qx) * 16 + 4 * q + b) << 4) + (kc & 1) * 8 + e0) = w;
 }
 
 // acc[slot] = X·Wᵀ for this wave's n-tiles of step S: X chunk kc read once (two transposed LDS
@@ -406,7 +407,6 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   float* const BIAS = (float*)(smem + A::L_BIAS);
   float* const PART = (float*)(smem + A::L_PART);
   // F8 only: the e4m3 twins of the bf16 images that feed e4m3 GEMMs (A::twin_off), and 1/s per layer
-  uint8_t* const X8 = (uint8_t*)(smem + A::L_X8);
   float* const INVS = (float*)(smem + A::L_INVS);
   // the X operand of step S from the bf16 image at LDS offset L: its e4m3 twin for an e4m3 GEMM
   auto opnd = [smem](auto sI, auto LI) -> const void* {
@@ -527,9 +527,13 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
 #pragma unroll
     for (int k = 0; k < UB; ++k) bv[k] = gld<f32x4>((const float*)(AR + A::bias_base) + 4 * min(k * NT + tid, NB4 - 1));
     float invv = 1.f;  // F8: 1/s of layer tid (F8Scale::inv_s in front of its Wf)
-    if constexpr (A::F8) {
-      const int l = min(tid, A::NL - 1);
-      invv = gld<float>((const float*)(AR + (A::f8(l) ? A::wf(l) - (int64_t)sizeof(F8Scale) + 4 : A::bias_base)));
+    if constexpr (A::F8) {  // offsets selected from compile-time constants (a runtime A::wf(tid) is a loop)
+      int64_t o = A::bias_base;
+      sfor<0, A::NL>([&](auto ll) {
+        constexpr int l = decltype(ll)::value;
+        if constexpr (A::f8(l)) o = tid == l ? A::wf(l) - (int64_t)sizeof(F8Scale) + 4 : o;
+      });
+      invv = gld<float>((const float*)(AR + o));
     }
     // the weight stream queues behind the x tile and the biases (vmcnt retires in order)
     ring_fill<A, P>(ring, AR, wave, lane);
@@ -542,8 +546,9 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     for (int k = 0; k < UB; ++k)
       if (k * NT + tid < NB4) ((f32x4*)BIAS)[k * NT + tid] = bv[k];
     if constexpr (A::F8) {
-      if (tid < A::NL) INVS[tid] = A::f8(tid) ? invv : 1.f;
-      if (tid < (Ip - I) * 4) img8(X8, I + tid / 4, bf16x4{}, tid & 3);  // e4m3 K padding of x_rel
+      bool f8l = false;
+      sfor<0, A::NL>([&](auto ll) { f8l = f8l || (A::f8(decltype(ll)::value) && tid == decltype(ll)::value); });
+      if (tid < A::NL) INVS[tid] = f8l ? invv : 1.f;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -572,10 +577,6 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
         }
         *(bf16x4*)(XIN + ioff(fl, rq)) = to_bf4(rl);
         *(bf16x4*)(XIN + ioff(fh, rq)) = to_bf4(rh);
-        if constexpr (A::F8) {
-          img8(X8, fl, to_bf4(rl), rq);
-          img8(X8, fh, to_bf4(rh), rq);
-        }
         if (c == 0) *(bf16x4*)(CIN + ioff(qd, rq)) = to_bf4(cv);
       }
     }
@@ -625,6 +626,18 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     img_copy<32, 0, 1>(CIN, XT(A::LC0), A::Kp(A::LC0), 0, b0);
     img_copy<Ip, 0, 2>(XIN, XT(A::LE0), A::Kp(A::LE0), 0, b0);
     img2(ICB{}, n, relu(acc[0], bias(A::LC0, n), integral_constant<int, A::MC0>{}));
+    if constexpr (A::F8) {
+      // the e4m3 twin of x_rel, one 64-wide K pair per wave at a time: lane (r, q) converts its own
+      // MFMA fragment (two transposed bf16 reads, f8x8) — each pair once, not once per wave (as an
+      // on-the-fly conversion inside the E0 GEMM: +2.6 us), and off the prologue (the unrolled
+      // prologue form cost it 2 us); one extra barrier
+      uint8_t* const X8 = (uint8_t*)(smem + A::L_X8);
+#pragma nounroll
+      for (int kp = wave; kp < A::NKI / 2; kp += NW)
+        *(l2*)(X8 + (((kp * 4 + (lane >> 4)) * 16 + (lane & 15)) << 4)) =
+            l2{f8x8(xfrag(XIN, 2 * kp)), f8x8(xfrag(XIN, 2 * kp + 1))};
+      lbar();
+    }
     sub();
     constexpr integral_constant<int, PL::sE0> sE0{};
     gemm<A, P, PL::sE0>(ring, opnd(sE0, integral_constant<int, A::L_XIN>{}), acc, AR, wave, lane, eps_side, scl(sE0));
