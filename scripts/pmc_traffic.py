@@ -15,7 +15,7 @@ from collections import defaultdict
 
 
 def short(name):
-    if "rowchain_kernel" in name or "fastchain_kernel" in name:
+    if "rowchain_kernel" in name or "fastchain_kernel" in name or "widechain_kernel" in name:
         return "rowchain"
     if "fused_step_kernel" in name:
         return "fused_step"
