@@ -59,6 +59,11 @@ struct cvae_handle {
   // the two dW buckets (CVAE_PART_DW_DEC / CVAE_PART_DW_REST): tiles of the decoder layers and of the rest
   std::vector<TileDesc> tiles_part[2];
   TileDesc* d_tiles_part[2] = {nullptr, nullptr};
+  // the generic dW kernel's tile list for a whole step: tiles, or (a long 16-bit list) with 32 × 64
+  // tiles where a layer's K pairs up (wtiles_ni2)
+  std::vector<TileDesc> wtiles;
+  TileDesc* d_wtiles = nullptr;
+  bool wtiles_ni2 = false;
   int64_t bucket_split = 0;   // flat index of decoder.0.weight
   // split-K of the dW launch for large batches (cvae_wgrad.h SplitK): partial workspace + tickets
   int splitk_max = 1;
@@ -221,6 +226,27 @@ int build_plan(cvae_handle* h) {
     return out;
   };
   h->tiles = xcd_order(seq);
+  // more 32 × 32 tiles than workgroup slots (2 dW workgroups per CU, 256 CUs): the generic dW
+  // launch takes 32 × 64 tiles where the layer's padded K is a multiple of 64 — fewer workgroups,
+  // and each G row is read by half as many tiles (BASELINE cfg5: 868 → 442 tiles)
+  h->wtiles = h->tiles;
+  h->wtiles_ni2 = false;
+  if (c.dtype != CVAE_F32 && seq.size() > 512) {
+    std::vector<TileDesc> wseq;
+    for (int l = 0; l < n.n_layers; ++l) {
+      const LayerDev& L = n.L[l];
+      const int ni = (L.Kp % 64 == 0 && !L.wt) ? 2 : 1;
+      if (L.Kp > L.Np) {
+        for (int i = 0; i < L.Kp; i += 32 * ni)
+          for (int o = 0; o < L.Np; o += 32) wseq.push_back({l, o, i, ni});
+      } else {
+        for (int o = 0; o < L.Np; o += 32)
+          for (int i = 0; i < L.Kp; i += 32 * ni) wseq.push_back({l, o, i, ni});
+      }
+      h->wtiles_ni2 = h->wtiles_ni2 || ni == 2;
+    }
+    h->wtiles = xcd_order(wseq);
+  }
   std::vector<TileDesc> dec, rest;
   for (const TileDesc& t : seq) (t.layer >= lD(n, 0) ? dec : rest).push_back(t);
   h->tiles_part[0] = xcd_order(dec);
@@ -372,9 +398,13 @@ int alloc_arena(cvae_handle* h) {
   // split-K for batches of >= 8192 rows: up to 16 splits of >= 2048 rows (cvae_wgrad.h SplitK)
   h->splitk_max = std::max(1, std::min(16, rup_i(h->cfg.max_batch, 32) / 2048));
   if (rup_i(h->cfg.max_batch, 32) < 8192) h->splitk_max = 1;
-  const int64_t skw_off = h->splitk_max > 1 ? take((int64_t)h->tiles.size() * h->splitk_max * (32 * 32 + 32) * 4) : 0;
-  const int64_t skt_off = h->splitk_max > 1 ? take((int64_t)h->tiles.size() * 4) : 0;
+  // split-K partials: [tile][split][pw] for either tile list (pw = 32·TW + 32 of its widest tile)
+  const int64_t skw_floats = std::max((int64_t)h->tiles.size() * (32 * 32 + 32),
+                                      (int64_t)h->wtiles.size() * (h->wtiles_ni2 ? 32 * 64 + 32 : 32 * 32 + 32));
+  const int64_t skw_off = h->splitk_max > 1 ? take(skw_floats * h->splitk_max * 4) : 0;
+  const int64_t skt_off = h->splitk_max > 1 ? take((int64_t)std::max(h->tiles.size(), h->wtiles.size()) * 4) : 0;
   const int64_t tile_off = take((int64_t)h->tiles.size() * sizeof(TileDesc));
+  const int64_t wtile_off = take((int64_t)h->wtiles.size() * sizeof(TileDesc));
   const int64_t tp_off0 = take((int64_t)h->tiles_part[0].size() * sizeof(TileDesc));
   const int64_t tp_off1 = take((int64_t)h->tiles_part[1].size() * sizeof(TileDesc));
   int64_t step_off[cvae_handle::ST_N];
@@ -400,6 +430,8 @@ int alloc_arena(cvae_handle* h) {
   }
   h->d_tiles = (TileDesc*)(h->arena + tile_off);
   HIPCK(hipMemcpy(h->d_tiles, h->tiles.data(), h->tiles.size() * sizeof(TileDesc), hipMemcpyHostToDevice));
+  h->d_wtiles = (TileDesc*)(h->arena + wtile_off);
+  HIPCK(hipMemcpy(h->d_wtiles, h->wtiles.data(), h->wtiles.size() * sizeof(TileDesc), hipMemcpyHostToDevice));
   const int64_t tp_off[2] = {tp_off0, tp_off1};
   for (int k = 0; k < 2; ++k) {
     h->d_tiles_part[k] = (TileDesc*)(h->arena + tp_off[k]);
@@ -797,16 +829,21 @@ int launch_wgrad(cvae_handle* h, int batch, const AdamArgs& aa, const LossArgs& 
     return klaunch(h, wgrad_kernel<float, MODE>, dim3(nt * sk.S), dim3(WG_THREADS), 0, s, h->net,
                    (const TileDesc*)h->d_tiles_part[k], bk_of(h, batch), aa, la, sk);
   }
-  const int nt = (int)h->tiles.size();
+  const int nt = (int)h->wtiles.size();
   if (h->fast_nki == 19)
     return klaunch(h, fchain::fastwgrad_kernel<19, MODE>, dim3(fchain::Tiles<19>::total() * sk.S + 1),
                    dim3(WG_THREADS), 0, s, h->arena, aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), h->net.S,
                    h->net.D, h->net.I, aa, la, sk);
+  if (is16(h) && h->wtiles_ni2) {
+    sk.pw = 32 * 64 + 32;
+    return klaunch(h, wgrad_kernel<__bf16, MODE, true>, dim3(nt * sk.S), dim3(WG_THREADS), 0, s, h->net,
+                   (const TileDesc*)h->d_wtiles, bk_of(h, batch), aa, la, sk);
+  }
   if (is16(h))
     return klaunch(h, wgrad_kernel<__bf16, MODE>, dim3(nt * sk.S), dim3(WG_THREADS), 0, s, h->net,
-                   (const TileDesc*)h->d_tiles, bk_of(h, batch), aa, la, sk);
+                   (const TileDesc*)h->d_wtiles, bk_of(h, batch), aa, la, sk);
   return klaunch(h, wgrad_kernel<float, MODE>, dim3(nt * sk.S), dim3(WG_THREADS), 0, s, h->net,
-                 (const TileDesc*)h->d_tiles, bk_of(h, batch), aa, la, sk);
+                 (const TileDesc*)h->d_wtiles, bk_of(h, batch), aa, la, sk);
 }
 
 // device counters, fused launch: its chain blocks do not bump the step (its dW tiles read it in the

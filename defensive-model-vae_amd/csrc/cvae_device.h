@@ -66,7 +66,8 @@ __host__ __device__ inline int lD(const NetDev& n, int i) { return 3 + n.n_enc +
 // parameter tensor, so the reference's 24 keys and init order come first)
 __host__ __device__ inline int lCE(const NetDev& n) { return 3 + n.n_enc + n.n_dec; }
 
-struct TileDesc { int layer, o0, i0, pad_; };
+// ni: input tiles per workgroup of the generic dW kernel (0/1: 32 × 32, 2: 32 × 64; wgrad_kernel)
+struct TileDesc { int layer, o0, i0, ni; };
 
 // element (feature f, batch row b) of an arena matrix with Kf feature rows
 __host__ __device__ inline size_t aoff(int f, int b, int Kf) {

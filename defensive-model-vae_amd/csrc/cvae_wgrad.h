@@ -362,9 +362,10 @@ struct WgradLds {
 // reads with sc1 loads after a workgroup barrier).  S = 1: the whole batch in one block.
 struct SplitK {
   int S, s;
-  float* ws;          // [tile][S][32·TW + 32] fp32 partials (dW then db)
+  float* ws;          // [tile][S][pw] fp32 partials (dW then db)
   unsigned* tickets;  // [tile], zero between launches
   int tile;
+  int pw;             // floats per partial (0: 32·TW + 32 of the tile)
 };
 
 // One workgroup = tile td of layer L: 32 outputs × 32·NI inputs (NI = 2: two 32-wide input tiles
@@ -411,7 +412,9 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
   const int nk_all = Bk / KC, per = (nk_all + sk.S - 1) / sk.S;
   const int c0 = sk.s * per, nk = max(0, min(per, nk_all - c0));
   const int nmine = nk > wave ? (nk - wave + WG_NW - 1) / WG_NW : 0;
-  constexpr int PF = 4;
+  // chunks in flight per wave: 4; 2 for 32 × 64 tiles, whose 6 operand vectors per chunk would
+  // otherwise take the kernel past 128 VGPRs (one workgroup per CU instead of two)
+  constexpr int PF = NI == 2 ? 2 : 4;
   V ga[PF][2], xb[PF][NX];
   __amdgpu_buffer_rsrc_t rg, rx;
   if (SC1) {
@@ -496,7 +499,7 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
     for (int w = 0; w < WG_NW; ++w) db += dbp[w * 32 + tid];
   }
   if (sk.S > 1) {  // split-K: publish this split's partial; the last of the S blocks finishes the tile
-    constexpr int PW = 32 * TW + 32;
+    const int PW = sk.pw ? sk.pw : 32 * TW + 32;
     static_assert(EPT == 2 || EPT == 4, "partial vectors of 8 or 16 B");
     float* mine = sk.ws + ((size_t)sk.tile * sk.S + sk.s) * PW;
     if (tid < 32 * TPR) {
@@ -551,14 +554,25 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
 
 // generic configurations: tile descriptors and layer records from memory
 // grid = ntiles × sk.S (split-major: split s owns blocks [s·ntiles, (s+1)·ntiles))
-template <typename T, int MODE>
-__global__ __launch_bounds__(WG_THREADS) void wgrad_kernel(NetDev net, const TileDesc* __restrict__ tiles,
+// NI2: the tile list holds 32 × 64 tiles (TileDesc::ni == 2) beside 32 × 32 ones — a large tile
+// list (BASELINE cfg5: 868 tiles of 32 × 32 for 512 workgroup slots) then needs fewer workgroups
+// and re-reads fewer arena rows (a tile reads 32 G rows + 32·ni X rows of the whole batch)
+// (launch bounds: 4 waves per SIMD = two workgroups per CU)
+template <typename T, int MODE, bool NI2 = false>
+__global__ __launch_bounds__(WG_THREADS, 4) void wgrad_kernel(NetDev net, const TileDesc* __restrict__ tiles,
                                                            int Bk, AdamArgs aa, LossArgs la, SplitK sk) {
-  __shared__ __attribute__((aligned(16))) WgradLds<1> sh;
+  __shared__ __attribute__((aligned(16))) WgradLds<NI2 ? 2 : 1> sh;
   const int ntiles = gridDim.x / sk.S;
   sk.s = blockIdx.x / ntiles;
   sk.tile = blockIdx.x - sk.s * ntiles;
   const TileDesc td = tiles[sk.tile];
+  if constexpr (NI2) {
+    if (td.ni == 2) {  // block-uniform
+      wgrad_body<T, MODE, false, 2>(net.L[td.layer], td, Bk, aa, la, blockIdx.x == 0, net.S, net.D, net.Z, sh.red,
+                                    sh.dbp, sk);
+      return;
+    }
+  }
   wgrad_body<T, MODE>(net.L[td.layer], td, Bk, aa, la, blockIdx.x == 0, net.S, net.D, net.Z, sh.red, sh.dbp, sk);
 }
 
