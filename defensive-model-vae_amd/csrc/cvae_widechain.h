@@ -275,6 +275,20 @@ __device__ __forceinline__ f32x4 xmfma(XOp<F8> x, bf16x8 w, f32x4 acc) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(x, w, acc, 0, 0, 0);
   }
 }
+// Two consecutive e4m3 K pairs in one block-scaled MFMA (16x16x128, unit E8M0 scales: 2x the
+// rate of the non-scaled fp8 form, which runs at the bf16 rate on gfx950).  A lane's 32 bytes
+// are its 16-B fragments of pairs kp and kp + 1, for A (activations) and B (weights) alike;
+// scripts/ubench/mxcheck.hip checks this equals four v_mfma_f32_16x16x32_fp8_fp8 on the GPU.
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+template <class X>  // X = l2 (an e4m3 pair); the bf16 instantiation of the callers never reaches it
+__device__ __forceinline__ f32x4 mx2(X x0, X x1, bf16x8 w0, bf16x8 w1, f32x4 acc) {
+  static_assert(std::is_same<X, l2>::value, "e4m3 pairs only");
+  const l2 w0l = __builtin_bit_cast(l2, w0), w1l = __builtin_bit_cast(l2, w1);
+  typedef long l4 __attribute__((ext_vector_type(4)));
+  const i32x8 a = __builtin_bit_cast(i32x8, l4{x0[0], x0[1], x1[0], x1[1]});
+  const i32x8 b = __builtin_bit_cast(i32x8, l4{w0l[0], w0l[1], w1l[0], w1l[1]});
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, acc, 0, 0, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
+}
 struct NoSide {
   template <class C>
   __device__ void operator()(C) const {}
@@ -291,11 +305,22 @@ __device__ __forceinline__ void gemm(Ring<P>& ring, const void* img, f32x4 (&acc
   sfor<0, TS>([&](auto t) { acc[decltype(t)::value] = f32x4{0.f, 0.f, 0.f, 0.f}; });
   static_assert(!st.KS || (st.KC == 1 && TS == 1 && !F8), "K split: one chunk per wave");
   XOp<F8> xf = xop<F8>(img, st.KS ? wave : 0);
+  XOp<F8> xe = xf;  // F8: the even pair, multiplied together with the odd one after it
   sfor<0, st.KC>([&](auto kc) {
     constexpr int c = decltype(kc)::value;
     // the next chunk's X fragment is read one chunk ahead
     const XOp<F8> xn = c + 1 < st.KC ? xop<F8>(img, c + 1) : xf;
-    sfor<0, TS>([&](auto t) {
+    if constexpr (F8 && c % 2 == 0 && c + 1 < st.KC) {
+      xe = xf;  // its MFMA (and refill) comes with pair c + 1
+    } else if constexpr (F8 && c % 2 == 1) {
+      sfor<0, TS>([&](auto t) {
+        constexpr int u = decltype(t)::value, g0 = G0 + (c - 1) * TS + u, g = G0 + c * TS + u;
+        acc[u] = mx2(xe, xf, ring.r[g0 % P], ring.r[g % P], acc[u]);
+        asm volatile("" : "+v"(acc[u]));  // MFMA before the refills, as below
+        ring_load<A, P, g0 + P>(ring, AR, wave, lane);
+        ring_load<A, P, g + P>(ring, AR, wave, lane);
+      });
+    } else sfor<0, TS>([&](auto t) {
       constexpr int u = decltype(t)::value, g = G0 + c * TS + u;
       acc[u] = xmfma<F8>(xf, ring.r[g % P], acc[u]);
       // Program order MFMA(g) → refill(g + P): the empty volatile asm on the result is ordered
@@ -330,6 +355,17 @@ __device__ __forceinline__ void gemm_grouped(Ring<P>& ring, const void* img, con
     sfor<0, GS>([&](auto i) { acc[decltype(i)::value] = f32x4{0.f, 0.f, 0.f, 0.f}; });
     sfor<0, KC>([&](auto kc) {
       constexpr int c = decltype(kc)::value;
+      if constexpr (F8 && c % 2 == 0 && c + 1 < KC) return;  // with pair c + 1 (mx2)
+      if constexpr (F8 && c % 2 == 1) {
+        sfor<0, GS>([&](auto i) {
+          constexpr int u = decltype(i)::value, g0 = G0 + (p * KC + c - 1) * GS + u, g = G0 + (p * KC + c) * GS + u;
+          acc[u] = mx2(xf[c - 1], xf[c], ring.r[g0 % P], ring.r[g % P], acc[u]);
+          asm volatile("" : "+v"(acc[u]));
+          ring_load<A, P, g0 + P>(ring, AR, wave, lane);
+          ring_load<A, P, g + P>(ring, AR, wave, lane);
+        });
+        return;
+      }
       sfor<0, GS>([&](auto i) {
         constexpr int u = decltype(i)::value, g = G0 + (p * KC + c) * GS + u;
         acc[u] = xmfma<F8>(xf[c], ring.r[g % P], acc[u]);
