@@ -231,7 +231,8 @@ int build_plan(cvae_handle* h) {
   // and each G row is read by half as many tiles (BASELINE cfg5: 868 → 442 tiles)
   h->wtiles = h->tiles;
   h->wtiles_ni2 = false;
-  if (c.dtype != CVAE_F32 && seq.size() > 512) {
+  const char* ni2_env = std::getenv("CVAE_DW_NI2");  // "0": 32 × 32 tiles only (A/B)
+  if (c.dtype != CVAE_F32 && seq.size() > 512 && !(ni2_env && ni2_env[0] == '0')) {
     std::vector<TileDesc> wseq;
     for (int l = 0; l < n.n_layers; ++l) {
       const LayerDev& L = n.L[l];
@@ -684,7 +685,7 @@ int plan_ring(cvae_handle* h) {
   h->ring = false;
   const char* env = std::getenv("CVAE_RING");
   if (!(env && env[0] == '1') || h->fast_nki != 19 || c.seq_len != A::S || c.dim != A::D) return CVAE_OK;
-  if (!wide_layout_matches<A>(h)) return CVAE_OK;
+  if (!wide_layout_matches<A>(h) || h->arena_bytes >= ((int64_t)1 << 31)) return CVAE_OK;
   HIPCK(hipFuncSetAttribute((const void*)wchain::widechain_kernel<A>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             A::L_TOTAL));
   h->ring = true;
@@ -694,7 +695,8 @@ int plan_ring(cvae_handle* h) {
 
 template <class A>
 int plan_wide_as(cvae_handle* h) {
-  if (!wide_layout_matches<A>(h)) return CVAE_OK;
+  // the wide chain stores to the arena through a buffer resource of 2^31 - 1 bytes
+  if (!wide_layout_matches<A>(h) || h->arena_bytes >= ((int64_t)1 << 31)) return CVAE_OK;
   HIPCK(hipFuncSetAttribute((const void*)wchain::widechain_kernel<A>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             A::L_TOTAL));
   h->wide = true;

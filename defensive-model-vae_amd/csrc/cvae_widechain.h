@@ -393,12 +393,20 @@ __device__ __forceinline__ void ring_fill(Ring<P>& ring, const char* AR, int wav
 #ifndef CVAE_WIDE_SC1
 #define CVAE_WIDE_SC1 1
 #endif
-__device__ __forceinline__ void st16(void* p, u32x4 v) {
+// The arena as a buffer resource: the 16-B stores are buffer_store_dwordx4 with the sc1 cache
+// policy (aux 16 on gfx950) through the builtin, so the compiler sees their operands.  (They were
+// an inline-asm global_store: with a one-lane f64 block added to the prologue, the stores of a
+// few lanes then wrote stale data — the hazard recognizer cannot see into inline asm.)
+struct ArenaDst {
+  __amdgpu_buffer_rsrc_t rs;
+  const char* base;
+};
+__device__ __forceinline__ ArenaDst arena_dst(const char* AR) {
+  return ArenaDst{__builtin_amdgcn_make_buffer_rsrc((void*)AR, (short)0, 0x7fffffff, 0x00020000), AR};
+}
+__device__ __forceinline__ void st16(const ArenaDst& d, const void* p, u32x4 v) {
   if (CVAE_DIAG_NOSTORE) return;
-  if (CVAE_WIDE_SC1)
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-  else
-    gst<u32x4>(p, v);
+  __builtin_amdgcn_raw_buffer_store_b128(v, d.rs, (int)((const char*)p - d.base), 0, CVAE_WIDE_SC1 ? 16 : 0);
 }
 
 // rounds [R0, R1) of the 16-B copy of features [0, NF) of an LDS image (ioff layout) to the arena
@@ -407,7 +415,7 @@ __device__ __forceinline__ void st16(void* p, u32x4 v) {
 // quads are the slot pair 2(h ^ (x >> 1)), +1, in swapped order when x is odd.
 // Threads T0.. take the tasks (T0 = 256: a 128-feature image on waves 4-7, beside another on 0-3).
 template <int NF, int R0, int R1, int T0 = 0>
-__device__ __forceinline__ void img_copy(const __bf16* img, void* mat, int Kf, int goff, int b0) {
+__device__ __forceinline__ void img_copy(const __bf16* img, const ArenaDst& dst, void* mat, int Kf, int goff, int b0) {
 #pragma unroll
   for (int r = R0; r < R1; ++r) {
     if (r * NT - T0 >= 2 * NF) break;
@@ -418,7 +426,7 @@ __device__ __forceinline__ void img_copy(const __bf16* img, void* mat, int Kf, i
       const int f = k >> 1, h = k & 1, x = (f >> 2) & 3;
       u32x4 v = *(const u32x4*)(img + f * 16 + 8 * (h ^ (x >> 1)));
       if (x & 1) v = u32x4{v[2], v[3], v[0], v[1]};
-      st16((__bf16*)mat + aoff(goff + f, b0 + 8 * h, Kf), v);
+      st16(dst, (__bf16*)mat + aoff(goff + f, b0 + 8 * h, Kf), v);
     }
   }
 }
@@ -481,6 +489,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     return (void*)(AR + A::act0 + 2 * (int64_t)bp * A::grows(l));
   };
   auto bias = [&](int l, int f) { return BIAS[A::bias_off(l) + f]; };
+  const ArenaDst dst = arena_dst(AR);
   const int n = 16 * wave + n16;  // this lane's feature in the 128-wide layers (n-tile = wave)
   auto img = [&](__bf16* im, int f, bf16x4 v) { *(bf16x4*)(im + ioff(f, q)) = v; };
   // an image (LDS offset L) that feeds an e4m3 GEMM (F8): the bf16 image (the arena copy) and its
@@ -659,8 +668,8 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   {  // C0 ‖ E0
     f32x4 acc[1];
     gemm<A, P, 0>(ring, CIN, acc, AR, wave, lane);
-    img_copy<32, 0, 1>(CIN, XT(A::LC0), A::Kp(A::LC0), 0, b0);
-    img_copy<Ip, 0, 2>(XIN, XT(A::LE0), A::Kp(A::LE0), 0, b0);
+    img_copy<32, 0, 1>(CIN, dst, XT(A::LC0), A::Kp(A::LC0), 0, b0);
+    img_copy<Ip, 0, 2>(XIN, dst, XT(A::LE0), A::Kp(A::LE0), 0, b0);
     img2(ICB{}, n, relu(acc[0], bias(A::LC0, n), integral_constant<int, A::MC0>{}));
     if constexpr (A::F8) {
       // the e4m3 twin of x_rel, one 64-wide K pair per wave at a time: lane (r, q) converts its own
@@ -685,8 +694,8 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     f32x4 acc[1];
     constexpr integral_constant<int, PL::sC1> sC1{};
     gemm<A, P, PL::sC1>(ring, opnd(sC1, ICB{}), acc, AR, wave, lane, NoSide{}, scl(sC1));
-    img_copy<H, 0, 1, 2 * H>(CB, XT(A::LC1), H, 0, b0);
-    img_copy<Ip, 2, 3>(XIN, XT(A::LE0), A::Kp(A::LE0), 0, b0);
+    img_copy<H, 0, 1, 2 * H>(CB, dst, XT(A::LC1), H, 0, b0);
+    img_copy<Ip, 2, 3>(XIN, dst, XT(A::LE0), A::Kp(A::LE0), 0, b0);
     const bf16x4 hc = relu(acc[0], bias(A::LC1, n), integral_constant<int, A::MC1>{});
     img2(IHC{}, H + n, hc);
     img2(IDC{}, Z + n, hc);
@@ -701,8 +710,8 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     using IIN = std::conditional_t<(i & 1), IA0, IA1>;
     using IOUT = std::conditional_t<i == NE - 1, IHC, std::conditional_t<(i & 1), IA1, IA0>>;
     gemm<A, P, PL::sC1 + i>(ring, opnd(sI, IIN{}), acc, AR, wave, lane, NoSide{}, scl(sI));
-    img_copy<H, 0, 1>(in, XT(A::LE(i)), H, 0, b0);
-    if constexpr (i >= 2 && i <= 3) img_copy<Ip, i + 1, i + 2>(XIN, XT(A::LE0), A::Kp(A::LE0), 0, b0);
+    img_copy<H, 0, 1>(in, dst, XT(A::LE(i)), H, 0, b0);
+    if constexpr (i >= 2 && i <= 3) img_copy<Ip, i + 1, i + 2>(XIN, dst, XT(A::LE0), A::Kp(A::LE0), 0, b0);
     const bf16x4 he = relu(acc[0], bias(A::LE(i), n), integral_constant<int, A::ME(i)>{});
     img2(IOUT{}, n, he);
   });
@@ -714,7 +723,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     float* const PFC = (float*)(smem + A::L_PFC);
     f32x4 acc[1];
     gemm<A, P, PL::sFC>(ring, HCAT, acc, AR, wave, lane);
-    img_copy<2 * H, 0, 1>(HCAT, XT(A::LFC), A::Kp(A::LFC), 0, b0);
+    img_copy<2 * H, 0, 1>(HCAT, dst, XT(A::LFC), A::Kp(A::LFC), 0, b0);
     *(f32x4*)(PFC + (wave * 16 + n16) * R + 4 * q) = acc[0];
     bar();
     if (wave == 0 && n16 < Z) {  // latent j = n16: mu at feature j, logvar at Z + j
@@ -740,7 +749,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   } else
   gemm_grouped<A, P, PL::sFC>(ring, opnd(integral_constant<int, PL::sFC>{}, IHC{}), AR, wave, lane, [&](auto kk, f32x4(&acc)[2]) {
     constexpr int k = decltype(kk)::value;
-    if constexpr (k == 0) img_copy<2 * H, 0, 1>(HCAT, XT(A::LFC), A::Kp(A::LFC), 0, b0);
+    if constexpr (k == 0) img_copy<2 * H, 0, 1>(HCAT, dst, XT(A::LFC), A::Kp(A::LFC), 0, b0);
     const int j = 16 * (wave + NW * k) + n16;
     const float bm = bias(A::LFC, j), bl = bias(A::LFC, Z + j);
     f32x4 z;
@@ -759,7 +768,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     f32x4 acc[1];
     constexpr integral_constant<int, PL::sD0> sD0{};
     gemm<A, P, PL::sD0>(ring, opnd(sD0, IDC{}), acc, AR, wave, lane, NoSide{}, scl(sD0));
-    img_copy<A::ZH, 0, 3>(DCAT, XT(A::LD0), A::Kp(A::LD0), 0, b0);
+    img_copy<A::ZH, 0, 3>(DCAT, dst, XT(A::LD0), A::Kp(A::LD0), 0, b0);
     img2(IA0{}, n, relu(acc[0], bias(A::LD0, n), integral_constant<int, A::MD(0)>{}));
   }
   // decoder layers 1 .. ND-2 (input: D(i-1)'s output, A0 for odd i)
@@ -772,7 +781,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     using IIN = std::conditional_t<(i & 1), IA0, IA1>;
     using IOUT = std::conditional_t<(i & 1), IA1, IA0>;
     gemm<A, P, PL::sD0 + i>(ring, opnd(sI, IIN{}), acc, AR, wave, lane, NoSide{}, scl(sI));
-    img_copy<H, 0, 1>(in, XT(A::LD(i)), H, 0, b0);
+    img_copy<H, 0, 1>(in, dst, XT(A::LD(i)), H, 0, b0);
     img2(IOUT{}, n, relu(acc[0], bias(A::LD(i), n), integral_constant<int, A::MD(i)>{}));
   });
   bar();
@@ -785,7 +794,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     f32x2 sr2 = {0.f, 0.f};
     gemm_grouped<A, P, PL::sDL>(ring, opnd(integral_constant<int, PL::sDL>{}, std::conditional_t<((ND - 2) & 1), IA1, IA0>{}), AR, wave, lane, [&](auto gg, f32x4(&accs)[1]) {
       constexpr int g = decltype(gg)::value;
-      if constexpr (g == 0) img_copy<H, 0, 1>(DLIN, XT(A::LDL), H, 0, b0);
+      if constexpr (g == 0) img_copy<H, 0, 1>(DLIN, dst, XT(A::LDL), H, 0, b0);
       if (!(NW * (g + 1) <= NG3 || wave + NW * g < NG3)) return;  // wave-uniform: tile past the output
       const int t = wave + NW * g;
       const f32x4 acc = accs[0];
@@ -866,7 +875,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   {  // last decoder layer ᵀ: dL/d h_D(ND-2) = GL · W_DL, ReLU mask of D(ND-2) → A0
     f32x4 acc[1];
     gemm<A, P, PL::sDLb>(ring, XIN, acc, AR, wave, lane);
-    img_copy<Ip, 0, 1>(XIN, GT(A::LDL), A::Np(A::LDL), 0, b0);
+    img_copy<Ip, 0, 1>(XIN, dst, GT(A::LDL), A::Np(A::LDL), 0, b0);
     img(A0, n, masked(acc[0], integral_constant<int, A::MD(ND - 2)>{}));
   }
   // D(i)ᵀ for i = ND-2 .. 1: input = dL/d(pre-activation of D(i)) = gT(D(i)), mask of D(i-1)
@@ -876,8 +885,8 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     __bf16* const in = (k & 1) ? A0 : A1;
     f32x4 acc[1];
     gemm<A, P, PL::sDLb + k>(ring, in, acc, AR, wave, lane);
-    img_copy<H, 0, 1>(in, GT(A::LD(i)), H, 0, b0);
-    if constexpr (k < XR) img_copy<Ip, k, k + 1>(XIN, GT(A::LDL), A::Np(A::LDL), 0, b0);
+    img_copy<H, 0, 1>(in, dst, GT(A::LD(i)), H, 0, b0);
+    if constexpr (k < XR) img_copy<Ip, k, k + 1>(XIN, dst, GT(A::LDL), A::Np(A::LDL), 0, b0);
     img((k & 1) ? A1 : A0, n, masked(acc[0], integral_constant<int, A::MD(i - 1)>{}));
   });
   bar();
@@ -889,7 +898,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     constexpr int TS = PL::step(PL::sD0b).TS, NTL = PL::step(PL::sD0b).NTL;
     f32x4 acc[TS];
     gemm<A, P, PL::sD0b>(ring, D0IN, acc, AR, wave, lane);
-    img_copy<H, 0, 1>(D0IN, GT(A::LD0), H, 0, b0);
+    img_copy<H, 0, 1>(D0IN, dst, GT(A::LD0), H, 0, b0);
     sfor<0, TS>([&](auto ss) {
       constexpr int s = decltype(ss)::value;
       const int t = wave + NW * s, f = 16 * t + n16;
@@ -915,7 +924,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   } else {
     f32x4 acc[NZT + 1];
     gemm<A, P, PL::sD0b>(ring, D0IN, acc, AR, wave, lane);
-    img_copy<H, 0, 1>(D0IN, GT(A::LD0), H, 0, b0);
+    img_copy<H, 0, 1>(D0IN, dst, GT(A::LD0), H, 0, b0);
 #pragma unroll
     for (int k = 0; k < NZT; ++k) {
       const int j = 16 * (wave + NW * k) + n16;
@@ -937,7 +946,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     f32x4 acc[2];
     gemm<A, P, PL::sFCb>(ring, GFC, acc, AR, wave, lane);
     sub();
-    img_copy<A::Np(A::LFC), 0, (2 * A::Np(A::LFC) + NT - 1) / NT>(GFC, GT(A::LFC), A::Np(A::LFC), 0, b0);
+    img_copy<A::Np(A::LFC), 0, (2 * A::Np(A::LFC) + NT - 1) / NT>(GFC, dst, GT(A::LFC), A::Np(A::LFC), 0, b0);
     if constexpr (A::SZ) dhc2 = *(const f32x4*)(DHC2 + n * R + 4 * q);
     img(A0, n, masked(acc[0], integral_constant<int, A::ME(NE - 1)>{}));
     img(CB, n, masked(acc[1] + dhc2, integral_constant<int, A::MC1>{}));
@@ -949,8 +958,8 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     __bf16* const in = (k & 1) ? A1 : A0;
     f32x4 acc[1];
     gemm<A, P, PL::sFCb + 1 + k>(ring, in, acc, AR, wave, lane);
-    img_copy<H, 0, 1>(in, GT(A::LE(i)), H, 0, b0);
-    if constexpr (k == 0) img_copy<H, 0, 1, 2 * H>(CB, GT(A::LC1), H, 0, b0);
+    img_copy<H, 0, 1>(in, dst, GT(A::LE(i)), H, 0, b0);
+    if constexpr (k == 0) img_copy<H, 0, 1, 2 * H>(CB, dst, GT(A::LC1), H, 0, b0);
     img((k & 1) ? A0 : A1, n, masked(acc[0], integral_constant<int, A::ME(i - 1)>{}));
   });
   bar();
@@ -960,7 +969,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     __bf16* const oC = GFC;                        // free (U region)
     f32x4 acc[1];
     gemm<A, P, PL::sC1b - 1>(ring, in, acc, AR, wave, lane);
-    img_copy<H, 0, 1>(in, GT(A::LE(1)), H, 0, b0);
+    img_copy<H, 0, 1>(in, dst, GT(A::LE(1)), H, 0, b0);
     img(oE, n, masked(acc[0], integral_constant<int, A::ME(0)>{}));
     gemm<A, P, PL::sC1b>(ring, CB, acc, AR, wave, lane);
     img(oC, n, masked(acc[0], integral_constant<int, A::MC0>{}));
@@ -978,8 +987,8 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
       PART[wave * 8 + 4] = s_relu;
     }
     bar();
-    img_copy<H, 0, 1>(oE, GT(A::LE0), H, 0, b0);
-    img_copy<H, 0, 1, 2 * H>(oC, GT(A::LC0), H, 0, b0);
+    img_copy<H, 0, 1>(oE, dst, GT(A::LE0), H, 0, b0);
+    img_copy<H, 0, 1, 2 * H>(oC, dst, GT(A::LC0), H, 0, b0);
   }
   if (tid < 5) {
     float s = 0.f;
