@@ -582,6 +582,19 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     }
     // the weight stream queues behind the x tile and the biases (vmcnt retires in order)
     ring_fill<A, P>(ring, AR, wave, lane);
+    // device counters: this launch begins optimizer step ctr[1] + 1 and precomputes its Adam
+    // scalars for the dW kernel behind it.  Wave 0 of block 0, wave-uniformly, while it waits for
+    // the x tile: the step count by scalar load, the f64 pow on every lane, one lane stores (at
+    // the kernel's end, one lane's f64 pow delays the chain's completion)
+    if (a.ctr && blk == 0 && wave == 0) {
+      const uint64_t t = *(const __attribute__((address_space(4))) uint64_t*)(a.ctr + 1) + 1;
+      float s0 = 0.f, s1 = 0.f;
+      if (a.adam_pre) adam_scalars(a.lr, a.beta1, a.beta2, (double)t, s0, s1);
+      if (lane == 0) {
+        a.ctr[1] = t;
+        if (a.adam_pre) *(adam_f32x2*)(a.ctr + 2) = adam_f32x2{s0, s1};
+      }
+    }
     sub();
     if (tid < 28 * 4) *(uint64_t*)(CIN + (4 + tid / 4) * 16 + 4 * (tid & 3)) = 0ull;
     if (tid < (Ip - I) * 4) *(uint64_t*)(XIN + (I + tid / 4) * 16 + 4 * (tid & 3)) = 0ull;
@@ -995,10 +1008,6 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     for (int w = 0; w < NW; ++w) s += PART[w * 8 + tid];
     gst<float>(a.partials + blk * 8 + tid, s);
   }
-  // device counters: this launch begins optimizer step ctr[1] + 1 and precomputes its Adam scalars
-  // for the dW kernel behind it — one lane of block 0, at the end (its loads and the f64 pow, under
-  // a branch, would otherwise stall the wave's weight stream)
-  if (a.ctr && blk == 0 && tid == 0) adam_precompute(a.ctr, a.lr, a.beta1, a.beta2, a.adam_pre);
   if (CVAE_DIAG_STAMPS && a.stamps && tid < 64)
     gst<unsigned long long>(a.stamps + blk * 64 + tid, tid < stamp_i ? STAMPS[tid] : 0ull);
 }
