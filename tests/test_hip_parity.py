@@ -520,6 +520,24 @@ def test_ring_chain_philox_training_and_determinism(cvae, monkeypatch):
     assert torch.equal(e3.params, e4.params) and torch.equal(e3.m, e4.m) and torch.equal(e3.v, e4.v)
 
 
+@pytest.mark.parametrize("ring", ["0", "1"])
+def test_reference_chain_repeatable(cvae, monkeypatch, ring):
+    """fastchain_kernel (default) and the ring chain (CVAE_RING=1) at the benchmark batch: eight
+    forward_backward calls on the same input and eps give bit-equal losses and gradients."""
+    torch.manual_seed(0)
+    ref = OracleCVAE(100, 6, 8)
+    monkeypatch.setenv("CVAE_RING", ring)
+    m, e = _model(cvae, 100, 6, 8, sd=ref.state_dict(), dtype="bf16", max_batch=1024)
+    monkeypatch.delenv("CVAE_RING")
+    assert e.train_kernel == ("ring" if ring == "1" else "fast")
+    x = torch.randn(1024, 100, 6, generator=torch.Generator().manual_seed(11)).to("cuda", torch.bfloat16)
+    eps = torch.randn(1024, 8, generator=torch.Generator().manual_seed(12))
+    l0 = e.forward_backward(x, eps=eps).clone()
+    g0 = e.grads.clone()
+    for _ in range(7):
+        assert torch.equal(e.forward_backward(x, eps=eps), l0) and torch.equal(e.grads, g0)
+
+
 def test_misaligned_input_runs_generic_chain(cvae):
     """x whose data pointer is not 16-B aligned takes the generic row chain (the fast chain loads
     16-B vectors) with the fast dW kernel behind it; the result matches the aligned run."""
