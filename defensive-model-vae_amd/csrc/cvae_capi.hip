@@ -675,16 +675,15 @@ bool wide_layout_matches(const cvae_handle* h) {
 
 // The reference architecture (the fast configuration, S=100: BASELINE cfg2) on the single-ring
 // weight-stream chain (cvae_widechain.h, small-latent form) instead of fastchain_kernel's per-step
-// register prefetch: the per-CU L2 stream stays busy across step barriers.  Opt-in (CVAE_RING=1 at
-// creation): measured equal to fastchain_kernel at B = 1024 (18.4-18.9 vs 18.5 us; both stream
-// ~1.05 MB of weight fragments per workgroup at the per-CU L2 rate).  The fused single
-// launch (CVAE_FUSE=1) is fastchain's.
+// register prefetch: the per-CU L2 stream stays busy across step barriers.  The default for this
+// shape (row chain 17.8 vs 18.35 us at B = 1024); CVAE_RING=0 at creation keeps
+// fastchain_kernel.  The fused single launch (CVAE_FUSE=1) is fastchain's.
 int plan_ring(cvae_handle* h) {
   using A = wchain::Cfg2;
   const cvae_config& c = h->cfg;
   h->ring = false;
   const char* env = std::getenv("CVAE_RING");
-  if (!(env && env[0] == '1') || h->fast_nki != 19 || c.seq_len != A::S || c.dim != A::D) return CVAE_OK;
+  if ((env && env[0] == '0') || h->fast_nki != 19 || c.seq_len != A::S || c.dim != A::D) return CVAE_OK;
   if (!wide_layout_matches<A>(h) || h->arena_bytes >= ((int64_t)1 << 31)) return CVAE_OK;
   HIPCK(hipFuncSetAttribute((const void*)wchain::widechain_kernel<A>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             A::L_TOTAL));

@@ -137,7 +137,7 @@ int cvae_bucket_split(const cvae_handle* h, int64_t* split);
  * (bf16, the reference architecture: hidden 128, latent 8, 4+4 layers, seq_len*dim 600) or
  * CVAE_KERNEL_WIDE (bf16, BASELINE cfg5's shape: seq_len 200, dim 6, latent 512, 8+8 layers) or
  * CVAE_KERNEL_RING (the fast configuration at seq_len 100, dim 6 on the single-ring weight-stream
- * chain, opt-in: CVAE_RING=1 at creation).
+ * chain: the default at that shape; CVAE_RING=0 at creation keeps CVAE_KERNEL_FAST).
  * Introspection only (no reference counterpart); CVAE_GENERIC=1 at creation forces the generic. */
 enum cvae_train_kernel_kind {
   CVAE_KERNEL_GENERIC = 0, CVAE_KERNEL_FAST = 1, CVAE_KERNEL_WIDE = 2, CVAE_KERNEL_RING = 3

@@ -446,15 +446,16 @@ def test_fast_and_generic_kernels_agree(cvae, monkeypatch):
 
 def _ring_pair(cvae, monkeypatch, B, seed=0):
     """Two bf16 engines of the reference architecture (S=100, D=6) on the same weights: the
-    single-ring chain (CVAE_RING=1 at creation, cvae_widechain.h small-latent form) and
-    fastchain_kernel (the default)."""
+    single-ring chain (the default, cvae_widechain.h small-latent form) and fastchain_kernel
+    (CVAE_RING=0 at creation)."""
     torch.manual_seed(seed)
     ref = OracleCVAE(100, 6, 8)
     monkeypatch.delenv("CVAE_GENERIC", raising=False)
-    monkeypatch.setenv("CVAE_RING", "1")
+    monkeypatch.delenv("CVAE_RING", raising=False)
     m1, e1 = _model(cvae, 100, 6, 8, sd=ref.state_dict(), dtype="bf16", max_batch=max(B, 32))
-    monkeypatch.delenv("CVAE_RING")
+    monkeypatch.setenv("CVAE_RING", "0")
     m2, e2 = _model(cvae, 100, 6, 8, sd=ref.state_dict(), dtype="bf16", max_batch=max(B, 32))
+    monkeypatch.delenv("CVAE_RING")
     assert e1.train_kernel == "ring" and e2.train_kernel == "fast"
     return ref, m1, e1, m2, e2
 
