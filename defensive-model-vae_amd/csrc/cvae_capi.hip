@@ -770,7 +770,7 @@ int launch_train_chain(cvae_handle* h, RowArgs ra, hipStream_t s) {
     ra.stamps = h->d_stamps;
     const int grid = rup_i(ra.batch, 32) / wchain::R;
     return klaunch(h, wchain::widechain_kernel<wchain::Cfg2>, dim3(grid), dim3(wchain::NT), h->ring_lds, s,
-                   h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra);
+                   h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra.ctr, ra);
   }
   if (std::is_same<T, __bf16>::value && fast_ok(h, ra)) {
     ra.steps = h->d_steps[cvae_handle::ST_TRAIN];
@@ -785,9 +785,9 @@ int launch_train_chain(cvae_handle* h, RowArgs ra, hipStream_t s) {
     const int grid = rup_i(ra.batch, 32) / wchain::R;
     if (h->cfg.dtype == CVAE_FP8)
       return klaunch(h, wchain::widechain_kernel<wchain::Cfg5F8>, dim3(grid), dim3(wchain::NT), h->wide_lds, s,
-                     h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra);
+                     h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra.ctr, ra);
     return klaunch(h, wchain::widechain_kernel<wchain::Cfg5>, dim3(grid), dim3(wchain::NT), h->wide_lds, s,
-                   h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra);
+                   h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra.ctr, ra);
   }
   return launch_rowchain<T, RC_TRAIN>(h, ra, s);
 }

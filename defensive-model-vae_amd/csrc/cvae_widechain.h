@@ -1026,14 +1026,18 @@ constexpr int RING = CVAE_WIDE_RING;
 #define CVAE_RING_P 12
 #endif
 
+// ctr (the device step counters) rides in the preloaded kernel-argument SGPRs beside the x-tile
+// arguments: read from RowArgs, the Philox-offset load waited for a kernel-argument fetch before
+// the first x load could issue
 template <class A>
 __global__ __launch_bounds__(NT) void widechain_kernel(char* arena, const void* x, const int64_t* idx, int Bp,
-                                                       int batch, RowArgs a) {
+                                                       int batch, uint64_t* ctr, RowArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   RowArgs ra = a;
   ra.x = x;
   ra.idx = idx;
   ra.batch = batch;
+  ra.ctr = ctr;
   wide_body<A, A::SZ ? CVAE_RING_P : RING>(arena, Bp, ra, smem, blockIdx.x);
 }
 
