@@ -23,7 +23,7 @@ for f in sorted(glob.glob(f"{d}/bench_*.json"), key=lambda p: int(p.rsplit("_", 
     for c in glob.glob(f"{d}/**/pmc_{B}*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(c)):
             k = r.get("Kernel_Name", "?")
-            k = "rowchain" if "fastchain" in k else "wgrad_adam" if "fastwgrad" in k else None
+            k = "rowchain" if ("fastchain" in k or "widechain" in k) else "wgrad_adam" if "fastwgrad" in k else None
             if k:
                 acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     rows.append((B, b, {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}))
