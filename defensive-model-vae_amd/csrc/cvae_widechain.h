@@ -208,6 +208,9 @@ struct Plan {
                 "step plan");
 };
 
+#ifndef CVAE_RING_SKIP
+#define CVAE_RING_SKIP 1
+#endif
 template <int P>
 struct Ring {
   bf16x8 r[P];
@@ -229,7 +232,13 @@ __device__ __forceinline__ void ring_load(Ring<P>& ring, const char* AR, int wav
     int t = w + NW * slot;
     if constexpr (NW * (slot + 1) > st.NTL) t = min(t, st.NTL - 1);
     const int64_t frag = st.KS ? w : t * st.KC + kc;  // KS: tile 0, chunk = wave
-    ring.r[G % P] = CVAE_DIAG_NOWLOAD ? bf16x8{} : gld<bf16x8>(AR + base + frag * 1024 + lane * 16);
+    if constexpr (CVAE_RING_SKIP && !st.KS && NW * (slot + 1) > st.NTL) {
+      // a slot past the layer's tiles: no load (wave-uniform); the stale ring register feeds an
+      // MFMA whose result the epilogue drops
+      if (w + NW * slot < st.NTL) ring.r[G % P] = gld<bf16x8>(AR + base + frag * 1024 + lane * 16);
+    } else {
+      ring.r[G % P] = CVAE_DIAG_NOWLOAD ? bf16x8{} : gld<bf16x8>(AR + base + frag * 1024 + lane * 16);
+    }
   }
 }
 
