@@ -71,6 +71,10 @@ struct cvae_handle {
   unsigned* splitk_tickets = nullptr;
   char* arena = nullptr;    // weight copies + activations
   unsigned* d_sync = nullptr;  // fused launch hand-off words (fchain::FusedArgs::sync), zero between launches
+  // sticky fault word in pinned, device-mapped host memory: a kernel that gives up a bounded spin
+  // sets it (system scope); the next training call reads it WITHOUT synchronising and fails
+  unsigned* fault_host = nullptr;
+  unsigned* fault_dev = nullptr;
   bool fused = false;          // training steps run as one fused_step_kernel launch
   int64_t arena_bytes = 0;
   float* d_partials = nullptr;
@@ -412,6 +416,9 @@ int alloc_arena(cvae_handle* h) {
   for (int m = 0; m < cvae_handle::ST_N; ++m) step_off[m] = take(64 * (int64_t)sizeof(StepDesc));
   HIPCK(hipMalloc(&h->arena, total));
   HIPCK(hipMemset(h->arena, 0, total));
+  HIPCK(hipHostMalloc((void**)&h->fault_host, 64, hipHostMallocMapped | hipHostMallocCoherent));
+  std::memset(h->fault_host, 0, 64);
+  HIPCK(hipHostGetDevicePointer((void**)&h->fault_dev, h->fault_host, 0));
   h->arena_bytes = total;
   for (int l = 0; l < n.n_layers; ++l) {
     LayerDev& L = n.L[l];
@@ -847,6 +854,25 @@ int launch_wgrad(cvae_handle* h, int batch, const AdamArgs& aa, const LossArgs& 
                  (const TileDesc*)h->d_wtiles, bk_of(h, batch), aa, la, sk);
 }
 
+// a training call fails while the handle's fault word is set (a kernel of an earlier call gave up
+// a bounded spin and skipped work: that step's parameters are incomplete).  A host read of pinned
+// memory the device writes at system scope: no synchronisation
+int check_fault(const cvae_handle* h) {
+  if (h->fault_host && __atomic_load_n(h->fault_host, __ATOMIC_ACQUIRE))
+    return fail(CVAE_E_TIMEOUT, "an earlier training launch timed out waiting for a hand-off and skipped its "
+                                "update (fault word set); the parameters are incomplete — cvae_clear_fault after "
+                                "restoring them");
+  return CVAE_OK;
+}
+
+// a step with no rows on this rank (a ragged global batch shorter than the world): advance the
+// device counters exactly as a row chain + dW launch would (steps begun + that step's Adam scalars,
+// Philox offset), so this rank's Adam and eps stay in step with the others
+__global__ void step_skip_kernel(uint64_t* c, double lr, double b1, double b2) {
+  adam_precompute(c, lr, b1, b2, true);
+  c[0] = c[0] + 1;
+}
+
 // device counters, fused launch: its chain blocks do not bump the step (its dW tiles read it in the
 // same launch), so the step begins with this one-lane kernel; the loss tile advances the offset
 // after every chain block has published (read) it
@@ -862,6 +888,7 @@ int launch_fused(cvae_handle* h, RowArgs ra, const AdamArgs& aa, float* loss_out
   f.aa = aa;
   f.la = make_loss(h, ra, loss_out, loss_accum);
   f.sync = h->d_sync;
+  f.fault = h->fault_dev;
   f.Bk = bk_of(h, ra.batch);
   f.nchain = rup_i(ra.batch, 32) / fchain::R;
   const int nt = fchain::Tiles<19>::total();
@@ -955,6 +982,7 @@ int cvae_destroy(cvae_handle* h) {
   if (!h) return CVAE_OK;
   for (auto e : h->pool) (void)hipEventDestroy(e);
   if (h->arena) (void)hipFree(h->arena);
+  if (h->fault_host) (void)hipHostFree(h->fault_host);
   delete h;
   return CVAE_OK;
 }
@@ -1072,6 +1100,7 @@ int cvae_train_fwd_bwd(cvae_handle* h, const void* x, const int64_t* idx, const 
   if (parts != CVAE_PART_ALL && parts != (CVAE_PART_CHAIN | CVAE_PART_DW_DEC) && parts != CVAE_PART_DW_REST)
     return fail(CVAE_E_INVALID, "parts must be CVAE_PART_ALL, CHAIN|DW_DEC, or DW_REST");
   int rc = check_batch(h, batch);
+  if (!rc) rc = check_fault(h);
   if (rc) return rc;
   if (adam && (rc = check_adam(adam))) return rc;
   return fwd_bwd_impl(h, CallX{x, idx, classes, batch, xflags, eps, seed, offset, eps_row0, w, counters, adam}, grads,
@@ -1105,6 +1134,7 @@ int cvae_adam(cvae_handle* h, float* params, const float* grads, float* m, float
   if (!h || !params || !grads || !m || !v) return fail(CVAE_E_INVALID, "null argument");
   if (!counters && step < 1) return fail(CVAE_E_INVALID, "step must be >= 1");
   int rc = check_adam(adam);
+  if (!rc) rc = check_fault(h);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   AdamArgs aa = make_adam(params, (float*)grads, m, v, step, *adam, grad_scale, counters);
@@ -1126,6 +1156,7 @@ int cvae_train_step(cvae_handle* h, const void* x, const int64_t* idx, const int
   if (!counters && step < 1) return fail(CVAE_E_INVALID, "step must be >= 1");
   int rc = check_batch(h, batch);
   if (!rc) rc = check_adam(adam);
+  if (!rc) rc = check_fault(h);
   if (rc) return rc;
   return train_step_impl(h, CallX{x, idx, classes, batch, xflags, eps, seed, offset, eps_row0, w, counters, adam}, params, m, v,
                          step, adam, loss_out, loss_accum, (hipStream_t)stream);
@@ -1188,6 +1219,28 @@ int cvae_bench_kernels(cvae_handle* h, const void* x, const int64_t* idx, int ba
   (void)hipEventDestroy(e1);
   h->timing = timing;
   return rc;
+}
+
+int cvae_step_skip(cvae_handle* h, uint64_t* counters, const cvae_adam_config* adam, void* stream) {
+  if (!h || !counters) return fail(CVAE_E_INVALID, "null argument");
+  int rc = check_adam(adam);
+  if (rc) return rc;
+  hipLaunchKernelGGL(step_skip_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, counters, adam->lr, adam->beta1,
+                     adam->beta2);
+  HIPCK(hipGetLastError());
+  return CVAE_OK;
+}
+
+int cvae_fault(const cvae_handle* h, unsigned* word) {
+  if (!h || !word) return fail(CVAE_E_INVALID, "null argument");
+  *word = h->fault_host ? __atomic_load_n(h->fault_host, __ATOMIC_ACQUIRE) : 0u;
+  return CVAE_OK;
+}
+
+int cvae_clear_fault(cvae_handle* h) {
+  if (!h) return fail(CVAE_E_INVALID, "null argument");
+  if (h->fault_host) __atomic_store_n(h->fault_host, 0u, __ATOMIC_RELEASE);
+  return CVAE_OK;
 }
 
 int cvae_sync_words(cvae_handle* h, unsigned* out) {

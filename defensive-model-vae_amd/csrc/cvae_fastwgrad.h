@@ -215,6 +215,7 @@ struct FusedArgs {
   AdamArgs aa;
   LossArgs la;
   unsigned* sync;  // [0..2] group counters (zeroed by the host before the launch), [3] unused, [4] sticky spin time-out flag
+  unsigned* fault; // the handle's fault word (pinned host memory): set on a time-out, fails the next training call
   int Bk;          // batch rows rounded to the dW K chunk
   int nchain;      // row-chain blocks
 };
@@ -247,6 +248,7 @@ __global__ __launch_bounds__(NT) void fused_step_kernel(FastNet fn, RowArgs a, F
       __builtin_amdgcn_s_sleep(FUSED_SLEEP);  // ~FUSED_SLEEP·64 cycles: ~200 pollers must not load the fabric
       if (++spins == (1u << 24) / FUSED_SLEEP) {
         __hip_atomic_store(f.sync + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (f.fault) __hip_atomic_store(f.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         to = 1;
         break;
       }

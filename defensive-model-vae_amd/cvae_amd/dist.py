@@ -116,8 +116,9 @@ class DataParallelStep:
                                  **({"classes": classes} if classes is not None else {}))
             ragged = batch * self.world_size != global_batch
             scale = 1.0 if ragged else 1.0 / self.world_size
-        else:  # an empty share of a ragged last batch still joins the collectives
-            eng.grads.zero_()
+        else:  # an empty share of a ragged last batch still joins the collectives, and its device
+            eng.grads.zero_()  # step counters advance as the other ranks' launches advance theirs
+            eng.skip_step()
             ragged, scale = True, 1.0
         g = eng.grads
         if two:

@@ -323,6 +323,41 @@ class CVAEEngine:
         self._ctr[1] += n_steps
         return self.loss
 
+    def prepare_steps(self, x, batch=None, weights=None, accumulate=True, row0=0):
+        """A callable ``run(n)`` that enqueues ``n`` fused steps on rows 0..batch-1 of the resident
+        ``x`` with Philox eps (cvae_train_steps) — what ``train_steps(x, n, batch=batch)`` does,
+        with every argument converted once here instead of per call.
+
+        train_steps spends ~40 µs of Python (input checks, the parameter-version scan of
+        ensure_packed, ctypes conversion of 21 arguments, the current-stream lookup) before its
+        first launch; a timed run of a few steps pays that once (short runs).  The
+        prepared call is bound to this stream, x, batch and these optimizer/loss settings; the
+        parameters must not be written from outside the engine between calls (call
+        ``ensure_packed`` / prepare again after ``load_state_dict`` or an external optimizer)."""
+        x = self.as_input(x, keep_f32=self.keep_f32)
+        B = int(batch if batch is not None else x.shape[0])
+        self._check_rows(x, None, B)
+        if self.n_classes:
+            raise ValueError("prepare_steps serves the reference model (n_classes=0)")
+        self.ensure_packed()
+        f = lib().cvae_train_steps
+        w = self._weights(weights)
+        a = self._adam()
+        keep = (x, w, a)  # referenced by the closure: the pointers stay valid
+        pre = (self._h, C.c_void_p(x.data_ptr()), None, None, C.c_int(B))
+        post = (C.c_int(self._xflags(x)), None, C.c_uint64(self.seed), C.c_uint64(0), C.c_int64(int(row0)),
+                C.byref(w), ptr(self.params), ptr(self.m), ptr(self.v), C.c_int64(0), C.byref(a), ptr(self.loss),
+                ptr(self.loss_accum) if accumulate else None, ptr(self.counters), self._stream())
+        ctr = self._ctr
+
+        def run(n, _f=f, _pre=pre, _post=post, _keep=keep, _ctr=ctr, _i=C.c_int):
+            rc = _f(*_pre, _i(n), *_post)
+            if rc < 0:
+                check(rc, "cvae_train_steps")
+            _ctr[0] += n
+            _ctr[1] += n
+        return run
+
     def forward_backward(self, x, idx=None, eps=None, batch=None, weights=None, accumulate=True, row0=0,
                          parts=CVAE_PART_ALL, classes=None):
         """fwd + loss + bwd into ``self.grads`` (means over this batch) — the DP half-step.
@@ -358,6 +393,24 @@ class CVAEEngine:
         a = self._adam()
         check(lib().cvae_adam(self._h, ptr(self.params), ptr(self.grads), ptr(self.m), ptr(self.v), 0,
                               C.byref(a), float(grad_scale), ptr(self.counters), self._stream()), "cvae_adam")
+
+    def skip_step(self):
+        """A data-parallel step with no rows on this rank (cvae_step_skip): the device counters
+        advance as a forward_backward would (step begun + its Adam scalars, Philox offset), so the
+        following adam_step matches every other rank's."""
+        check(lib().cvae_step_skip(self._h, ptr(self.counters), C.byref(self._adam()), self._stream()),
+              "cvae_step_skip")
+        self._ctr[0] += 1
+        self._ctr[1] += 1
+
+    def fault(self):
+        """The handle's sticky fault word (cvae_fault): non-zero after a launch gave up a bounded wait."""
+        w = C.c_uint()
+        check(lib().cvae_fault(self._h, C.byref(w)), "cvae_fault")
+        return w.value
+
+    def clear_fault(self):
+        check(lib().cvae_clear_fault(self._h), "cvae_clear_fault")
 
     def adam_host_step(self, step, grad_scale=1.0, grads=None):
         """Adam with a host step number (no device counters): grads default ``self.grads``."""

@@ -105,12 +105,13 @@ def save_checkpoint(path, model, eng, epoch, loss_history):
 def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidden_dim=128,
           weights=(0.1, 0.1, 1.0, 1.0), model_save_path=None, loss_save_path=None, dtype="fp32",
           eps="host", device=None, seed=None, engine_seed=0, log=print, model=None, buckets=1,
-          checkpoint_path=None, resume=None, classes=None, class_dim=16):
+          checkpoint_path=None, resume=None, classes=None, class_dim=0):
     """Train like ``python Training_VAE.py`` (mode='training').
 
     data: path to the (N, seq_len, dim) ``.npy`` (TrajectoryDataset, :105-115) or an array; or a
-    LIST of paths (scenes) — their rows are concatenated and, with ``class_dim`` > 0, each row's
-    class is its file's index (BASELINE cfg4: one model over the Town04/Town05 scenes).
+    LIST of paths (scenes) — their rows are concatenated and, with ``class_dim`` > 0 and more than
+    one file, each row's class is its file's index (BASELINE cfg4: one model over the Town04/Town05
+    scenes); the default ``class_dim=0`` trains the reference's 24-key model on the rows.
     classes: per-row class ids (cfg4 class embedding, ``class_dim`` wide); None = the reference model.
     weights: (recon, kld, start, time) — the values of :300-306.
     seed: if given, ``torch.manual_seed(seed)`` first (the reference leaves it unseeded).
@@ -130,7 +131,7 @@ def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidd
     if isinstance(data, (list, tuple)) and data and isinstance(data[0], (str, os.PathLike)):
         parts = [TrajectoryDataset(p).data for p in data]
         arr = np.ascontiguousarray(np.concatenate(parts, 0))
-        if classes is None and class_dim:
+        if classes is None and class_dim and len(parts) > 1:
             classes = np.concatenate([np.full(len(a), i, np.int32) for i, a in enumerate(parts)])
     elif isinstance(data, (str, os.PathLike)):
         arr = TrajectoryDataset(data).data
@@ -171,7 +172,7 @@ def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidd
         ck = torch.load(resume, weights_only=True)
         model.load_state_dict(ck["model"])
         load_optimizer_state_dict(eng, ck["optimizer"])
-        eng.set_optimizer(lr=lr)
+        eng.set_optimizer(lr=lr, betas=eng.betas, eps=eng.eps)  # the checkpoint's betas / eps stay
         eng.rng_offset = ck["rng_offset"]
         torch.set_rng_state(ck["cpu_rng_state"])
         loss_history = {k: list(ck["loss_history"][k]) for k in LOSS_KEYS}

@@ -47,7 +47,8 @@ enum cvae_status {
   CVAE_E_INVALID = -1,   /* bad argument / unsupported configuration        */
   CVAE_E_HIP = -2,       /* a HIP runtime call failed (message has details) */
   CVAE_E_CAPACITY = -3,  /* batch larger than cfg.max_batch                  */
-  CVAE_E_NOMEM = -4
+  CVAE_E_NOMEM = -4,
+  CVAE_E_TIMEOUT = -5    /* an earlier launch gave up a bounded wait and skipped work (fault word) */
 };
 
 /* Input flags (the `xflags` argument of the calls that read trajectories). */
@@ -285,6 +286,22 @@ int cvae_bench_kernels(cvae_handle* h, const void* x, const int64_t* idx, int ba
  * step's parameters are incomplete: the caller must treat the step as failed).  Synchronises
  * the device. */
 int cvae_sync_words(cvae_handle* h, unsigned* out);
+
+/* The handle's sticky fault word.  A kernel that waits on a hand-off (the fused launch's tiles, the
+ * peer exchange) waits a bounded time; on a time-out it skips its update and sets this word in
+ * pinned host memory.  Every later training call (cvae_train_step[s], cvae_train_fwd_bwd, cvae_adam)
+ * then returns CVAE_E_TIMEOUT without launching; the check reads host memory and does not
+ * synchronise, so it sees a time-out once the faulting launch has run.  cvae_fault reads the word,
+ * cvae_clear_fault resets it (after the caller restored consistent parameters). */
+int cvae_fault(const cvae_handle* h, unsigned* word);
+int cvae_clear_fault(cvae_handle* h);
+
+/* A data-parallel step in which this rank has no rows (a ragged last global batch shorter than the
+ * world): advances the device counters exactly as a training step's launches would — counters[1]
+ * += 1 with that step's Adam scalars, counters[0] += 1 — so the rank's following cvae_adam uses the
+ * same step number and scalars as every other rank, and its later eps draws stay in step
+ * (Training_VAE.py:363, the step every rank takes). */
+int cvae_step_skip(cvae_handle* h, uint64_t* counters, const cvae_adam_config* adam, void* stream);
 
 /* Adam's per-step scalars as the device computes them from a step counter (t = 1..n): writes
  * out[2*(t-1)] = -lr/(1-beta1^t) and out[2*(t-1)+1] = sqrt(1-beta2^t), both rounded to fp32 —

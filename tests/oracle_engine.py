@@ -53,6 +53,10 @@ class OracleEngine:
 
     def forward_backward(self, x, idx=None, eps=None, batch=None, weights=None, accumulate=True, row0=0, parts=7,
                          classes=None):
+        # the device-counter path: the launch that begins a step advances steps-begun and the offset;
+        # adam_step then takes its step number from that counter (CVAEEngine / include/cvae.h)
+        self.step_count += 1
+        self.rng_offset += 1
         self.calls.append(("fb", None if idx is None else idx.clone(), batch, row0, parts))
         rows = x[idx] if idx is not None else x[:batch]
         cls = None if classes is None else (classes[idx] if idx is not None else classes[:batch]).long()
@@ -73,8 +77,13 @@ class OracleEngine:
     def wgrad_rest(self, batch=None):
         self.calls.append(("rest", None, batch, None, 4))
 
-    def adam_step(self, grad_scale=1.0):
+    def skip_step(self):
+        """cvae_step_skip: an empty share advances the counters as a forward_backward would."""
+        self.calls.append(("skip", None, 0, None, 0))
         self.step_count += 1
+        self.rng_offset += 1
+
+    def adam_step(self, grad_scale=1.0):
         b1, b2 = self.betas
         g = self.grads * grad_scale if grad_scale != 1.0 else self.grads
         self.m.lerp_(g, 1 - b1)

@@ -382,3 +382,57 @@ def test_splitk_dw_matches_single_split_and_is_deterministic(cvae, monkeypatch, 
     e3.adam_step()
     torch.cuda.synchronize()
     assert torch.equal(e2.params, e3.params) and torch.equal(e2.m, e3.m)
+
+
+# ---------------------------------------------------------------- round 3: empty shares, fault word, prepared call
+def test_step_skip_advances_counters_like_a_step(cvae):
+    """cvae_step_skip (a rank with no rows in a ragged global batch) advances the device counters
+    exactly as forward_backward does — steps begun, that step's Adam scalars, the Philox offset —
+    so the following adam_step on a zero gradient uses every other rank's step number."""
+    torch.manual_seed(0)
+    ref = OracleCVAE(100, 6, 8)
+    _, a = _model(cvae, 100, 6, 8, sd=ref.state_dict(), dtype="bf16", max_batch=64)
+    _, b = _model(cvae, 100, 6, 8, sd=ref.state_dict(), dtype="bf16", max_batch=64)
+    x = a.as_input(torch.randn(64, 100, 6, generator=torch.Generator().manual_seed(3)))
+    for _ in range(3):
+        a.forward_backward(x, batch=64)
+        a.adam_step()
+        b.grads.zero_()
+        b.skip_step()
+        b.adam_step()
+    torch.cuda.synchronize()
+    assert torch.equal(a.counters, b.counters)          # [offset, steps, the step's Adam scalars]
+    assert a._ctr == b._ctr == [3, 3]
+    assert b.sync_counters() == (3, 3)
+
+
+def test_fault_word_starts_clear_and_clears(cvae):
+    """The handle's sticky fault word (pinned host memory a timed-out launch sets) reads 0 on a
+    healthy handle and after cvae_clear_fault; training calls check it without synchronising."""
+    _, eng = _model(cvae, 100, 6, 8, dtype="bf16", max_batch=64)
+    assert eng.fault() == 0
+    x = eng.as_input(torch.randn(64, 100, 6))
+    eng.train_step(x)
+    torch.cuda.synchronize()
+    assert eng.fault() == 0
+    eng.clear_fault()
+    assert eng.fault() == 0
+
+
+def test_prepared_steps_equal_train_steps(cvae):
+    """prepare_steps (bench.py's timed call: arguments converted once) runs exactly train_steps:
+    params, moments, counters and loss accumulators equal bit for bit."""
+    torch.manual_seed(0)
+    ref = OracleCVAE(100, 6, 8)
+    _, a = _model(cvae, 100, 6, 8, sd=ref.state_dict(), dtype="bf16", max_batch=1024)
+    _, b = _model(cvae, 100, 6, 8, sd=ref.state_dict(), dtype="bf16", max_batch=1024)
+    x = a.as_input(torch.randn(1024, 100, 6, generator=torch.Generator().manual_seed(11)))
+    a.train_steps(x, 5, batch=1024)
+    a.train_steps(x, 3, batch=1024)
+    run = b.prepare_steps(x, batch=1024)
+    run(5)
+    run(3)
+    torch.cuda.synchronize()
+    for k in ("params", "m", "v", "counters", "loss", "loss_accum"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+    assert a._ctr == b._ctr

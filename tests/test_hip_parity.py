@@ -264,20 +264,20 @@ def test_bf16_training_decreases_loss_full_size(cvae):
     assert float(last[0]) < 0.7 * float(first[0])
 
 
-def test_philox_eps_is_standard_normal_and_deterministic(cvae):
+def test_philox_forward_deterministic_per_offset(cvae):
+    """Same (seed, offset) → bit-identical sampled forward; another offset → another draw.  (The
+    distribution itself — mean, variance, KS, lag correlation over 2^20 draws — is checked by
+    test_gpu_dp_autograd.py::test_philox_eps_statistics_and_determinism.)"""
     torch.manual_seed(0)
     m, eng = _model(cvae, 10, 3, 8, max_batch=4096, seed=123)
     x = torch.randn(4096, 10, 3).cuda()
-    eng.rng_offset = 7
-    _, mu, lv, _ = eng.forward(x)
     eng.rng_offset = 7
     r1, _, _, _ = eng.forward(x)
     eng.rng_offset = 7
     r2, _, _, _ = eng.forward(x)
     assert torch.equal(r1, r2)
-    # recover eps through z = mu + eps*std is not exposed; check the decode of the sampled z statistically
     zs = []
-    for off in range(4):
+    for off in range(2):
         eng.rng_offset = off
         rec, mu, lv, _ = eng.forward(x, outputs=("recon", "mu", "logvar"))
         zs.append(rec)
