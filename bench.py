@@ -223,6 +223,10 @@ def main():
                     help="operand dtype (default: bf16; cfg1: fp32)")
     ap.add_argument("--dp", action="store_true",
                     help="data-parallel split step even at N=1: fwd/bwd → RCCL all-reduce → Adam")
+    ap.add_argument("--exchange", default="auto", choices=["auto", "peer", "rccl"],
+                    help="N>1 gradient exchange: peer = dW + reduce-scatter + Adam + all-gather inside the "
+                         "weight-gradient launch over IPC-mapped peer memory (cvae_amd.peer); rccl = all-reduce of "
+                         "the flat gradient, then Adam; auto = peer where the configuration has it")
     ap.add_argument("--buckets", type=int, default=1, choices=[1, 2],
                     help="split step: 2 = decoder-gradient all-reduce overlapped with the rest of dW")
     ap.add_argument("--graph", action="store_true",
@@ -243,6 +247,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N>1 path on a one-GPU box: every rank on GPU 0, gloo for the host-side
+    # collectives (RCCL refuses two ranks on one GPU); the numbers are not a scaling measurement
+    share = os.environ.get("CVAE_BENCH_SHARE_GPU") == "1"
+    if share:
+        local = 0
     if world > 1 or args.dp:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if world == 1:
@@ -250,7 +259,10 @@ def main():
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -268,7 +280,8 @@ def main():
     torch.manual_seed(0)
     model = ConditionalTrajectoryVAE(S, D, Z, H, NE, ND)
     eng = model.attach(dtype=dtype, max_batch=B, device=dev, seed=4321)
-    dp = DataParallelStep(eng, force_split=args.dp, buckets=args.buckets)
+    dp = DataParallelStep(eng, force_split=args.dp, buckets=args.buckets,
+                          exchange="rccl" if wl == "cfg1" else args.exchange)
     dp.broadcast_params()
 
     if wl == "cfg1":
@@ -302,10 +315,13 @@ def main():
         x = eng.as_input(x)  # resident in HBM, operand dtype
         rows_per_step = B
         graphed = prepared = None
-        use_graph = args.graph or (dp.split and not args.no_graph)
+        use_graph = args.graph or (dp.split and dp.px is None and not args.no_graph)
         graph_note = ""
         graphed1 = None
-        if not dp.split and not use_graph:
+        if dp.px is not None and not use_graph:
+            # peer exchange: two launches per step, no collective call, no host work per step
+            prepared = dp.px.prepare(x, B)
+        elif not dp.split and not use_graph:
             # the fused steps through one prepared C call (arguments converted once): train_steps'
             # ~40 us of Python before the first launch would otherwise be a fixed cost of every
             # timed region — 1.5 us per step at the driver's 20 steps (short runs)
@@ -365,7 +381,7 @@ def main():
     # each kernel alone, launched back-to-back (cvae_bench_kernels): the step's kernels without
     # their neighbours' cache/instruction-cache effects
     b2b = None
-    if not args.no_b2b and wl != "cfg1":
+    if not args.no_b2b and wl != "cfg1" and world == 1:
         b2b = eng.bench_kernels(x, max(args.steps, 20), batch=B)
     if world > 1:
         tt = torch.tensor([t], device=dev, dtype=torch.float64)
@@ -374,6 +390,7 @@ def main():
     if not os.environ.get("CVAE_LIB"):  # diagnostic builds (scripts/bench_variants.sh) compute garbage
         assert torch.isfinite(eng.loss).all(), "non-finite loss"
 
+    px_stats = dp.px.stats() if dp.px is not None else None
     if rank == 0:
         fl = flops_per_traj(S, D, Z, H, n_enc=NE, n_dec=ND)
         tsize = 4 if dtype == "fp32" else 2  # fp8: bf16 activations
@@ -388,6 +405,9 @@ def main():
         flop["fused_step"] = flop["rowchain"] + flop["wgrad_adam"]
         nbytes["fused_step"] = nbytes["rowchain"] + nbytes["wgrad_adam"]
         flop["adam"], nbytes["adam"] = 0, ADAM_BYTES_PER_PARAM * n_par
+        # peer exchange: every dW tile over the local rows + Adam on this rank's 1/world of the tiles
+        flop["px_wgrad"] = flop["wgrad"]
+        nbytes["px_wgrad"] = bt["wgrad"] * rows_launch + ADAM_BYTES_PER_PARAM * n_par // max(world, 1)
         dom = max((k for k in kt if k in flop and flop[k] > 0), key=lambda k: kt[k][0])
         std = (S, D, Z, H, NE, ND) == (100, 6, 8, 128, 4, 4)
         traffic = measured_traffic(args.traffic_file, dom, B, dtype) if std else None
@@ -416,6 +436,8 @@ def main():
             data = "synthetic x~N(0,1) (seeded), random-init weights (torch.manual_seed(0))"
         if wl == "cfg1":
             path = "split" if dp.split else "fused"
+        elif dp.px is not None:
+            path = "peer-exchange (dW + reduce-scatter + Adam + all-gather in one launch, no collective)"
         else:
             path = (("graphed " if graphed is not None else "") + ("split" if dp.split else "fused")
                     + (f" x{graphed.n}/replay" if graphed is not None and graphed.n > 1 else "") + graph_note)
@@ -425,16 +447,21 @@ def main():
                "scaling": "weak", "vs_baseline": None, "dtype": dtype, "data": data,
                "config": {"workload": f"{wl}: Training_VAE step, B_local={B} S={S} D={D} Z={Z} H={H}, "
                                       f"{NE}+{ND} layers, {dtype} operands / fp32 master+Adam, {path} step"
-                                      + (f", {args.buckets} buckets" if dp.split else ""),
+                                      + (f", rccl all-reduce, {args.buckets} buckets" if dp.split and dp.px is None
+                                         else "") + (f" [{dp.exchange_note}]" if dp.exchange_note else ""),
                           "global_batch": B * world, "seq_len": S, "state_dim": D, "latent_dim": Z,
-                          "hidden_dim": H, "parallelism": f"dp{world}"},
+                          "hidden_dim": H, "parallelism": f"dp{world}" + (" (rehearsal: all ranks on GPU 0)"
+                                                                          if share else "")},
                "roofline": roof,
                "flop_per_traj": fl["total"]}
+        if px_stats is not None:
+            res["exchange_waits_rank0"] = px_stats
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(B, S, D, Z, H, args.cpu_seconds, NE, ND,
                                                data=data_cpu if wl == "cfg1" else None)
             res["speedup_vs_cpu"] = round(value / res["cpu_baseline"]["value"], 1)
         print(json.dumps(res), file=out, flush=True)
+    dp.close()
     if dist.is_initialized():
         dist.destroy_process_group()
 

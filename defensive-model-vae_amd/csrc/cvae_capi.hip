@@ -75,6 +75,15 @@ struct cvae_handle {
   // sets it (system scope); the next training call reads it WITHOUT synchronising and fails
   unsigned* fault_host = nullptr;
   unsigned* fault_dev = nullptr;
+  // data-parallel peer exchange (cvae_peer.h): this rank's mailbox (uncached, IPC-exported) and
+  // every rank's arena / mailbox as mapped into this process
+  int px_world = 0, px_rank = 0;
+  char* px_mbox = nullptr;
+  int64_t px_mbox_bytes = 0, px_done_off = 0, px_inbox_off = 0;
+  char* px_arena[PX_MAX] = {};
+  char* px_mb[PX_MAX] = {};
+  bool px_ready = false;
+  uint64_t px_base = 0;
   bool fused = false;          // training steps run as one fused_step_kernel launch
   int64_t arena_bytes = 0;
   float* d_partials = nullptr;
@@ -983,6 +992,7 @@ int cvae_destroy(cvae_handle* h) {
   for (auto e : h->pool) (void)hipEventDestroy(e);
   if (h->arena) (void)hipFree(h->arena);
   if (h->fault_host) (void)hipHostFree(h->fault_host);
+  cvae_px_close(h);
   delete h;
   return CVAE_OK;
 }
@@ -1229,6 +1239,218 @@ int cvae_step_skip(cvae_handle* h, uint64_t* counters, const cvae_adam_config* a
                      adam->beta2);
   HIPCK(hipGetLastError());
   return CVAE_OK;
+}
+
+// ---------------------------------------------------------------- data parallel: peer exchange
+namespace {
+struct PxBlob {
+  int magic, world, rank, nt;
+  int64_t arena_bytes, mbox_bytes;
+  hipIpcMemHandle_t arena, mbox;
+};
+constexpr int PX_MAGIC = 0x43505831;  // "CPX1"
+int px_tiles(const cvae_handle*) { return fchain::Tiles<19>::total(); }
+// bound of every exchange wait: CVAE_PX_TIMEOUT_MS (default 2000 ms), in s_memrealtime ticks
+uint64_t px_timeout_ticks() {
+  const char* e = std::getenv("CVAE_PX_TIMEOUT_MS");
+  const double ms = e ? std::atof(e) : 2000.0;
+  return (uint64_t)(std::max(1.0, ms) * 1e5);
+}
+
+// set-up check of the mapping and the protocol's primitives: every rank stores a tagged word into
+// every peer's probe slot, releases it and counts one arrival there; then waits (bounded) for the
+// world − 1 arrivals in its own mailbox and checks every tag.  The probe area follows the done
+// counter: [done_off + 64] arrivals, [done_off + 128 + 8·r] rank r's tag.
+__global__ void px_probe_kernel(PeerArgs p, int* ok) {
+  if (threadIdx.x != 0) return;
+  const uint64_t tag = 0x5EED000000000000ull;
+  for (int r = 0; r < p.world; ++r) {
+    if (r == p.rank) continue;
+    char* pr = p.mbox[r] + p.done_off;
+    __hip_atomic_store((uint64_t*)(pr + 128) + p.rank, tag | (uint64_t)(p.rank + 1), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __hip_atomic_fetch_add((uint64_t*)(pr + 64), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  char* mine = p.mbox[p.rank] + p.done_off;
+  int good = px_wait((const uint64_t*)(mine + 64), (uint64_t)(p.world - 1), nullptr, p.timeout) ? 1 : 0;
+  for (int r = 0; r < p.world && good; ++r)
+    if (r != p.rank &&
+        __hip_atomic_load((const uint64_t*)(mine + 128) + r, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) !=
+            (tag | (uint64_t)(r + 1)))
+      good = 0;
+  *ok = good;
+}
+}  // namespace
+
+int cvae_px_blob_bytes(int64_t* bytes) {
+  if (!bytes) return fail(CVAE_E_INVALID, "null argument");
+  *bytes = (int64_t)sizeof(PxBlob);
+  return CVAE_OK;
+}
+
+int cvae_px_export(cvae_handle* h, int world, int rank, void* blob) {
+  if (!h || !blob) return fail(CVAE_E_INVALID, "null argument");
+  if (world < 2 || world > PX_MAX || rank < 0 || rank >= world)
+    return fail(CVAE_E_INVALID, "peer exchange: 2 <= world <= " + std::to_string(PX_MAX) + ", 0 <= rank < world");
+  if (h->fast_nki != 19 || !h->ring)
+    return fail(CVAE_E_INVALID, "peer exchange serves the reference architecture at seq_len 100, dim 6, bf16 "
+                                "(the ring chain and fastwgrad tiles); use the collective path otherwise");
+  cvae_px_close(h);
+  const int nt = px_tiles(h);
+  h->px_done_off = ((int64_t)nt * 8 + 255) / 256 * 256;
+  h->px_inbox_off = h->px_done_off + 512;  // done, probe words, statistics (cvae_peer.h)
+  h->px_mbox_bytes = h->px_inbox_off + (int64_t)nt * world * PX_PW * 4;
+  HIPCK(hipSetDevice(h->device));
+  HIPCK(hipExtMallocWithFlags((void**)&h->px_mbox, h->px_mbox_bytes, hipDeviceMallocUncached));
+  HIPCK(hipMemset(h->px_mbox, 0, h->px_mbox_bytes));
+  HIPCK(hipDeviceSynchronize());
+  PxBlob b{};
+  b.magic = PX_MAGIC; b.world = world; b.rank = rank; b.nt = nt;
+  b.arena_bytes = h->arena_bytes; b.mbox_bytes = h->px_mbox_bytes;
+  HIPCK(hipIpcGetMemHandle(&b.arena, h->arena));
+  HIPCK(hipIpcGetMemHandle(&b.mbox, h->px_mbox));
+  std::memcpy(blob, &b, sizeof(b));
+  h->px_world = world;
+  h->px_rank = rank;
+  h->px_ready = false;
+  return CVAE_OK;
+}
+
+int cvae_px_import(cvae_handle* h, const void* blobs, uint64_t base) {
+  if (!h || !blobs || !h->px_mbox) return fail(CVAE_E_INVALID, "peer exchange: export first");
+  const PxBlob* b = (const PxBlob*)blobs;
+  HIPCK(hipSetDevice(h->device));
+  for (int r = 0; r < h->px_world; ++r) {
+    if (b[r].magic != PX_MAGIC || b[r].world != h->px_world || b[r].rank != r || b[r].nt != px_tiles(h) ||
+        b[r].arena_bytes != h->arena_bytes || b[r].mbox_bytes != h->px_mbox_bytes)
+      return fail(CVAE_E_INVALID, "peer exchange: rank " + std::to_string(r) +
+                                      "'s blob does not match this configuration (same model, batch capacity, world)");
+    if (r == h->px_rank) {
+      h->px_arena[r] = h->arena;
+      h->px_mb[r] = h->px_mbox;
+      continue;
+    }
+    HIPCK(hipIpcOpenMemHandle((void**)&h->px_arena[r], b[r].arena, hipIpcMemLazyEnablePeerAccess));
+    HIPCK(hipIpcOpenMemHandle((void**)&h->px_mb[r], b[r].mbox, hipIpcMemLazyEnablePeerAccess));
+  }
+  h->px_base = base;
+  h->px_ready = true;
+  return CVAE_OK;
+}
+
+int cvae_px_probe(cvae_handle* h, int* ok) {
+  if (!h || !ok) return fail(CVAE_E_INVALID, "null argument");
+  if (!h->px_ready) return fail(CVAE_E_INVALID, "peer exchange not set up");
+  PeerArgs px{};
+  px.world = h->px_world;
+  px.rank = h->px_rank;
+  for (int r = 0; r < px.world; ++r) px.mbox[r] = h->px_mb[r];
+  px.done_off = h->px_done_off;
+  px.timeout = px_timeout_ticks();
+  int* d_ok = (int*)(h->fault_dev + 4);  // a spare word of the pinned fault page
+  h->fault_host[4] = 0;
+  hipLaunchKernelGGL(px_probe_kernel, dim3(1), dim3(64), 0, 0, px, d_ok);
+  HIPCK(hipGetLastError());
+  HIPCK(hipDeviceSynchronize());
+  *ok = (int)__atomic_load_n(h->fault_host + 4, __ATOMIC_ACQUIRE);
+  return CVAE_OK;
+}
+
+int cvae_px_stats(cvae_handle* h, uint64_t* out, int reset) {
+  if (!h || !out) return fail(CVAE_E_INVALID, "null argument");
+  if (!h->px_mbox) return fail(CVAE_E_INVALID, "peer exchange not set up");
+  char* st = h->px_mbox + h->px_done_off + PX_STATS_OFF;
+  HIPCK(hipDeviceSynchronize());
+  HIPCK(hipMemcpy(out, st, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  if (reset) {
+    HIPCK(hipMemset(st, 0, 4 * sizeof(uint64_t)));
+    HIPCK(hipDeviceSynchronize());
+  }
+  return CVAE_OK;
+}
+
+int cvae_px_close(cvae_handle* h) {
+  if (!h) return fail(CVAE_E_INVALID, "null handle");
+  for (int r = 0; r < PX_MAX; ++r) {
+    if (r != h->px_rank) {
+      if (h->px_arena[r]) (void)hipIpcCloseMemHandle(h->px_arena[r]);
+      if (h->px_mb[r]) (void)hipIpcCloseMemHandle(h->px_mb[r]);
+    }
+    h->px_arena[r] = h->px_mb[r] = nullptr;
+  }
+  if (h->px_mbox) (void)hipFree(h->px_mbox);
+  h->px_mbox = nullptr;
+  h->px_ready = false;
+  h->px_world = 0;
+  return CVAE_OK;
+}
+
+int cvae_px_owned(const cvae_handle* h, uint8_t* mask) {
+  if (!h || !mask) return fail(CVAE_E_INVALID, "null argument");
+  if (!h->px_world) return fail(CVAE_E_INVALID, "peer exchange not set up");
+  std::memset(mask, 0, (size_t)h->nparams);
+  const int nt = px_tiles(h);
+  for (int b = 0; b < nt; ++b) {
+    if (px_owner(b, h->px_world) != h->px_rank) continue;
+    const TileDesc td = fchain::Tiles<19>::at(b);
+    const LayerDev& L = h->net.L[td.layer];
+    for (int o = td.o0; o < td.o0 + 32 && o < L.N; ++o) {
+      const int seg = (L.nseg == 2 && o >= L.seg_rows0) ? 1 : 0;
+      const int orow = seg ? o - L.seg_rows0 : o;
+      for (int i = td.i0; i < td.i0 + 32 && i < L.K; ++i) mask[L.pw[seg] + (int64_t)orow * L.K + i] = 1;
+      if (td.i0 == 0) mask[L.pb[seg] + orow] = 1;
+    }
+  }
+  return CVAE_OK;
+}
+
+int cvae_px_train_step(cvae_handle* h, const void* x, const int64_t* idx, int batch, int xflags, const float* eps,
+                       uint64_t seed, int64_t eps_row0, const cvae_loss_weights* w, float* params, float* m, float* v,
+                       const cvae_adam_config* adam, const float* rank_scales, float* loss_out, double* loss_accum,
+                       uint64_t* counters, void* stream) {
+  if (!h || !params || !m || !v || !counters) return fail(CVAE_E_INVALID, "null argument");
+  if (!h->px_ready) return fail(CVAE_E_INVALID, "peer exchange not set up (cvae_px_export / cvae_px_import)");
+  if (batch < 0 || batch > h->cfg.max_batch) return fail(CVAE_E_CAPACITY, "batch out of range");
+  if (batch > 0 && !x) return fail(CVAE_E_INVALID, "null x");
+  int rc = check_adam(adam);
+  if (!rc) rc = check_fault(h);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  tbegin(h);
+  PeerArgs px{};
+  px.world = h->px_world;
+  px.rank = h->px_rank;
+  px.ragged = rank_scales ? 1 : 0;
+  for (int r = 0; r < px.world; ++r) {
+    px.c[r] = rank_scales ? rank_scales[r] : 0.f;
+    px.arena[r] = h->px_arena[r];
+    px.mbox[r] = h->px_mb[r];
+  }
+  const int nt = px_tiles(h);
+  int own = 0;
+  for (int b = 0; b < nt; ++b) own += px_owner(b, px.world) == px.rank;
+  px.n_remote = nt - own;
+  px.done_off = h->px_done_off;
+  px.inbox_off = h->px_inbox_off;
+  px.base = h->px_base;
+  px.fault = h->fault_dev;
+  px.timeout = px_timeout_ticks();
+  LossArgs la{};
+  if (batch > 0) {
+    CallX c{x, idx, nullptr, batch, xflags, eps, seed, 0, eps_row0, w, counters, adam};
+    const RowArgs ra = row_args(h, c);
+    if (!fast_ok(h, ra)) return fail(CVAE_E_INVALID, "peer exchange: x must be 16-B aligned operand-dtype rows");
+    if ((rc = launch_train_chain<__bf16>(h, ra, s))) return rc;
+    la = make_loss(h, ra, loss_out, loss_accum);
+  } else {  // no rows on this rank this step: the counters advance as a chain + dW launch would
+    hipLaunchKernelGGL(step_skip_kernel, dim3(1), dim3(1), 0, s, counters, adam->lr, adam->beta1, adam->beta2);
+    HIPCK(hipGetLastError());
+  }
+  const AdamArgs aa = make_adam(params, nullptr, m, v, 0, *adam, rank_scales ? 1.f : 1.f / (float)px.world, counters);
+  if ((rc = tmark(h, s, "px_wgrad"))) return rc;
+  return klaunch(h, fchain::px_wgrad_kernel<19>, dim3(nt + 1), dim3(WG_THREADS), 0, s, h->arena, params, m, v,
+                 h->net.Bp, bk_of(h, batch), h->net.S, h->net.D, h->net.I, aa, la, px);
 }
 
 int cvae_fault(const cvae_handle* h, unsigned* word) {

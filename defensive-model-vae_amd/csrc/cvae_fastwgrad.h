@@ -158,6 +158,42 @@ __global__ __launch_bounds__(WG_THREADS) void fastwgrad_kernel(char* arena, floa
     wgrad_body<__bf16, MODE, false, 1>(L, td, Bk, aa, la, false, fn.S, fn.D, Z, sh.red, sh.dbp, sk);
 }
 
+// ---------------------------------------------------------------- data parallel: the peer exchange
+// fastwgrad_kernel's tiles with cvae_peer.h's exchange: tile b is owned by rank b mod world (its
+// block runs the Adam epilogue and broadcasts the operand copies), every other rank's block for b
+// pushes its partial to the owner.  The last block finishes this rank's loss, then waits until
+// every tile the other ranks own has arrived (px.n_remote per step).  grid = tiles + 1.
+// Two workgroups per CU (4 waves per SIMD, <= 128 VGPRs): every block of the launch is resident at
+// once with room to spare, so waiting owner blocks can never hold the slots their pushers need —
+// also when several ranks share one GPU (tests/test_gpu_peer.py).
+template <int NKI>
+__global__ __launch_bounds__(WG_THREADS, 4) void px_wgrad_kernel(char* arena, float* params, float* mst, float* vst,
+                                                               int Bp, int Bk, int S, int D, int I, AdamArgs a,
+                                                               LossArgs la, PeerArgs px) {
+  const FastNet fn{arena, Bp, S, D, I};
+  AdamArgs aa = a;
+  aa.params = params;
+  aa.m = mst;
+  aa.v = vst;
+  constexpr int NTL = Tiles<NKI>::total();
+  if ((int)blockIdx.x == NTL) {
+    if (threadIdx.x < 64 && la.partials) finish_loss(la, fn.S, fn.D, Z);
+    if (threadIdx.x == 0)
+      px_wait(px_done(px, px.mbox[px.rank]), (uint64_t)px.n_remote * px_epoch(px, aa.ctr), px.fault, px.timeout, 3,
+              px_stats(px), 1);
+    return;
+  }
+  __shared__ __attribute__((aligned(16))) WgradLds<1> sh;
+  SplitK sk{1, 0, nullptr, nullptr, (int)blockIdx.x, 0};
+  const TileDesc td = Tiles<NKI>::at(sk.tile);
+  const LayerDev L = fast_layer<NKI>(td.layer, fn.arena, fn.Bp, fn.I);
+  static_assert(Tiles<NKI>::ni_max() == 1, "the exchange's partial is one 32 x 32 tile");
+  if (px_owner(sk.tile, px.world) == px.rank)  // block-uniform
+    wgrad_body<__bf16, PM_ADAM, false, 1>(L, td, Bk, aa, la, false, fn.S, fn.D, Z, sh.red, sh.dbp, sk, &px);
+  else
+    wgrad_body<__bf16, PM_GRAD, false, 1>(L, td, Bk, aa, la, false, fn.S, fn.D, Z, sh.red, sh.dbp, sk, &px);
+}
+
 // ---------------------------------------------------------------- the fused training step
 // One launch = the row chain (blocks 0 .. nchain-1) and every dW ⊕ Adam tile (blocks nchain ..).
 // The tiles are listed in the order their arena rows become final (chain_body's groups), so the

@@ -22,6 +22,7 @@
 // instead of 2-B element stores scattered over the fragment layout.
 #pragma once
 #include "cvae_device.h"
+#include "cvae_peer.h"
 
 enum { PM_GRAD = 0, PM_ADAM = 1, PM_PACK = 2 };
 
@@ -316,6 +317,28 @@ __device__ __forceinline__ void tile_epilogue(const LayerDev& L, int o0, int i0,
   WSTAMP(6);
 }
 
+// peer exchange (cvae_peer.h): after the owner's tile_epilogue, the same new operand copies (the
+// LDS image wt) and bias into every other rank's arena, released at system scope, then one arrival
+// on each of their done counters
+template <typename T, int NTHR>
+__device__ __forceinline__ void px_broadcast(const PeerArgs& p, const LayerDev& L, int o0, int i0, const float* wt) {
+  const int tid = threadIdx.x;
+  const float nb = (i0 == 0 && tid < 32 && o0 + tid < L.Np) ? L.bias[o0 + tid] : 0.f;  // this thread's own store
+  for (int r = 0; r < p.world; ++r) {
+    if (r == p.rank) continue;
+    const ptrdiff_t d = p.arena[r] - p.arena[p.rank];
+    LayerDev Lr = L;
+    Lr.Wf = (char*)L.Wf + d;
+    Lr.Wb = (char*)L.Wb + d;
+    store_operands<T, NTHR>(Lr, o0, i0, wt);
+    if (i0 == 0 && tid < 32 && o0 + tid < L.Np) *(float*)((char*)(L.bias + o0 + tid) + d) = nb;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __syncthreads();
+  if (tid < p.world && tid != p.rank)
+    __hip_atomic_fetch_add(px_done(p, p.mbox[tid]), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // called by one whole wave: lane-strided partial sums, then a fixed-order butterfly (deterministic).
 // SC1: the partials were handed over inside the launch (sc1 loads, fused_step_kernel).
 template <bool SC1 = false>
@@ -375,7 +398,8 @@ struct SplitK {
 template <typename T, int MODE, bool SC1 = false, int NI = 1>
 __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td, int Bk, AdamArgs aa,
                                            const LossArgs& la, bool loss_block, int S, int D, int Z,
-                                           float* red, float* dbp, SplitK sk = SplitK{1, 0, nullptr, nullptr, 0}) {
+                                           float* red, float* dbp, SplitK sk = SplitK{1, 0, nullptr, nullptr, 0},
+                                           const PeerArgs* px = nullptr) {
   using V = typename Op<T>::V;
   constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC;
   constexpr int NX = 2 * NI, TW = 32 * NI, LD = TW + 4;  // X fragments per chunk, tile width, image stride
@@ -498,6 +522,18 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
 #pragma unroll
     for (int w = 0; w < WG_NW; ++w) db += dbp[w * 32 + tid];
   }
+  if (px) {  // peer exchange (cvae_peer.h): PM_GRAD = a non-owner's tile, PM_ADAM = the owner's
+    if (MODE == PM_GRAD) {
+      px_push(*px, sk.tile, o, iv, g4, db, bias_tile);
+      return;
+    }
+    __syncthreads();  // every wave has read red (g4): dbp[0] becomes the wait flag
+    if (!px_gather(*px, aa.ctr, sk.tile, o, iv, g4, db, bias_tile, (int*)dbp)) return;
+    if (!px->ragged) {
+      g4 = g4 * aa.grad_scale;
+      db = db * aa.grad_scale;
+    }
+  }
   if (sk.S > 1) {  // split-K: publish this split's partial; the last of the S blocks finishes the tile
     const int PW = sk.pw ? sk.pw : 32 * TW + 32;
     static_assert(EPT == 2 || EPT == 4, "partial vectors of 8 or 16 B");
@@ -550,6 +586,7 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
   }
   __syncthreads();  // red becomes the image of the new weights
   tile_epilogue<T, MODE, WG_THREADS, EPT, NI>(L, td.o0, td.i0, st, sb, g4, db, aa, red);
+  if (MODE == PM_ADAM && px) px_broadcast<T, WG_THREADS>(*px, L, td.o0, td.i0, red);
 #if CVAE_DIAG_STAMPS
   __syncthreads();
   WSTAMP(3);

@@ -74,6 +74,16 @@ _SIGS = {
     "cvae_fault": (_i, [_v, C.POINTER(C.c_uint)]),
     "cvae_clear_fault": (_i, [_v]),
     "cvae_step_skip": (_i, [_v, _v, _A, _v]),  # h, counters, adam, stream
+    "cvae_px_blob_bytes": (_i, [c_i64p]),
+    "cvae_px_export": (_i, [_v, _i, _i, _v]),  # h, world, rank, blob
+    "cvae_px_import": (_i, [_v, _v, _u64]),    # h, blobs, base
+    "cvae_px_owned": (_i, [_v, _v]),           # h, mask (host uint8[n_params])
+    "cvae_px_probe": (_i, [_v, C.POINTER(_i)]),
+    "cvae_px_close": (_i, [_v]),
+    "cvae_px_stats": (_i, [_v, C.POINTER(C.c_uint64), _i]),
+    # h, x, idx, batch, xflags, eps, seed, eps_row0, w, params, m, v, adam, rank_scales, loss_out, loss_accum,
+    # counters, stream
+    "cvae_px_train_step": (_i, [_v, _v, _v, _i, _i, _v, _u64, _i64, _W, _v, _v, _v, _A, _v, _v, _v, _v, _v]),
     "cvae_loss": (_i, [_v, _v, _v, _v, _i, _i, _i, _i, _W, _v, _v, _v]),
     "cvae_loss_backward": (_i, [_v, _v, _v, _v, _i, _i, _i, _i, _W, _v, _v, _v, _v, _v]),
     "cvae_adam_scalars": (_i, [_A, _i64, _v, _v]),

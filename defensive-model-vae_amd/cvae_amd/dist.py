@@ -72,7 +72,7 @@ class DataParallelStep:
     ``buckets``: 1 = one all-reduce after the whole dW launch; 2 = decoder bucket overlapped with
     the rest of the dW GEMMs (see the module docstring)."""
 
-    def __init__(self, engine, group=None, force_split=False, buckets=1):
+    def __init__(self, engine, group=None, force_split=False, buckets=1, exchange="rccl"):
         self.engine = engine
         self.group = group
         self.rank, self.world_size = world()
@@ -82,6 +82,26 @@ class DataParallelStep:
         if buckets not in (1, 2):
             raise ValueError("buckets must be 1 or 2")
         self.buckets = buckets
+        # exchange: "rccl" = all-reduce of the flat gradient, then Adam; "peer" = the in-kernel
+        # exchange over IPC-mapped peer memory (cvae_amd.peer); "auto" = peer where it serves the
+        # configuration and its set-up probe passes, else rccl.  self.exchange says which runs.
+        self.px = None
+        self.exchange = "rccl"
+        self.exchange_note = ""
+        if exchange not in ("rccl", "peer", "auto"):
+            raise ValueError("exchange must be 'rccl', 'peer' or 'auto'")
+        if exchange != "rccl" and self.world_size > 1:
+            try:
+                from .peer import PeerExchange
+                if getattr(engine, "train_kernel", None) != "ring":
+                    raise ValueError(f"the peer exchange serves the ring chain, this engine runs "
+                                     f"{getattr(engine, 'train_kernel', None)!r}")
+                self.px = PeerExchange(engine, group)
+                self.exchange = "peer"
+            except Exception as e:  # noqa: BLE001 — "auto" falls back, "peer" re-raises
+                if exchange == "peer":
+                    raise
+                self.exchange_note = f"peer exchange unavailable ({type(e).__name__}: {e}); rccl"
 
     @property
     def split(self):
@@ -104,6 +124,11 @@ class DataParallelStep:
             global_batch = batch * self.world_size
         if row0 is None:
             row0 = self.rank * batch
+        if self.px is not None:
+            if classes is not None:
+                raise ValueError("the peer exchange serves the reference model (no class embedding)")
+            return self.px.step(x, idx=idx, eps=eps, batch=batch, global_batch=global_batch, weights=weights,
+                                row0=row0)
         if not self.split:
             if batch > 0:
                 eng.train_step(x, idx=idx, eps=eps, batch=batch, weights=weights, row0=row0,
@@ -139,6 +164,17 @@ class DataParallelStep:
             dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group)
         eng.adam_step(grad_scale=scale)
         return eng.loss
+
+    def sync_state(self):
+        """Whole parameters and Adam moments on every rank (the peer exchange keeps each element
+        current on its owner only); a no-op for the all-reduce path, where every rank holds all."""
+        if self.px is not None:
+            self.px.gather_state()
+
+    def close(self):
+        if self.px is not None:
+            self.px.close()
+            self.px = None
 
     def epoch_loss_sums(self):
         """Σ over ranks of the device Σ loss·batch accumulators (5 doubles); resets them."""

@@ -1,0 +1,170 @@
+"""The data-parallel exchange over xGMI without a collective library (include/cvae.h cvae_px_*,
+csrc/cvae_peer.h; SURVEY §8e — the gradient exchange the reference's single process never needs,
+Training_VAE.py:362-363 across ranks).
+
+One process per GPU.  At set-up every rank exports its workspace and an uncached mailbox through
+HIP IPC, the descriptors are all-gathered over the process group (any backend: gloo or RCCL) and
+every rank maps every other rank's buffers.  From then on a training step is two launches per
+rank — the row chain on its rows, and the weight-gradient launch that pushes each dW tile's fp32
+partial to the tile's owner (rank = tile mod world), lets the owner sum the partials in rank
+order and apply Adam, and has the owner write the new operand copies into every rank's
+workspace.  No collective call, no host synchronisation, no per-step host values (the step's
+epoch is the device counter), so steps replay from a hipGraph as well.
+
+State ownership: the fp32 master parameters and Adam moments of a weight are current only on the
+rank owning its tile; ``gather_state`` (masked sum over the group: exact, one non-zero term per
+element) makes them whole on every rank — before a checkpoint, a state_dict, the end of training.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+import torch.distributed as dist
+
+from ._lib import CVAE_X_OPERAND, check, lib, ptr
+
+
+class PeerExchange:
+    def __init__(self, engine, group=None, probe=True):
+        """Collective over the group: every rank constructs it together.  A failure on any rank
+        (export, import, the probe) is agreed on by all ranks before anyone raises, so no rank
+        is left waiting in a collective the others skipped."""
+        self.engine = engine
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self._open = False
+        if self.world < 2:
+            raise ValueError("the peer exchange needs world >= 2 (one GPU trains with the fused step)")
+        h = engine._h
+
+        def agree(ok, what):
+            oks = [None] * self.world
+            dist.all_gather_object(oks, ok, group=group)
+            bad = [r for r, v in enumerate(oks) if v is not True]
+            if bad:
+                lib().cvae_px_close(h)
+                raise RuntimeError(f"peer exchange {what} failed on ranks {bad}: "
+                                   f"{[oks[r] for r in bad][:2]}")
+
+        blob = b""
+        try:
+            n = C.c_int64()
+            check(lib().cvae_px_blob_bytes(C.byref(n)))
+            buf = (C.c_char * n.value)()
+            check(lib().cvae_px_export(h, self.world, self.rank, buf), "cvae_px_export")
+            blob, ok = bytes(buf), True
+        except Exception as e:  # noqa: BLE001
+            ok = f"{type(e).__name__}: {e}"
+        agree(ok, "export")
+        blobs = [None] * self.world
+        dist.all_gather_object(blobs, blob, group=group)
+        # the step epoch is counted from here: every rank must be at the same optimizer step
+        base = engine.sync_counters()[1]
+        steps = [None] * self.world
+        dist.all_gather_object(steps, base, group=group)
+        agree(True if len(set(steps)) == 1 else f"optimizer steps differ {steps}", "set-up")
+        try:
+            allb = b"".join(blobs)
+            cbuf = (C.c_char * len(allb)).from_buffer_copy(allb)
+            check(lib().cvae_px_import(h, cbuf, int(base)), "cvae_px_import")
+            ok = True
+        except Exception as e:  # noqa: BLE001
+            ok = f"{type(e).__name__}: {e}"
+        agree(ok, "import")
+        dist.barrier(group=group)  # every mailbox is zeroed and mapped before anyone stores into it
+        if probe:
+            try:
+                good = C.c_int()
+                check(lib().cvae_px_probe(h, C.byref(good)), "cvae_px_probe")
+                ok = True if good.value == 1 else "tags did not arrive"
+            except Exception as e:  # noqa: BLE001
+                ok = f"{type(e).__name__}: {e}"
+            agree(ok, "probe")
+        mask = (C.c_uint8 * engine.n_params)()
+        check(lib().cvae_px_owned(h, mask), "cvae_px_owned")
+        self.owned = torch.frombuffer(bytearray(mask), dtype=torch.uint8).to(engine.device).bool()
+        self._open = True
+
+    def step(self, x, idx=None, eps=None, batch=None, global_batch=None, weights=None, row0=None, accumulate=True):
+        """One data-parallel step: this rank's ``batch`` rows (0 allowed) of a global batch."""
+        eng = self.engine
+        if batch is None:
+            batch = idx.numel() if idx is not None else x.shape[0]
+        batch = int(batch)
+        if global_batch is None:
+            global_batch = batch * self.world
+        if row0 is None:
+            row0 = self.rank * batch
+        scales = None
+        if batch * self.world != global_batch:  # ragged: every rank needs every rank's weight
+            sizes = [None] * self.world
+            dist.all_gather_object(sizes, batch, group=self.group)
+            scales = (C.c_float * self.world)(*[s / global_batch for s in sizes])
+        xp = idxp = ep = None
+        xfl = CVAE_X_OPERAND
+        if batch > 0:
+            x, idx, batch = eng._prep(x, idx, batch)
+            xp, idxp, xfl = ptr(x), ptr(idx), eng._xflags(x)
+            e = eng._eps(eps, batch)
+            ep = ptr(e)
+        eng.ensure_packed()
+        check(lib().cvae_px_train_step(
+            eng._h, xp, idxp, batch, xfl, ep, eng.seed, int(row0), C.byref(eng._weights(weights)), ptr(eng.params),
+            ptr(eng.m), ptr(eng.v), C.byref(eng._adam()), scales, ptr(eng.loss),
+            ptr(eng.loss_accum) if accumulate else None, ptr(eng.counters), eng._stream()), "cvae_px_train_step")
+        eng._ctr[0] += 1
+        eng._ctr[1] += 1
+        return eng.loss
+
+    def prepare(self, x, batch):
+        """``run(k)``: k equal-share steps on rows 0..batch-1 of the resident ``x``, Philox eps
+        (bench.py's timed call: every argument converted once)."""
+        eng = self.engine
+        x = eng.as_input(x)
+        B = int(batch)
+        eng._check_rows(x, None, B)
+        eng.ensure_packed()
+        f = lib().cvae_px_train_step
+        w, a = eng._weights(None), eng._adam()
+        args = (eng._h, C.c_void_p(x.data_ptr()), None, C.c_int(B), C.c_int(eng._xflags(x)), None,
+                C.c_uint64(eng.seed), C.c_int64(self.rank * B), C.byref(w), ptr(eng.params), ptr(eng.m),
+                ptr(eng.v), C.byref(a), None, ptr(eng.loss), ptr(eng.loss_accum), ptr(eng.counters), eng._stream())
+        ctr = eng._ctr
+
+        def run(k, _f=f, _args=args, _keep=(x, w, a), _ctr=ctr):
+            for _ in range(k):
+                rc = _f(*_args)
+                if rc < 0:
+                    check(rc, "cvae_px_train_step")
+            _ctr[0] += k
+            _ctr[1] += k
+        return run
+
+    def stats(self, reset=False):
+        """This rank's exchange waits (cvae_px_stats), in microseconds: the longest owner-tile
+        wait for the partials, the longest end-of-launch wait, the mean owner-tile wait."""
+        out = (C.c_uint64 * 4)()
+        check(lib().cvae_px_stats(self.engine._h, out, 1 if reset else 0), "cvae_px_stats")
+        return {"owner_wait_max_us": out[0] / 100.0, "end_wait_max_us": out[1] / 100.0,
+                "owner_wait_mean_us": out[2] / 100.0 / max(out[3], 1), "owner_waits": int(out[3])}
+
+    def gather_state(self):
+        """Whole fp32 params / Adam moments on every rank (each element from its owner), and the
+        operand copies repacked from them."""
+        eng = self.engine
+        with torch.no_grad():
+            for t in (eng.params, eng.m, eng.v):
+                t.copy_(torch.where(self.owned, t, torch.zeros_like(t)))
+                dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        eng.pack()
+
+    def close(self):
+        """Unmap the peers and free the mailbox; every rank calls it (it barriers first)."""
+        if not self._open:
+            return
+        torch.cuda.synchronize(self.engine.device)
+        dist.barrier(group=self.group)
+        lib().cvae_px_close(self.engine._h)
+        self._open = False

@@ -105,7 +105,7 @@ def save_checkpoint(path, model, eng, epoch, loss_history):
 def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidden_dim=128,
           weights=(0.1, 0.1, 1.0, 1.0), model_save_path=None, loss_save_path=None, dtype="fp32",
           eps="host", device=None, seed=None, engine_seed=0, log=print, model=None, buckets=1,
-          checkpoint_path=None, resume=None, classes=None, class_dim=0):
+          checkpoint_path=None, resume=None, classes=None, class_dim=0, exchange="auto"):
     """Train like ``python Training_VAE.py`` (mode='training').
 
     data: path to the (N, seq_len, dim) ``.npy`` (TrajectoryDataset, :105-115) or an array; or a
@@ -116,8 +116,10 @@ def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidd
     weights: (recon, kld, start, time) — the values of :300-306.
     seed: if given, ``torch.manual_seed(seed)`` first (the reference leaves it unseeded).
     Under ``torch.distributed`` every rank runs this with the same arguments; batch_size is
-    then per rank (global batch = batch_size · world) and rank 0 logs and saves; ``buckets=2``
-    overlaps the decoder gradients' all-reduce with the rest of the dW GEMMs.
+    then per rank (global batch = batch_size · world) and rank 0 logs and saves; ``exchange``
+    picks the gradient exchange ("auto": the in-kernel peer exchange where the configuration has
+    it — cvae_amd.peer — else the RCCL all-reduce; "rccl"; "peer"); ``buckets=2`` overlaps the
+    decoder gradients' all-reduce with the rest of the dW GEMMs (rccl).
 
     checkpoint_path: write a resume point (save_checkpoint) after every epoch; resume: continue
     from one — ``epochs`` counts the total, so train(epochs=4, resume=ckpt_after_2) runs epochs 3-4
@@ -157,7 +159,7 @@ def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidd
     eng.set_optimizer(lr=lr)
     eng.weights = tuple(float(w) for w in weights)
     eng.keep_f32 = True                                   # relative transform in fp32 (see above)
-    step = dp.DataParallelStep(eng, buckets=buckets)
+    step = dp.DataParallelStep(eng, buckets=buckets, exchange="rccl" if classes is not None else exchange)
     step.broadcast_params()
     x_dev = eng.as_input(torch.from_numpy(arr), keep_f32=True)  # resident for the whole run
     cls_dev = None if classes is None else torch.from_numpy(classes).to(x_dev.device)
@@ -195,8 +197,12 @@ def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidd
             loss_history[k].append(float(v))
         if rank == 0 and log:
             log(epoch_line(epoch, means))
-        if rank == 0 and checkpoint_path:
-            save_checkpoint(checkpoint_path, model, eng, epoch + 1, loss_history)
+        if checkpoint_path:
+            step.sync_state()  # every rank (a collective under the peer exchange)
+            if rank == 0:
+                save_checkpoint(checkpoint_path, model, eng, epoch + 1, loss_history)
+    step.sync_state()
+    step.close()
     weighted = weighted_history(loss_history, weights)
     if rank == 0:
         if loss_save_path:

@@ -296,6 +296,46 @@ int cvae_sync_words(cvae_handle* h, unsigned* out);
 int cvae_fault(const cvae_handle* h, unsigned* word);
 int cvae_clear_fault(cvae_handle* h);
 
+/* ---- Data parallelism over xGMI without a collective library (Training_VAE.py:362-363
+ * across ranks): the "peer exchange".  One process per GPU; every rank's workspace and a mailbox
+ * are mapped into every other rank through HIP IPC, and the weight-gradient launch of each step
+ * does dW ⊕ reduce-scatter ⊕ Adam ⊕ all-gather itself: tile t of the padded weights is owned by
+ * rank t mod world, the other ranks push their fp32 partial of t into the owner's mailbox, the
+ * owner sums the world partials in rank order, applies Adam to its fp32 master state and writes
+ * the new operand copies into every rank's workspace.  Serves the reference architecture at
+ * seq_len 100, dim 6, bf16 (cvae_train_kernel == CVAE_KERNEL_RING).
+ *   cvae_px_blob_bytes: size of one rank's exchange descriptor (handle-free).
+ *   cvae_px_export: allocate this rank's mailbox (zeroed) and write its descriptor to `blob`.
+ *   cvae_px_import: `blobs` = the world descriptors in rank order (all-gathered by the caller, who
+ *     must also barrier after every rank's import and before any rank's first step); `base` =
+ *     counters[1] at this point, the same on every rank.
+ *   cvae_px_train_step: one training step of this rank's rows (batch may be 0: an empty share of
+ *     a ragged global batch), the exchange included; rank_scales = host float[world] of
+ *     B_r / B_global for a ragged batch, NULL for equal shares (gradient = sum / world).  Every
+ *     rank must call it for every step.  Master parameters and moments are current on the OWNER
+ *     of each element only (cvae_px_owned: host uint8[n_params] mask of this rank's elements);
+ *     the caller gathers them (e.g. masked sum across ranks) before reading them.
+ *   cvae_px_close: unmap the peers and free the mailbox (after a barrier). */
+int cvae_px_blob_bytes(int64_t* bytes);
+int cvae_px_export(cvae_handle* h, int world, int rank, void* blob);
+int cvae_px_import(cvae_handle* h, const void* blobs, uint64_t base);
+int cvae_px_owned(const cvae_handle* h, uint8_t* mask);
+int cvae_px_train_step(cvae_handle* h, const void* x, const int64_t* idx, int batch, int xflags, const float* eps,
+                       uint64_t seed, int64_t eps_row0, const cvae_loss_weights* w, float* params, float* m, float* v,
+                       const cvae_adam_config* adam, const float* rank_scales, float* loss_out, double* loss_accum,
+                       uint64_t* counters, void* stream);
+int cvae_px_close(cvae_handle* h);
+/* Set-up check after cvae_px_import (every rank calls it once, concurrently): each rank stores a
+ * tagged word into every peer's mailbox and waits (bounded, ~1 s) for theirs; *ok = 1 when every
+ * peer's tag arrived intact.  Synchronises the device. */
+int cvae_px_probe(cvae_handle* h, int* ok);
+/* This rank's exchange wait statistics since set-up or the last reset, in 10-ns ticks: out[0] the
+ * longest owner-tile wait for the other ranks' partials, out[1] the longest end-of-launch wait for
+ * the other owners' operand copies, out[2] the sum and out[3] the number of owner-tile waits.
+ * Every wait is bounded by CVAE_PX_TIMEOUT_MS (default 2000); a time-out sets the fault word to 2
+ * (owner tile) or 3 (end of launch).  Synchronises the device. */
+int cvae_px_stats(cvae_handle* h, uint64_t* out, int reset);
+
 /* A data-parallel step in which this rank has no rows (a ragged last global batch shorter than the
  * world): advances the device counters exactly as a training step's launches would — counters[1]
  * += 1 with that step's Adam scalars, counters[0] += 1 — so the rank's following cvae_adam uses the

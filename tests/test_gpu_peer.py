@@ -1,0 +1,134 @@
+"""The data-parallel peer exchange (include/cvae.h cvae_px_*, csrc/cvae_peer.h, cvae_amd.peer) on
+the GPU, with several ranks on this box's ONE GPU: every rank is its own process holding its own
+engine, workspace and IPC-exported mailbox, and the ranks reach each other's buffers through the
+same IPC mappings they use across GPUs (the protocol — pushes, system-scope flags, owner-side
+Adam, broadcast of the operand copies — is identical; only the link differs).
+
+Oracle: the split data-parallel step computed in ONE process from the same kernels — each rank's
+forward_backward on its rows (eps keyed by its global rows, the same Philox offset), the partial
+gradients weighted and summed in rank order, then cvae_adam — which is what the exchange must
+produce.  Params, moments and device counters must equal it BIT FOR BIT; the loss accumulators
+(fp64 sums over ranks in another order) to 1e-12.  Cases: equal shares (world 2 and 4), a ragged
+global batch, and an empty share (world 3, a rank with no rows).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+S, D, Z = 100, 6, 8
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _data(n):
+    return torch.randn(n, S, D, generator=torch.Generator().manual_seed(21))
+
+
+def _model():
+    import cvae_amd
+    torch.manual_seed(0)
+    m = cvae_amd.ConditionalTrajectoryVAE(S, D, Z)
+    return m, m.attach(dtype="bf16", max_batch=256, device="cuda:0", seed=4321)
+
+
+def _worker(rank, world, port, sizes, steps, out):
+    import torch.distributed as dist
+    from cvae_amd.dist import DataParallelStep
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    # ranks sharing one GPU are scheduled by the GPU's process scheduler, which can hold one
+    # rank's queue off the GPU for milliseconds to seconds: a longer bound than the 2 s default
+    # (one rank per GPU); a protocol deadlock still fails the test
+    os.environ["CVAE_PX_TIMEOUT_MS"] = "30000"
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        m, eng = _model()
+        gb = sum(sizes)
+        lo = sum(sizes[:rank])
+        x = eng.as_input(_data(gb)[lo:lo + max(sizes[rank], 1)])
+        dp = DataParallelStep(eng, exchange="peer")
+        assert dp.exchange == "peer"
+        for _ in range(steps):
+            dp.step(x, batch=sizes[rank], global_batch=gb, row0=lo)
+        torch.cuda.synchronize()
+        fault = eng.fault()
+        print(f"rank {rank}: fault {fault}, waits {dp.px.stats()}", flush=True)
+        dp.sync_state()
+        acc = dp.epoch_loss_sums()
+        torch.cuda.synchronize()
+        if rank == 0:
+            torch.save({"params": eng.params.cpu(), "m": eng.m.cpu(), "v": eng.v.cpu(),
+                        "counters": eng.counters.cpu(), "acc": acc.cpu(), "fault": fault}, out)
+        dp.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def _reference(sizes, steps):
+    """One process: per step, every rank's forward_backward at the step's Philox offset, partial
+    gradients weighted (ragged) and summed in rank order, then Adam."""
+    m, eng = _model()
+    gb = sum(sizes)
+    world = len(sizes)
+    xs = _data(gb)
+    ragged = any(s != sizes[0] for s in sizes)
+    acc = torch.zeros(5, dtype=torch.float64, device="cuda:0")
+    for _ in range(steps):
+        off, st = eng._ctr
+        total = None
+        lo = 0
+        for r, b in enumerate(sizes):
+            eng.rng_offset, eng.step_count = off, st
+            if b > 0:
+                eng.loss_accum.zero_()
+                eng.forward_backward(eng.as_input(xs[lo:lo + b]), batch=b, row0=lo)
+                acc += eng.loss_accum
+                g = eng.grads.clone()
+            else:
+                g = torch.zeros_like(eng.grads)
+            if ragged:
+                g = g * (b / gb)
+            total = g if total is None else total + g
+            lo += b
+        eng.rng_offset, eng.step_count = off + 1, st + 1
+        eng.grads.copy_(total)
+        eng.adam_step(grad_scale=1.0 if ragged else 1.0 / world)
+    torch.cuda.synchronize()
+    return {"params": eng.params.cpu(), "m": eng.m.cpu(), "v": eng.v.cpu(), "counters": eng.counters.cpu(),
+            "acc": acc.cpu()}
+
+
+@pytest.mark.parametrize("sizes", [(64, 64), (64, 64, 64, 64), (96, 32), (40, 24, 0)],
+                         ids=["w2", "w4", "ragged", "empty-share"])
+def test_peer_exchange_equals_split_step(sizes, tmp_path):
+    """world ranks on one GPU through the in-kernel exchange == the split data-parallel step of
+    the same partial gradients in one process, bit for bit, after 3 steps."""
+    steps = 3
+    out = str(tmp_path / "r0.pt")
+    ctx = mp.get_context("spawn")
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, len(sizes), port, sizes, steps, out)) for r in range(len(sizes))]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert codes == [0] * len(sizes), codes
+    got = torch.load(out, weights_only=True)
+    assert got["fault"] == 0
+    ref = _reference(sizes, steps)
+    for k in ("params", "m", "v", "counters"):
+        assert torch.equal(got[k], ref[k]), (k, float((got[k].double() - ref[k].double()).abs().max()))
+    np.testing.assert_allclose(got["acc"].numpy(), ref["acc"].numpy(), rtol=1e-12)
