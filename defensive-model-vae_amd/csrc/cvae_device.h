@@ -184,6 +184,31 @@ __device__ __forceinline__ V gld(const void* p) { return *(const CVAE_GLOBAL V*)
 template <typename V>
 __device__ __forceinline__ void gst(void* p, V v) { *(CVAE_GLOBAL V*)p = v; }
 
+// Store of the dW ⊕ Adam epilogue (master state, operand copies).  CVAE_WT_STORES=1 makes it a
+// write-through buffer store (sc1 cache policy = aux 16 on gfx950: the line leaves the XCD's L2 now
+// instead of in the kernel-end writeback) — measured slower (dW 8.2-8.3 vs 7.7-7.9 µs, round 3,
+// profiles/r03d), so the default is the plain global store.  `base` must be wave-uniform (it
+// becomes the buffer resource); the byte offset is per lane and below 2^31.
+#ifndef CVAE_WT_STORES
+#define CVAE_WT_STORES 0
+#endif
+template <typename V>
+__device__ __forceinline__ void st_wt(void* base, size_t byte_off, V v) {
+  if (!CVAE_WT_STORES) {
+    gst<V>((char*)base + byte_off, v);
+    return;
+  }
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
+  static_assert(sizeof(V) == 16 || sizeof(V) == 8 || sizeof(V) == 4, "16, 8 or 4 bytes");
+  typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+  if constexpr (sizeof(V) == 16)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)byte_off, 0, 16);
+  else if constexpr (sizeof(V) == 8)
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, (int)byte_off, 0, 16);
+  else
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)byte_off, 0, 16);
+}
+
 // ------------------------------------------------------------------ Adam step scalars (device step counters)
 // torch's two per-step Adam scalars from the step count t, in doubles as Python forms them
 // (torch/optim/adam.py: bias_correction1 = 1 - beta1 ** step, step_size = lr / bias_correction1,

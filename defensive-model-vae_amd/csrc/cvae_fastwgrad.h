@@ -130,6 +130,16 @@ __host__ __device__ inline LayerDev fast_layer(int l, char* arena, int Bp, int I
   return L;
 }
 
+// The tile and its layer record (compile-time decode: scalar selects, no memory round trip).
+// Measured alternative (round 3): wave 0 decodes and broadcasts the record through LDS +
+// readfirstlane, cutting the kernel's SALU instructions ~8x — no faster (dW 7.8 vs 7.7-7.9 µs,
+// profiles/r03d): the scalar issue is not what the tiles wait on.
+template <int NKI>
+__device__ __forceinline__ void decode_tile(int tile, char* arena, int Bp, int I, TileDesc& td, LayerDev& L) {
+  td = Tiles<NKI>::at(tile);
+  L = fast_layer<NKI>(td.layer, arena, Bp, I);
+}
+
 // Scalars first (SGPR-preloaded at wave launch, as fastchain_kernel's): the arena and master-state
 // pointers every first load needs.
 // grid = total tiles × sk.S + 1 (split-major; the last block finishes the loss)
@@ -150,8 +160,9 @@ __global__ __launch_bounds__(WG_THREADS) void fastwgrad_kernel(char* arena, floa
   __shared__ __attribute__((aligned(16))) WgradLds<Tiles<NKI>::ni_max()> sh;
   sk.s = blockIdx.x / NTL;
   sk.tile = blockIdx.x - sk.s * NTL;
-  const TileDesc td = Tiles<NKI>::at(sk.tile);
-  const LayerDev L = fast_layer<NKI>(td.layer, fn.arena, fn.Bp, fn.I);
+  TileDesc td;
+  LayerDev L;
+  decode_tile<NKI>(sk.tile, fn.arena, fn.Bp, fn.I, td, L);
   if (Tiles<NKI>::ni(td.layer) == 2)  // block-uniform
     wgrad_body<__bf16, MODE, false, 2>(L, td, Bk, aa, la, false, fn.S, fn.D, Z, sh.red, sh.dbp, sk);
   else
@@ -185,8 +196,9 @@ __global__ __launch_bounds__(WG_THREADS, 4) void px_wgrad_kernel(char* arena, fl
   }
   __shared__ __attribute__((aligned(16))) WgradLds<1> sh;
   SplitK sk{1, 0, nullptr, nullptr, (int)blockIdx.x, 0};
-  const TileDesc td = Tiles<NKI>::at(sk.tile);
-  const LayerDev L = fast_layer<NKI>(td.layer, fn.arena, fn.Bp, fn.I);
+  TileDesc td;
+  LayerDev L;
+  decode_tile<NKI>(sk.tile, fn.arena, fn.Bp, fn.I, td, L);
   static_assert(Tiles<NKI>::ni_max() == 1, "the exchange's partial is one 32 x 32 tile");
   if (px_owner(sk.tile, px.world) == px.rank)  // block-uniform
     wgrad_body<__bf16, PM_ADAM, false, 1>(L, td, Bk, aa, la, false, fn.S, fn.D, Z, sh.red, sh.dbp, sk, &px);

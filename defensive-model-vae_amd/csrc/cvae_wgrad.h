@@ -189,9 +189,9 @@ __device__ __forceinline__ typename VecF<EPT>::T applyn(PreN<EPT> s, typename Ve
           mv[c] = s.m[c];
           vv[c] = s.v[c];
         }
-        *(V*)(a.params + s.base) = pv;
-        *(V*)(a.m + s.base) = mv;
-        *(V*)(a.v + s.base) = vv;
+        st_wt(a.params, (size_t)s.base * 4, pv);
+        st_wt(a.m, (size_t)s.base * 4, mv);
+        st_wt(a.v, (size_t)s.base * 4, vv);
       }
     } else {
 #pragma unroll
@@ -228,24 +228,26 @@ __device__ __forceinline__ PreB loadb(const LayerDev& L, int o, const AdamArgs& 
   }
   return b;
 }
+// returns the padded bias value written to L.bias (the peer exchange broadcasts it)
 template <int MODE>
-__device__ __forceinline__ void apply_bias(const LayerDev& L, int o, PreB b, float g, const AdamArgs& a) {
-  if (o >= L.Np) return;
+__device__ __forceinline__ float apply_bias(const LayerDev& L, int o, PreB b, float g, const AdamArgs& a) {
+  if (o >= L.Np) return 0.f;
   float w = 0.f;
   if (b.idx >= 0) {
-    if (MODE == PM_GRAD) { a.grads[b.idx] = g; return; }
+    if (MODE == PM_GRAD) { a.grads[b.idx] = g; return 0.f; }
     w = b.p;
     if (MODE == PM_ADAM) {
       w = adam_math(w, g, b.m, b.v, a);
-      a.params[b.idx] = w;
-      a.m[b.idx] = b.m;
-      a.v[b.idx] = b.v;
+      st_wt(a.params, (size_t)b.idx * 4, w);
+      st_wt(a.m, (size_t)b.idx * 4, b.m);
+      st_wt(a.v, (size_t)b.idx * 4, b.v);
     }
   } else if (MODE == PM_GRAD) {
-    return;
+    return 0.f;
   }
-  if (CVAE_DIAG_NOWPACK && MODE == PM_ADAM) return;
-  L.bias[o] = w;
+  if (CVAE_DIAG_NOWPACK && MODE == PM_ADAM) return w;
+  st_wt(L.bias, (size_t)o * 4, w);
+  return w;
 }
 
 // Both operand copies of one 32×32 tile from its LDS image, as whole MFMA fragments.  Fragment
@@ -270,7 +272,7 @@ __device__ __forceinline__ void store_operands(const LayerDev& L, int o0, int i0
     if (wb) {  // Wb = Wᵀ: rows = inputs i, K = outputs o
 #pragma unroll
       for (int e = 0; e < EPL; ++e) val[e] = to_t<T>(wt[(kl + frag_k<T>(q, e)) * LD + nl]);
-      gst<V>((T*)L.Wb + ((size_t)(((i0 >> 4) + bt) * (L.Np / KC) + (o0 + kl) / KC) * 64 + ln) * EPL, val);
+      st_wt(L.Wb, ((size_t)(((i0 >> 4) + bt) * (L.Np / KC) + (o0 + kl) / KC) * 64 + ln) * EPL * sizeof(T), val);
     } else if (EPL == 8 && L.f8) {  // CVAE_FP8: e4m3(s·W), 8 B per lane into its K-pair fragment
       const float sc = f8_header(L.Wf)->s;
       float f[8];
@@ -288,7 +290,7 @@ __device__ __forceinline__ void store_operands(const LayerDev& L, int o0, int i0
 #pragma unroll
         for (int c = 0; c < 4; ++c) val[e + c] = to_t<T>(v4[c]);
       }
-      gst<V>((T*)L.Wf + ((size_t)(((o0 >> 4) + bt) * (L.Kp / KC) + (i0 + kl) / KC) * 64 + ln) * EPL, val);
+      st_wt(L.Wf, ((size_t)(((o0 >> 4) + bt) * (L.Kp / KC) + (i0 + kl) / KC) * 64 + ln) * EPL * sizeof(T), val);
     }
   }
 }
@@ -298,8 +300,9 @@ __device__ __forceinline__ void store_operands(const LayerDev& L, int o0, int i0
 // (o0+o, i0+i..+EPT-1) (state st from loadn); threads < 32 own bias o0+tid (tiles with i0 == 0).
 // wt: an LDS tile image (32 rows of 32·NI + 4 floats) the caller no longer needs.  Every thread of
 // the block calls it (barrier inside).
+// returns (threads < 32 of a tile with i0 == 0) the new padded bias value, else 0
 template <typename T, int MODE, int NTHR, int EPT, int NI = 1>
-__device__ __forceinline__ void tile_epilogue(const LayerDev& L, int o0, int i0, const PreN<EPT>& st, const PreB& sb,
+__device__ __forceinline__ float tile_epilogue(const LayerDev& L, int o0, int i0, const PreN<EPT>& st, const PreB& sb,
                                               typename VecF<EPT>::T g, float db, const AdamArgs& aa, float* wt) {
   using V = typename VecF<EPT>::T;
   constexpr int TW = 32 * NI, LD = TW + 4, TPR = TW / EPT;  // tile width, image row stride, threads per row
@@ -307,23 +310,25 @@ __device__ __forceinline__ void tile_epilogue(const LayerDev& L, int o0, int i0,
   V w = {};
   if (tid < 32 * TPR) w = applyn<MODE, EPT>(st, g, aa);
   WSTAMP(4);
-  if (i0 == 0 && tid < 32) apply_bias<MODE>(L, o0 + tid, sb, db, aa);
-  if (MODE == PM_GRAD || (CVAE_DIAG_NOWPACK && MODE == PM_ADAM)) return;
+  float nb = 0.f;
+  if (i0 == 0 && tid < 32) nb = apply_bias<MODE>(L, o0 + tid, sb, db, aa);
+  if (MODE == PM_GRAD || (CVAE_DIAG_NOWPACK && MODE == PM_ADAM)) return nb;
   if (tid < 32 * TPR) *(V*)(wt + o * LD + iv) = w;
   __syncthreads();
   WSTAMP(5);
 #pragma unroll
   for (int s = 0; s < NI; ++s) store_operands<T, NTHR, LD>(L, o0, i0 + 32 * s, wt + 32 * s);
   WSTAMP(6);
+  return nb;
 }
 
 // peer exchange (cvae_peer.h): after the owner's tile_epilogue, the same new operand copies (the
 // LDS image wt) and bias into every other rank's arena, released at system scope, then one arrival
 // on each of their done counters
 template <typename T, int NTHR>
-__device__ __forceinline__ void px_broadcast(const PeerArgs& p, const LayerDev& L, int o0, int i0, const float* wt) {
+__device__ __forceinline__ void px_broadcast(const PeerArgs& p, const LayerDev& L, int o0, int i0, const float* wt,
+                                             float nb) {
   const int tid = threadIdx.x;
-  const float nb = (i0 == 0 && tid < 32 && o0 + tid < L.Np) ? L.bias[o0 + tid] : 0.f;  // this thread's own store
   for (int r = 0; r < p.world; ++r) {
     if (r == p.rank) continue;
     const ptrdiff_t d = p.arena[r] - p.arena[p.rank];
@@ -585,8 +590,8 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
     if (tid == 0) sk.tickets[sk.tile] = 0u;  // every split has added: reset for the next launch
   }
   __syncthreads();  // red becomes the image of the new weights
-  tile_epilogue<T, MODE, WG_THREADS, EPT, NI>(L, td.o0, td.i0, st, sb, g4, db, aa, red);
-  if (MODE == PM_ADAM && px) px_broadcast<T, WG_THREADS>(*px, L, td.o0, td.i0, red);
+  const float nb = tile_epilogue<T, MODE, WG_THREADS, EPT, NI>(L, td.o0, td.i0, st, sb, g4, db, aa, red);
+  if (MODE == PM_ADAM && px) px_broadcast<T, WG_THREADS>(*px, L, td.o0, td.i0, red, nb);
 #if CVAE_DIAG_STAMPS
   __syncthreads();
   WSTAMP(3);

@@ -1,0 +1,58 @@
+"""Per-kernel register / LDS / scratch usage of the built library (the gfx950 code object's
+AMDGPU metadata notes), without running anything: a kernel with VGPRs > 128 at 512 threads fits
+one workgroup per CU, <= 128 two.
+
+usage: python3 scripts/kernel_resources.py [pattern ...]   (substrings of the mangled names)
+"""
+import os
+import re
+import struct
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "defensive-model-vae_amd", "cvae_amd", "libcvae_hip.so")
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+
+def code_objects(blob):
+    """gfx950 ELF images inside the clang offload bundles of the shared library."""
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    out = []
+    for m in re.finditer(re.escape(magic), blob):
+        p = m.start() + len(magic)
+        n = struct.unpack_from("<Q", blob, p)[0]
+        p += 8
+        for _ in range(n):
+            off, size, idlen = struct.unpack_from("<QQQ", blob, p)
+            p += 24
+            ident = blob[p:p + idlen].decode(errors="replace")
+            p += idlen
+            if "gfx950" in ident:
+                out.append(blob[m.start() + off:m.start() + off + size])
+    return out
+
+
+def main():
+    pats = sys.argv[1:]
+    blob = open(LIB, "rb").read()
+    for co in code_objects(blob):
+        with tempfile.NamedTemporaryFile(suffix=".co") as f:
+            f.write(co)
+            f.flush()
+            notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", f.name], capture_output=True, text=True).stdout
+        for k in re.split(r"\n\s+- \.agpr_count", notes)[1:]:
+            name = re.search(r"\.name:\s+(\S+)", k)
+            if not name or (pats and not any(p in name.group(1) for p in pats)):
+                continue
+            g = lambda key: (re.search(rf"\.{key}:\s+(\S+)", k) or [None, "?"])[1]  # noqa: E731
+            dem = subprocess.run(["c++filt"], input=name.group(1), capture_output=True,
+                                 text=True).stdout.strip()
+            print(f"vgpr {g('vgpr_count'):>4} agpr {k.split()[0] if k.split() else '?':>4} sgpr {g('sgpr_count'):>3} "
+                  f"lds {g('group_segment_fixed_size'):>6} scratch {g('private_segment_fixed_size'):>5} "
+                  f"wg {g('max_flat_workgroup_size'):>4}  {dem[:150]}")
+
+
+if __name__ == "__main__":
+    main()
