@@ -49,15 +49,17 @@ PEAK = {"bf16": 2500.0, "fp32": 157.3, "fp8": 5000.0}  # dense TFLOP/s, MI355X_M
 HBM_PEAK_GBS = 8000.0                      # HBM3E peak, MI355X_MICROARCH.md
 
 
-def fwd_macs(S, D, Z, H, C=2, n_enc=4, n_dec=4):
-    """F of SURVEY §8d: forward multiply-accumulates per trajectory (4+4 layers by default)."""
+def fwd_macs(S, D, Z, H, C=2, n_enc=4, n_dec=4, E=0):
+    """F of SURVEY §8d: forward multiply-accumulates per trajectory (4+4 layers by default); E > 0:
+    the cfg4 class embedding widens the fc and decoder-L0 inputs by E (the embedding itself is a
+    gather)."""
     I = S * D
-    return ((C * H + H * H) + (I * H + (n_enc - 1) * H * H) + 2 * (2 * H * Z)
-            + ((Z + H) * H + (n_dec - 2) * H * H + H * I))
+    return ((C * H + H * H) + (I * H + (n_enc - 1) * H * H) + (2 * H + E) * 2 * Z
+            + ((Z + H + E) * H + (n_dec - 2) * H * H + H * I))
 
 
-def flops_per_traj(S, D, Z, H, C=2, n_enc=4, n_dec=4):
-    F = fwd_macs(S, D, Z, H, C, n_enc, n_dec)
+def flops_per_traj(S, D, Z, H, C=2, n_enc=4, n_dec=4, E=0):
+    F = fwd_macs(S, D, Z, H, C, n_enc, n_dec, E)
     I = S * D
     return {"total": 2 * (3 * F - C * H - I * H),
             "rowchain": 2 * F + 2 * (F - C * H - I * H),  # forward + every dX
@@ -216,9 +218,10 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (cfg2/wide: 1024, cfg1: 32)")
-    ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg1", "wide"],
+    ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg1", "wide", "cfg4"],
                     help="cfg2: the headline (S=100, Z=8, 4+4 layers, synthetic); cfg1: the reference's sce1 "
-                         "data at B=32, fp32; wide: BASELINE cfg5's shape (S=200, Z=512, 8+8 layers)")
+                         "data at B=32, fp32; wide: BASELINE cfg5's shape (S=200, Z=512, 8+8 layers); cfg4: cfg2's "
+                         "shape with the scenario-class embedding (4 classes, class_dim 16; a build-side extension)")
     ap.add_argument("--dtype", default=None, choices=["bf16", "fp32", "fp8"],
                     help="operand dtype (default: bf16; cfg1: fp32)")
     ap.add_argument("--dp", action="store_true",
@@ -277,11 +280,12 @@ def main():
         S, D = 10, 3
     dtype = args.dtype or ("fp32" if wl == "cfg1" else "bf16")
     B = args.batch or (32 if wl == "cfg1" else 1024)
+    NC, CE = (4, 16) if wl == "cfg4" else (0, 0)  # cfg4: scenes (Town04/Town05 sce1-4) and embedding width
     torch.manual_seed(0)
-    model = ConditionalTrajectoryVAE(S, D, Z, H, NE, ND)
+    model = ConditionalTrajectoryVAE(S, D, Z, H, NE, ND, n_classes=NC, class_dim=CE or 16)
     eng = model.attach(dtype=dtype, max_batch=B, device=dev, seed=4321)
     dp = DataParallelStep(eng, force_split=args.dp, buckets=args.buckets,
-                          exchange="rccl" if wl == "cfg1" else args.exchange)
+                          exchange="rccl" if wl in ("cfg1", "cfg4") else args.exchange)
     dp.broadcast_params()
 
     if wl == "cfg1":
@@ -313,6 +317,11 @@ def main():
     else:
         x = torch.randn(B, S, D, generator=torch.Generator().manual_seed(1234 + rank))
         x = eng.as_input(x)  # resident in HBM, operand dtype
+        cls = None
+        if NC:  # cfg4: a scene class per trajectory, uniform over the NC scenes (seeded)
+            cls = torch.randint(0, NC, (B,), generator=torch.Generator().manual_seed(99 + rank),
+                                dtype=torch.int32).to(dev)
+        ckw = {"classes": cls} if cls is not None else {}
         rows_per_step = B
         graphed = prepared = None
         use_graph = args.graph or (dp.split and dp.px is None and not args.no_graph)
@@ -325,9 +334,9 @@ def main():
             # the fused steps through one prepared C call (arguments converted once): train_steps'
             # ~40 us of Python before the first launch would otherwise be a fixed cost of every
             # timed region — 1.5 us per step at the driver's 20 steps (short runs)
-            prepared = eng.prepare_steps(x, batch=B)
+            prepared = eng.prepare_steps(x, batch=B, classes=cls)
         if use_graph:
-            one = lambda: dp.step(x, batch=B, global_batch=B * world)  # noqa: E731
+            one = lambda: dp.step(x, batch=B, global_batch=B * world, **ckw)  # noqa: E731
             try:
                 if dist.is_initialized():  # RCCL's communicator is created outside the capture
                     dist.all_reduce(torch.zeros(1, device=dev))
@@ -350,10 +359,10 @@ def main():
             elif prepared is not None:
                 prepared(k)
             elif not dp.split:
-                eng.train_steps(x, k, batch=B)
+                eng.train_steps(x, k, batch=B, **ckw)
             else:
                 for _ in range(k):
-                    dp.step(x, batch=B, global_batch=B * world)
+                    dp.step(x, batch=B, global_batch=B * world, **ckw)
 
     run(args.warmup)
     torch.cuda.synchronize(dev)
@@ -372,7 +381,7 @@ def main():
     eng.set_timing(True)
     if wl != "cfg1" and graphed is not None:
         for _ in range(args.steps):
-            dp.step(x, batch=B, global_batch=B * world)
+            dp.step(x, batch=B, global_batch=B * world, **ckw)
     else:
         run(args.steps)
     torch.cuda.synchronize(dev)
@@ -381,7 +390,7 @@ def main():
     # each kernel alone, launched back-to-back (cvae_bench_kernels): the step's kernels without
     # their neighbours' cache/instruction-cache effects
     b2b = None
-    if not args.no_b2b and wl != "cfg1" and world == 1:
+    if not args.no_b2b and wl not in ("cfg1", "cfg4") and world == 1:
         b2b = eng.bench_kernels(x, max(args.steps, 20), batch=B)
     if world > 1:
         tt = torch.tensor([t], device=dev, dtype=torch.float64)
@@ -392,7 +401,7 @@ def main():
 
     px_stats = dp.px.stats() if dp.px is not None else None
     if rank == 0:
-        fl = flops_per_traj(S, D, Z, H, n_enc=NE, n_dec=ND)
+        fl = flops_per_traj(S, D, Z, H, n_enc=NE, n_dec=ND, E=CE)
         tsize = 4 if dtype == "fp32" else 2  # fp8: bf16 activations
         bt = bytes_per_traj(S, D, Z, H, tsize, n_enc=NE, n_dec=ND)
         n_par = eng.n_params
@@ -431,6 +440,11 @@ def main():
             metric = (f"trajectories/sec per ELBO step, sce1 StaticBlindTown05 data, batch={B} seq_len=10 "
                       f"(BASELINE configs[0])")
             data = "the reference's trajectory_sce1_cond.npy rows (38x10x3, committed fixture), host eps"
+        elif wl == "cfg4":
+            metric = (f"trajectories/sec per ELBO step, batch={B} seq_len={S}, scenario-class embedding "
+                      f"(BASELINE configs[3])")
+            data = (f"synthetic x~N(0,1) and class ids uniform over {NC} scenes (seeded), random-init weights "
+                    f"(torch.manual_seed(0)); class_dim {CE}; parity unpinned vs the reference (no such model)")
         else:
             metric = f"trajectories/sec per ELBO step, batch={B} seq_len={S} (BASELINE cfg5 shape)"
             data = "synthetic x~N(0,1) (seeded), random-init weights (torch.manual_seed(0))"

@@ -99,6 +99,7 @@ struct cvae_handle {
   bool wide = false;        // bf16 training at BASELINE cfg5's shape runs wchain::widechain_kernel<Cfg5>
   int wide_lds = 0;
   bool ring = false;        // the fast configuration's training chain runs wchain::widechain_kernel<Cfg2>
+  bool ring_cls = false;    // cfg4 (class embedding) at cfg2's shape: widechain_kernel<Cfg4>, generic dW
   int ring_lds = 0;
   bool timing = false;
   // timing: per call, a chain of events on the caller's stream; segment i of a
@@ -683,7 +684,7 @@ bool wide_layout_matches(const cvae_handle* h) {
         (char*)L.xT != h->arena + A::act0 + Bp2 * A::xrows(l) ||
         (char*)L.gT != h->arena + A::act0 + Bp2 * A::grows(l))
       return false;
-    const bool relu = !(l == A::LFC || l == A::LDL);
+    const bool relu = !(l == A::LFC || l == A::LDL || l == A::LCE);
     if (L.relu != (relu ? 1 : 0)) return false;
   }
   return true;
@@ -704,6 +705,27 @@ int plan_ring(cvae_handle* h) {
   HIPCK(hipFuncSetAttribute((const void*)wchain::widechain_kernel<A>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             A::L_TOTAL));
   h->ring = true;
+  h->ring_lds = A::L_TOTAL;
+  return CVAE_OK;
+}
+
+// BASELINE cfg4 (the class embedding) at cfg2's shape on the ring chain (wchain::Cfg4; its dW ⊕ Adam
+// is the generic tile-list kernel: the fast dW decode knows the 11 reference layers only)
+int plan_ring_cls(cvae_handle* h) {
+  using A = wchain::Cfg4;
+  const cvae_config& c = h->cfg;
+  h->ring_cls = false;
+  const char* env = std::getenv("CVAE_RING");
+  const char* gen = std::getenv("CVAE_GENERIC");
+  if ((env && env[0] == '0') || (gen && gen[0] == '1') || c.dtype != CVAE_BF16 || c.n_classes < 1 ||
+      c.n_classes > A::CLS_NMAX || c.class_dim < 4 || c.class_dim > A::CLS_EMAX || c.class_dim % 4 ||
+      c.seq_len != A::S || c.dim != A::D || c.latent_dim != A::Z || c.hidden_dim != wchain::H || c.n_enc != A::NE ||
+      c.n_dec != A::ND || h->R != wchain::R)
+    return CVAE_OK;
+  if (!wide_layout_matches<A>(h) || h->arena_bytes >= ((int64_t)1 << 31)) return CVAE_OK;
+  HIPCK(hipFuncSetAttribute((const void*)wchain::widechain_kernel<A>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            A::L_TOTAL));
+  h->ring_cls = true;
   h->ring_lds = A::L_TOTAL;
   return CVAE_OK;
 }
@@ -760,11 +782,17 @@ RowArgs row_args(cvae_handle* h, const CallX& c) {
   ra.w_recon = c.w ? c.w->recon : 0.1f; ra.w_kld = c.w ? c.w->kld : 0.1f;
   ra.w_start = c.w ? c.w->start : 1.0f; ra.w_time = c.w ? c.w->time : 1.0f;
   ra.partials = h->d_partials;
+  ra.ncls = h->net.n_cls;
+  ra.cdim = h->net.cls_dim;
   return ra;
 }
 
 bool fast_ok(const cvae_handle* h, const RowArgs& ra) {
   return h->fast_nki > 0 && (((uintptr_t)ra.x) & 15) == 0 && !ra.x_f32 && !ra.ext && !ra.x_relative;
+}
+bool ring_cls_ok(const cvae_handle* h, const RowArgs& ra) {
+  return h->ring_cls && (((uintptr_t)ra.x) & 15) == 0 && (((uintptr_t)ra.eps) & 15) == 0 && !ra.x_f32 && !ra.ext &&
+         !ra.x_relative;
 }
 bool wide_ok(const cvae_handle* h, const RowArgs& ra) {
   return h->wide && (((uintptr_t)ra.x) & 15) == 0 && (((uintptr_t)ra.eps) & 15) == 0 && !ra.x_f32 && !ra.ext &&
@@ -773,6 +801,7 @@ bool wide_ok(const cvae_handle* h, const RowArgs& ra) {
 // rows per workgroup of the training row chain a call runs (its loss partials are per workgroup)
 int chain_rows(const cvae_handle* h, const RowArgs& ra) {
   if (fast_ok(h, ra)) return fchain::R;
+  if (ring_cls_ok(h, ra)) return wchain::R;
   if (wide_ok(h, ra)) return wchain::R;
   return h->R;
 }
@@ -786,6 +815,12 @@ int launch_train_chain(cvae_handle* h, RowArgs ra, hipStream_t s) {
     ra.stamps = h->d_stamps;
     const int grid = rup_i(ra.batch, 32) / wchain::R;
     return klaunch(h, wchain::widechain_kernel<wchain::Cfg2>, dim3(grid), dim3(wchain::NT), h->ring_lds, s,
+                   h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra.ctr, ra);
+  }
+  if (std::is_same<T, __bf16>::value && ring_cls_ok(h, ra)) {
+    ra.stamps = h->d_stamps;
+    const int grid = rup_i(ra.batch, 32) / wchain::R;
+    return klaunch(h, wchain::widechain_kernel<wchain::Cfg4>, dim3(grid), dim3(wchain::NT), h->ring_lds, s,
                    h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra.ctr, ra);
   }
   if (std::is_same<T, __bf16>::value && fast_ok(h, ra)) {
@@ -982,6 +1017,7 @@ int cvae_create(const cvae_config* cfg, int device, cvae_handle** out) {
   if (!rc) rc = plan_fast(h);
   if (!rc) rc = plan_wide(h);
   if (!rc) rc = plan_ring(h);
+  if (!rc) rc = plan_ring_cls(h);
   if (rc) { cvae_destroy(h); return rc; }
   *out = h;
   return CVAE_OK;
@@ -1033,7 +1069,7 @@ int cvae_workspace_bytes(const cvae_handle* h, int64_t* bytes) {
 
 int cvae_train_kernel(const cvae_handle* h, int* kind) {
   if (!h || !kind) return fail(CVAE_E_INVALID, "null argument");
-  *kind = h->ring && !h->fused ? CVAE_KERNEL_RING
+  *kind = (h->ring && !h->fused) || h->ring_cls ? CVAE_KERNEL_RING
            : h->fast_nki > 0      ? CVAE_KERNEL_FAST
            : h->wide              ? CVAE_KERNEL_WIDE
                                   : CVAE_KERNEL_GENERIC;

@@ -194,6 +194,7 @@ struct RowArgs {
   const float* d_lv;      // (batch, Z)
   const float* d_hc;      // (batch, H)
   const int* classes;     // cfg4: class id per row of x (gathered by idx like x); NULL = class 0
+  int ncls, cdim;         // cfg4: n_classes, class_dim (0 for the reference model)
 };
 
 // Philox offset of this launch's eps draws: the device counter when given (a replayable step)

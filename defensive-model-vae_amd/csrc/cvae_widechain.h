@@ -53,28 +53,42 @@ __device__ __forceinline__ void sfor(F&& f) {
 
 // F8_: the CVAE_FP8 form — every forward GEMM whose padded K is a multiple of 64 multiplies e4m3
 // activations by e4m3(s·W) fragments (half the weight stream); backward GEMMs stay bf16.
-template <int S_, int D_, int Z_, int NE_, int ND_, bool F8_ = false>
+// CLS_: BASELINE cfg4's scenario-class embedding (a build-side extension of Training_VAE.py:193,
+// :214): e = table[class] (class_dim <= CLS_EMAX features, n_classes <= 32) joins both
+// concatenations, [h_traj ‖ h_c ‖ e] and [z ‖ h_c ‖ e]; the table is the last layer (LCE, one-hot
+// input, no bias, no activation).  Its padded dims do not depend on class_dim within that bound, so
+// one instantiation serves every class_dim the host accepts (plan_ring_cls).
+template <int S_, int D_, int Z_, int NE_, int ND_, bool F8_ = false, bool CLS_ = false>
 struct Arch {
   static constexpr int S = S_, D = D_, Z = Z_, NE = NE_, ND = ND_, I = S_ * D_;
-  static constexpr bool F8 = F8_;
+  static constexpr bool F8 = F8_, CLS = CLS_;
+  static constexpr int CLS_EMAX = 24, CLS_NMAX = 32;
   static constexpr int NKI = (I + 31) / 32, Ip = 32 * NKI;
-  static constexpr int NL = 3 + NE + ND, ZH = Z + H;
+  static constexpr int NL = 3 + NE + ND + (CLS_ ? 1 : 0), ZH = Z + H;
   // SZ: a latent of one 16-feature tile of mu ‖ logvar (the reference architecture, latent 8): fc is
   // one n-tile, split over the waves by K; dz and dh_c of the decoder-L0 backward are not tile-aligned
   static constexpr bool SZ = 2 * Z == 16;
   static constexpr int r32(int v) { return (v + 31) / 32 * 32; }
-  static constexpr int LC0 = 0, LC1 = 1, LE0 = 2, LFC = 2 + NE, LD0 = 3 + NE, LDL = 2 + NE + ND;
+  static constexpr int LC0 = 0, LC1 = 1, LE0 = 2, LFC = 2 + NE, LD0 = 3 + NE, LDL = 2 + NE + ND,
+                       LCE = CLS_ ? 3 + NE + ND : -1;
   static constexpr int LE(int i) { return 2 + i; }
   static constexpr int LD(int i) { return 3 + NE + i; }
-  static constexpr int Kp(int l) { return l == LC0 ? 32 : l == LE0 ? Ip : l == LFC ? 2 * H : l == LD0 ? r32(ZH) : H; }
-  static constexpr int Np(int l) { return l == LFC ? r32(2 * Z) : l == LDL ? Ip : H; }
+  static constexpr int Kp(int l) {
+    return l == LC0 ? 32 : l == LE0 ? Ip : l == LFC ? (CLS ? r32(2 * H + CLS_EMAX) : 2 * H)
+         : l == LD0 ? r32(ZH + (CLS ? CLS_EMAX : 0)) : l == LCE ? CLS_NMAX : H;
+  }
+  static constexpr int Np(int l) { return l == LFC ? r32(2 * Z) : l == LDL ? Ip : l == LCE ? r32(CLS_EMAX) : H; }
+  // fc's K chunks (32 wide): 2H/32, and one more for the class embedding
+  static constexpr int FC_KCH = (CLS ? r32(2 * H + CLS_EMAX) : 2 * H) / 32;
   // ReLU masks (forward order): C0 C1 E0..E(NE-1) D0..D(ND-2)
   static constexpr int MC0 = 0, MC1 = 1;
   static constexpr int ME(int i) { return 2 + i; }
   static constexpr int MD(int i) { return 2 + NE + i; }
   static constexpr int NMASK = 2 + NE + ND - 1, NMW = (NMASK + 7) / 8;
   static_assert(Z % 128 == 0 || SZ, "latent tiles: 8 waves x whole 16-feature tiles of mu and logvar, or one tile");
-  static_assert(!SZ || 2 * H / 32 == NW, "small latent: fc's K chunks split one per wave");
+  static_assert(!SZ || (FC_KCH >= NW && FC_KCH <= 2 * NW), "small latent: fc's K chunks split over the waves");
+  static_assert(!CLS || (SZ && r32(2 * H + CLS_EMAX) == r32(2 * H + 4) && r32(ZH + CLS_EMAX) == r32(ZH + 4)),
+                "class embedding: padded fc / decoder-input K independent of class_dim in [4, CLS_EMAX]");
   static_assert(I % 8 == 0 && D >= 3, "x rows load as 16-B vectors; channels 0..2 = t, x, y");
   // the layers the fp8 form runs in e4m3 (cvae_capi.hip build_plan: padded K % 64 == 0)
   static constexpr bool f8(int l) { return F8 && Kp(l) % 64 == 0; }
@@ -107,7 +121,7 @@ struct Arch {
   // pass; dL/d[mu ‖ logvar] (the fc backward's input image) from the decoder-L0 backward on
   static constexpr int L_XIN = 0, L_CIN = L_XIN + Ip * 32, L_CB = L_CIN + 32 * 32, L_A0 = L_CB + H * 32,
                        L_A1 = L_A0 + H * 32, L_U = L_A1 + H * 32;
-  static constexpr int L_HCAT = L_U, L_DCAT = L_HCAT + 2 * H * 32, L_RCH0 = L_DCAT + Kp(LD0) * 32,
+  static constexpr int L_HCAT = L_U, L_DCAT = L_HCAT + Kp(LFC) * 32, L_RCH0 = L_DCAT + Kp(LD0) * 32,
                        L_GD0 = L_RCH0 + S * R * 4, L_UEND = L_GD0 + S * R * 4, L_GFC = L_U;
   static_assert(Np(LFC) * 32 <= L_UEND - L_U, "the fc-backward image fits in the dead forward buffers");
   // SZ only: fc's per-wave partial sums (fp32 [wave][feature][row], in A0 ‖ A1, dead at fc) and the
@@ -131,7 +145,12 @@ struct Arch {
     return L == L_A0 ? L_A08 : L == L_A1 ? L_A18 : L == L_CB ? L_CB8 : L == L_HCAT ? L_HCAT8
          : L == L_DCAT ? L_DCAT8 : L == L_XIN ? L_X8 : -1;
   }
-  static constexpr int L_BIAS = L_INVS + (F8 ? 32 * 4 : 0), L_PART = L_BIAS + nbias * 4,
+  // CLS: the one-hot class image (xT(LCE), 32 features), the de image (gT(LCE)), the decoder's
+  // share of de (fp32 [feature][row]) and the rows' class ids
+  static constexpr int L_CLS1H = L_INVS + (F8 ? 32 * 4 : 0), L_GCE = L_CLS1H + (CLS ? CLS_NMAX * 32 : 0),
+                       L_DCE2 = L_GCE + (CLS ? Np(LCE) * 32 : 0), L_CLSID = L_DCE2 + (CLS ? CLS_EMAX * R * 4 : 0),
+                       L_CTAB = L_CLSID + (CLS ? R * 4 : 0);  // the table's operand copy (Wf(LCE), 2 KB)
+  static constexpr int L_BIAS = L_CTAB + (CLS ? 2 * Np(LCE) * Kp(LCE) : 0), L_PART = L_BIAS + nbias * 4,
                        L_STAMPS = L_PART + NW * 8 * 4, L_TOTAL = L_STAMPS + (CVAE_DIAG_STAMPS ? 64 * 8 : 0);
   static_assert(NL <= 32, "1/s table");
   static_assert(L_TOTAL <= 160 * 1024, "LDS");
@@ -167,7 +186,9 @@ struct Plan {
     if (s == k++) return {A::LC1, 0, H / 32, 1, H / 16};
     for (int i = 1; i < A::NE; ++i)
       if (s == k++) return {A::LE(i), 0, H / 32, 1, H / 16};
-    if (s == k++) return A::SZ ? StepInfo{A::LFC, 0, 1, 1, 1, 0, 1} : StepInfo{A::LFC, 0, 2 * H / 32, A::Z / 64, A::Z / 8, 2};
+    if (s == k++)  // SZ: K chunks wave, wave + 8 (KC items per wave; a chunk past FC_KCH is skipped)
+      return A::SZ ? StepInfo{A::LFC, 0, (A::FC_KCH + NW - 1) / NW, 1, 1, 0, 1}
+                   : StepInfo{A::LFC, 0, 2 * H / 32, A::Z / 64, A::Z / 8, 2};
     if (s == k++) return {A::LD0, 0, A::Kp(A::LD0) / 32, 1, H / 16};
     for (int i = 1; i < A::ND - 1; ++i)
       if (s == k++) return {A::LD(i), 0, H / 32, 1, H / 16};
@@ -176,7 +197,7 @@ struct Plan {
     for (int i = A::ND - 2; i >= 1; --i)
       if (s == k++) return {A::LD(i), 1, H / 32, 1, H / 16};
     if (s == k++) return {A::LD0, 1, H / 32, (A::Kp(A::LD0) / 16 + NW - 1) / NW, A::Kp(A::LD0) / 16};
-    if (s == k++) return {A::LFC, 1, A::Np(A::LFC) / 32, 2, 2 * H / 16};
+    if (s == k++) return {A::LFC, 1, A::Np(A::LFC) / 32, (A::Kp(A::LFC) / 16 + NW - 1) / NW, A::Kp(A::LFC) / 16};
     for (int i = A::NE - 1; i >= 1; --i)
       if (s == k++) return {A::LE(i), 1, H / 32, 1, H / 16};
     if (s == k++) return {A::LC1, 1, H / 32, 1, H / 16};
@@ -231,8 +252,11 @@ __device__ __forceinline__ void ring_load(Ring<P>& ring, const char* AR, int wav
     asm volatile("" : "+s"(w));  // recomputed per item: hoisted, ~400 item addresses would be live SGPRs
     int t = w + NW * slot;
     if constexpr (NW * (slot + 1) > st.NTL) t = min(t, st.NTL - 1);
-    const int64_t frag = st.KS ? w : t * st.KC + kc;  // KS: tile 0, chunk = wave
-    if constexpr (CVAE_RING_SKIP && !st.KS && NW * (slot + 1) > st.NTL) {
+    const int64_t frag = st.KS ? w + NW * kc : t * st.KC + kc;  // KS: tile 0, chunk = wave + 8·item
+    if constexpr (st.KS && NW * (kc + 1) > A::FC_KCH) {
+      // a K chunk past the layer (wave-uniform): no load, and gemm skips its MFMA
+      if (w + NW * kc < A::FC_KCH) ring.r[G % P] = gld<bf16x8>(AR + base + frag * 1024 + lane * 16);
+    } else if constexpr (CVAE_RING_SKIP && !st.KS && NW * (slot + 1) > st.NTL) {
       // a slot past the layer's tiles: no load (wave-uniform); the stale ring register feeds an
       // MFMA whose result the epilogue drops
       if (w + NW * slot < st.NTL) ring.r[G % P] = gld<bf16x8>(AR + base + frag * 1024 + lane * 16);
@@ -312,8 +336,21 @@ __device__ __forceinline__ void gemm(Ring<P>& ring, const void* img, f32x4 (&acc
   static_assert(st.TS == TS && st.GRP == 0, "accumulator slots");
   constexpr int G0 = PL::start(S);
   sfor<0, TS>([&](auto t) { acc[decltype(t)::value] = f32x4{0.f, 0.f, 0.f, 0.f}; });
-  static_assert(!st.KS || (st.KC == 1 && TS == 1 && !F8), "K split: one chunk per wave");
-  XOp<F8> xf = xop<F8>(img, st.KS ? wave : 0);
+  static_assert(!st.KS || (TS == 1 && !F8), "K split: chunks wave, wave + 8, .. of one n-tile");
+  if constexpr (st.KS) {  // chunk wave + 8c of the one n-tile; chunks past FC_KCH (wave-uniform) skipped
+    sfor<0, st.KC>([&](auto kc) {
+      constexpr int c = decltype(kc)::value, g = G0 + c;
+      const int ch = wave + NW * c;
+      if (NW * (c + 1) <= A::FC_KCH || ch < A::FC_KCH) {
+        acc[0] = xmfma<false>(xop<false>(img, ch), ring.r[g % P], acc[0]);
+        asm volatile("" : "+v"(acc[0]));
+      }
+      ring_load<A, P, g + P>(ring, AR, wave, lane);
+      side(kc);
+    });
+    return;
+  }
+  XOp<F8> xf = xop<F8>(img, 0);
   XOp<F8> xe = xf;  // F8: the even pair, multiplied together with the odd one after it
   sfor<0, st.KC>([&](auto kc) {
     constexpr int c = decltype(kc)::value;
@@ -589,6 +626,18 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
       });
       invv = gld<float>((const float*)(AR + o));
     }
+    // CLS: this tile's class ids (gathered like x) and the embedding table's operand copy (2 KB)
+    int cid = -1;
+    u32x4 tab = {0u, 0u, 0u, 0u};
+    if constexpr (A::CLS) {
+      if (tid < R) {
+        int64_t g = min(b0 + tid, last);
+        if (a.idx) g = gld<int64_t>(a.idx + g);
+        const int c = a.classes ? gld<int>(a.classes + g) : 0;
+        cid = tid < nrows ? min(max(c, 0), a.ncls - 1) : -1;  // out-of-range ids clamp (host validates)
+      }
+      if (tid < 2 * A::Np(A::LCE) * A::Kp(A::LCE) / 16) tab = gld<u32x4>(AR + A::wf(A::LCE) + 16 * tid);
+    }
     // the weight stream queues behind the x tile and the biases (vmcnt retires in order)
     ring_fill<A, P>(ring, AR, wave, lane);
     // device counters: this launch begins optimizer step ctr[1] + 1 and precomputes its Adam
@@ -612,6 +661,10 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
 #pragma unroll
     for (int k = 0; k < UB; ++k)
       if (k * NT + tid < NB4) ((f32x4*)BIAS)[k * NT + tid] = bv[k];
+    if constexpr (A::CLS) {
+      if (tid < R) ((int*)(smem + A::L_CLSID))[tid] = cid;
+      if (tid < 2 * A::Np(A::LCE) * A::Kp(A::LCE) / 16) ((u32x4*)(smem + A::L_CTAB))[tid] = tab;
+    }
     if constexpr (A::F8) {
       bool f8l = false;
       sfor<0, A::NL>([&](auto ll) { f8l = f8l || (A::f8(decltype(ll)::value) && tid == decltype(ll)::value); });
@@ -650,6 +703,27 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   }
   sub();
   bar();
+  if constexpr (A::CLS) {
+    // the one-hot class image (xT(LCE)) and e = table[class] into both concatenations at 2H + k and
+    // Z + H + k (bf16: what one-hot · Wf(LCE) gives the generic chain; zeros in the K padding)
+    const int* CLSID = (const int*)(smem + A::L_CLSID);
+    const __bf16* TAB = (const __bf16*)(smem + A::L_CTAB);
+    const int f = (tid >> 2) & 31, qq = tid & 3;
+    bf16x4 v;
+    if (tid < 128) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = (__bf16)(CLSID[4 * qq + i] == f ? 1.f : 0.f);
+      *(bf16x4*)((__bf16*)(smem + A::L_CLS1H) + ioff(f, qq)) = v;
+    } else if (tid < 256) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = CLSID[4 * qq + i];
+        v[i] = (c >= 0 && f < a.cdim) ? TAB[frag_off<__bf16>(f, c, A::Kp(A::LCE))] : (__bf16)0.f;
+      }
+      *(bf16x4*)((__bf16*)(smem + A::L_HCAT) + ioff(2 * H + f, qq)) = v;
+      if (A::ZH + f < A::Kp(A::LD0)) *(bf16x4*)((__bf16*)(smem + A::L_DCAT) + ioff(A::ZH + f, qq)) = v;
+    }
+  }
 
   const float Bf = (float)a.batch;
   const float inv_BSD = 1.f / (Bf * (float)(S * D)), inv_2B = 1.f / (2.f * Bf), inv_B = 1.f / Bf;
@@ -734,6 +808,8 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     gemm<A, P, PL::sC1 + i>(ring, opnd(sI, IIN{}), acc, AR, wave, lane, NoSide{}, scl(sI));
     img_copy<H, 0, 1>(in, dst, XT(A::LE(i)), H, 0, b0);
     if constexpr (i >= 2 && i <= 3) img_copy<Ip, i + 1, i + 2>(XIN, dst, XT(A::LE0), A::Kp(A::LE0), 0, b0);
+    if constexpr (A::CLS && i == 1)
+      img_copy<A::Kp(A::LCE), 0, 1, 2 * H>((const __bf16*)(smem + A::L_CLS1H), dst, XT(A::LCE), A::Kp(A::LCE), 0, b0);
     const bf16x4 he = relu(acc[0], bias(A::LE(i), n), integral_constant<int, A::ME(i)>{});
     img2(IOUT{}, n, he);
   });
@@ -745,7 +821,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     float* const PFC = (float*)(smem + A::L_PFC);
     f32x4 acc[1];
     gemm<A, P, PL::sFC>(ring, HCAT, acc, AR, wave, lane);
-    img_copy<2 * H, 0, 1>(HCAT, dst, XT(A::LFC), A::Kp(A::LFC), 0, b0);
+    img_copy<A::Kp(A::LFC), 0, (2 * A::Kp(A::LFC) + NT - 1) / NT>(HCAT, dst, XT(A::LFC), A::Kp(A::LFC), 0, b0);
     *(f32x4*)(PFC + (wave * 16 + n16) * R + 4 * q) = acc[0];
     bar();
     if (wave == 0 && n16 < Z) {  // latent j = n16: mu at feature j, logvar at Z + j
@@ -790,7 +866,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     f32x4 acc[1];
     constexpr integral_constant<int, PL::sD0> sD0{};
     gemm<A, P, PL::sD0>(ring, opnd(sD0, IDC{}), acc, AR, wave, lane, NoSide{}, scl(sD0));
-    img_copy<A::ZH, 0, 3>(DCAT, dst, XT(A::LD0), A::Kp(A::LD0), 0, b0);
+    img_copy<A::CLS ? A::Kp(A::LD0) : A::ZH, 0, 3>(DCAT, dst, XT(A::LD0), A::Kp(A::LD0), 0, b0);
     img2(IA0{}, n, relu(acc[0], bias(A::LD0, n), integral_constant<int, A::MD(0)>{}));
   }
   // decoder layers 1 .. ND-2 (input: D(i-1)'s output, A0 for odd i)
@@ -939,6 +1015,8 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
         img(GFC, Z + j, to_bf4(gl));
       } else if (f < A::ZH) {
         *(f32x4*)(DHC2 + (f - Z) * R + 4 * q) = acc[s];
+      } else if (A::CLS && f < A::ZH + A::CLS_EMAX) {  // cfg4: the decoder's share of de
+        *(f32x4*)((float*)(smem + A::L_DCE2) + (f - A::ZH) * R + 4 * q) = acc[s];
       }
     });
     // the fc-backward image's K padding (the region held the forward fc input until now)
@@ -965,13 +1043,24 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   }
   bar();
   {  // fcᵀ: dh = G_fc · W_fc → h_traj gradient (mask E(NE-1)) and h_c gradient (+ decoder share, mask C1)
-    f32x4 acc[2];
+    // CLS: tiles 16, 17 (waves 0, 1, slot 2) are de = fc share + decoder share (no activation) → gT(LCE)
+    constexpr int TS = PL::step(PL::sFCb).TS;
+    f32x4 acc[TS];
     gemm<A, P, PL::sFCb>(ring, GFC, acc, AR, wave, lane);
     sub();
     img_copy<A::Np(A::LFC), 0, (2 * A::Np(A::LFC) + NT - 1) / NT>(GFC, dst, GT(A::LFC), A::Np(A::LFC), 0, b0);
     if constexpr (A::SZ) dhc2 = *(const f32x4*)(DHC2 + n * R + 4 * q);
     img(A0, n, masked(acc[0], integral_constant<int, A::ME(NE - 1)>{}));
     img(CB, n, masked(acc[1] + dhc2, integral_constant<int, A::MC1>{}));
+    if constexpr (A::CLS) {
+      static_assert(TS == 3 && A::Kp(A::LFC) == 2 * H + 32, "the class tiles are slot 2 of waves 0, 1");
+      if (wave < 2) {  // wave-uniform
+        const int k = 16 * wave + n16;
+        f32x4 de = acc[2];
+        if (k < A::CLS_EMAX) de += *(const f32x4*)((const float*)(smem + A::L_DCE2) + k * R + 4 * q);
+        img((__bf16*)(smem + A::L_GCE), k, to_bf4(de));
+      }
+    }
   }
   // E(i)ᵀ for i = NE-1 .. 2 (input: gT(E(i)) image), mask of E(i-1)
   sfor<0, NE - 2>([&](auto kk) {
@@ -982,6 +1071,8 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     gemm<A, P, PL::sFCb + 1 + k>(ring, in, acc, AR, wave, lane);
     img_copy<H, 0, 1>(in, dst, GT(A::LE(i)), H, 0, b0);
     if constexpr (k == 0) img_copy<H, 0, 1, 2 * H>(CB, dst, GT(A::LC1), H, 0, b0);
+    if constexpr (A::CLS && k == 0)
+      img_copy<A::Np(A::LCE), 1, 2, NT>((const __bf16*)(smem + A::L_GCE), dst, GT(A::LCE), A::Np(A::LCE), 0, b0);
     img((k & 1) ? A0 : A1, n, masked(acc[0], integral_constant<int, A::ME(i - 1)>{}));
   });
   bar();
@@ -1027,6 +1118,8 @@ using Cfg5 = Arch<200, 6, 512, 8, 8>;
 using Cfg2 = Arch<100, 6, 8, 4, 4>;
 // BASELINE cfg5 in the CVAE_FP8 form (e4m3 forward GEMMs)
 using Cfg5F8 = Arch<200, 6, 512, 8, 8, true>;
+// BASELINE cfg4: the reference architecture at cfg2's shape with the scenario-class embedding
+using Cfg4 = Arch<100, 6, 8, 4, 4, false, true>;
 #ifndef CVAE_WIDE_RING
 #define CVAE_WIDE_RING 12
 #endif

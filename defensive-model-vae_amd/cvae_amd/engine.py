@@ -323,7 +323,7 @@ class CVAEEngine:
         self._ctr[1] += n_steps
         return self.loss
 
-    def prepare_steps(self, x, batch=None, weights=None, accumulate=True, row0=0):
+    def prepare_steps(self, x, batch=None, weights=None, accumulate=True, row0=0, classes=None):
         """A callable ``run(n)`` that enqueues ``n`` fused steps on rows 0..batch-1 of the resident
         ``x`` with Philox eps (cvae_train_steps) — what ``train_steps(x, n, batch=batch)`` does,
         with every argument converted once here instead of per call.
@@ -337,14 +337,13 @@ class CVAEEngine:
         x = self.as_input(x, keep_f32=self.keep_f32)
         B = int(batch if batch is not None else x.shape[0])
         self._check_rows(x, None, B)
-        if self.n_classes:
-            raise ValueError("prepare_steps serves the reference model (n_classes=0)")
+        cl = self._classes(classes, x.shape[0])  # cfg4: class ids per row of x (None for the reference model)
         self.ensure_packed()
         f = lib().cvae_train_steps
         w = self._weights(weights)
         a = self._adam()
-        keep = (x, w, a)  # referenced by the closure: the pointers stay valid
-        pre = (self._h, C.c_void_p(x.data_ptr()), None, None, C.c_int(B))
+        keep = (x, w, a, cl)  # referenced by the closure: the pointers stay valid
+        pre = (self._h, C.c_void_p(x.data_ptr()), None, ptr(cl), C.c_int(B))
         post = (C.c_int(self._xflags(x)), None, C.c_uint64(self.seed), C.c_uint64(0), C.c_int64(int(row0)),
                 C.byref(w), ptr(self.params), ptr(self.m), ptr(self.v), C.c_int64(0), C.byref(a), ptr(self.loss),
                 ptr(self.loss_accum) if accumulate else None, ptr(self.counters), self._stream())
