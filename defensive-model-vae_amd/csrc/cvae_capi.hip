@@ -790,8 +790,14 @@ RowArgs row_args(cvae_handle* h, const CallX& c) {
 bool fast_ok(const cvae_handle* h, const RowArgs& ra) {
   return h->fast_nki > 0 && (((uintptr_t)ra.x) & 15) == 0 && !ra.x_f32 && !ra.ext && !ra.x_relative;
 }
+// the ring chain (cvae_widechain.h Cfg2 / Cfg4) also takes fp32 rows (CVAE_X_F32, the train loop's
+// real data): its prologue subtracts the start point in fp32 and rounds once
+bool ring_ok(const cvae_handle* h, const RowArgs& ra) {
+  return h->ring && h->fast_nki > 0 && (((uintptr_t)ra.x) & 15) == 0 && (((uintptr_t)ra.eps) & 15) == 0 && !ra.ext &&
+         !ra.x_relative;
+}
 bool ring_cls_ok(const cvae_handle* h, const RowArgs& ra) {
-  return h->ring_cls && (((uintptr_t)ra.x) & 15) == 0 && (((uintptr_t)ra.eps) & 15) == 0 && !ra.x_f32 && !ra.ext &&
+  return h->ring_cls && (((uintptr_t)ra.x) & 15) == 0 && (((uintptr_t)ra.eps) & 15) == 0 && !ra.ext &&
          !ra.x_relative;
 }
 bool wide_ok(const cvae_handle* h, const RowArgs& ra) {
@@ -801,7 +807,7 @@ bool wide_ok(const cvae_handle* h, const RowArgs& ra) {
 // rows per workgroup of the training row chain a call runs (its loss partials are per workgroup)
 int chain_rows(const cvae_handle* h, const RowArgs& ra) {
   if (fast_ok(h, ra)) return fchain::R;
-  if (ring_cls_ok(h, ra)) return wchain::R;
+  if (ring_ok(h, ra) || ring_cls_ok(h, ra)) return wchain::R;
   if (wide_ok(h, ra)) return wchain::R;
   return h->R;
 }
@@ -811,7 +817,7 @@ template <typename T>
 int launch_train_chain(cvae_handle* h, RowArgs ra, hipStream_t s) {
   int rc = tmark(h, s, "rowchain");
   if (rc) return rc;
-  if (std::is_same<T, __bf16>::value && h->ring && fast_ok(h, ra)) {
+  if (std::is_same<T, __bf16>::value && ring_ok(h, ra)) {
     ra.stamps = h->d_stamps;
     const int grid = rup_i(ra.batch, 32) / wchain::R;
     return klaunch(h, wchain::widechain_kernel<wchain::Cfg2>, dim3(grid), dim3(wchain::NT), h->ring_lds, s,
@@ -1476,7 +1482,7 @@ int cvae_px_train_step(cvae_handle* h, const void* x, const int64_t* idx, int ba
   if (batch > 0) {
     CallX c{x, idx, nullptr, batch, xflags, eps, seed, 0, eps_row0, w, counters, adam};
     const RowArgs ra = row_args(h, c);
-    if (!fast_ok(h, ra)) return fail(CVAE_E_INVALID, "peer exchange: x must be 16-B aligned operand-dtype rows");
+    if (!ring_ok(h, ra)) return fail(CVAE_E_INVALID, "peer exchange: x must be 16-B aligned rows (operand dtype or fp32)");
     if ((rc = launch_train_chain<__bf16>(h, ra, s))) return rc;
     la = make_loss(h, ra, loss_out, loss_accum);
   } else {  // no rows on this rank this step: the counters advance as a chain + dW launch would

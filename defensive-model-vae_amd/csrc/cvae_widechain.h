@@ -589,12 +589,17 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   float s_recon = 0.f, s_kl = 0.f, s_start = 0.f, s_t0 = 0.f, s_relu = 0.f;
 
   // ---- prologue: x tile (relative transform, Training_VAE.py:345-348), biases, LDS pads
+  // x_f32 (CVAE_X_F32: real data with ~200 m absolute coordinates): fp32 rows, the start point
+  // subtracted in fp32 and the relative offsets rounded to bf16 once
   {
     constexpr int U = (R * A::NKI * 4 + NT - 1) / NT;  // 16-B vectors per thread
     constexpr int VPR = I / 8, NV = R * VPR;
     const int last = max(a.batch - 1, 0);
     const __bf16* xg = (const __bf16*)a.x;
-    bf16x8 xv[U], x0[U];
+    const float* xg32 = (const float*)a.x;
+    const bool x32 = a.x_f32 != 0;
+    typedef float f32x8 __attribute__((ext_vector_type(8)));
+    f32x8 xv[U], x0[U];
     int64_t gr[U];
     int cc[U];
 #pragma unroll
@@ -608,10 +613,25 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
 #pragma unroll
       for (int u = 0; u < U; ++u) gr[u] = gld<int64_t>(a.idx + gr[u]);
     }
+    if (x32) {  // wave-uniform: before the weight stream starts
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      xv[u] = gld<bf16x8>(xg + gr[u] * I + cc[u] * 8);
-      x0[u] = gld<bf16x8>(xg + gr[u] * I);  // the row's start point x[:,0,1:3] (Training_VAE.py:345)
+      for (int u = 0; u < U; ++u) {
+        const f32x4 lo = gld<f32x4>(xg32 + gr[u] * I + cc[u] * 8), hi = gld<f32x4>(xg32 + gr[u] * I + cc[u] * 8 + 4);
+        const f32x4 s0 = gld<f32x4>(xg32 + gr[u] * I);  // the row's start point x[:,0,1:3] (Training_VAE.py:345)
+        xv[u] = f32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        x0[u] = f32x8{s0[0], s0[1], s0[2], s0[3], 0.f, 0.f, 0.f, 0.f};
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bf16x8 v = gld<bf16x8>(xg + gr[u] * I + cc[u] * 8);
+        const bf16x8 v0 = gld<bf16x8>(xg + gr[u] * I);  // the row's start point x[:,0,1:3] (Training_VAE.py:345)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          xv[u][e] = (float)v[e];
+          x0[u][e] = (float)v0[e];
+        }
+      }
     }
     constexpr int NB4 = A::nbias / 4, UB = (NB4 + NT - 1) / NT;
     f32x4 bv[UB];
@@ -676,9 +696,9 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
       if (v < NV) {  // NV % 4 == 0: quads are whole
         const int w = v >> 2, rq = w / VPR, c = w - rq * VPR;
         const int qd = lane & 3, f0 = c * 8;
-        const f32x4 xlo = quad_t(f32x4{(float)xv[u][0], (float)xv[u][1], (float)xv[u][2], (float)xv[u][3]});
-        const f32x4 xhi = quad_t(f32x4{(float)xv[u][4], (float)xv[u][5], (float)xv[u][6], (float)xv[u][7]});
-        const float s0 = (float)x0[u][1], s1 = (float)x0[u][2];
+        const f32x4 xlo = quad_t(f32x4{xv[u][0], xv[u][1], xv[u][2], xv[u][3]});
+        const f32x4 xhi = quad_t(f32x4{xv[u][4], xv[u][5], xv[u][6], xv[u][7]});
+        const float s0 = x0[u][1], s1 = x0[u][2];
         const f32x4 S0 = fchain::quad_all(s0), S1 = fchain::quad_all(s1);
         const int fl = f0 + qd, fh = fl + 4;
         const int dl = fl % D, dh = fh % D;

@@ -132,3 +132,60 @@ def test_peer_exchange_equals_split_step(sizes, tmp_path):
     for k in ("params", "m", "v", "counters"):
         assert torch.equal(got[k], ref[k]), (k, float((got[k].double() - ref[k].double()).abs().max()))
     np.testing.assert_allclose(got["acc"].numpy(), ref["acc"].numpy(), rtol=1e-12)
+
+
+def _train_worker(rank, world, port, n, batch, epochs, out):
+    import torch.distributed as dist
+    import cvae_amd
+    from cvae_amd.train import train
+    os.environ["CVAE_PX_TIMEOUT_MS"] = "30000"
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        x = _data(n).numpy()
+        torch.manual_seed(0)
+        m = cvae_amd.ConditionalTrajectoryVAE(S, D, Z)
+        m.attach(dtype="bf16", max_batch=batch, device="cuda:0", seed=4321)
+        ck = os.path.join(os.path.dirname(out), "ck.pt")
+        model, hist, _ = train(x, S, D, Z, batch_size=batch, epochs=epochs, dtype="bf16", eps="philox", model=m,
+                               log=None, checkpoint_path=ck)
+        if rank == 0:
+            torch.save({"sd": {k: v.cpu() for k, v in model.state_dict().items()}, "hist": hist}, out)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_train_loop_over_peer_exchange(tmp_path):
+    """cvae_amd.train under torch.distributed with the peer exchange (2 ranks sharing the GPU,
+    S=100 D=6 bf16, Philox eps, a checkpoint every epoch: sync_state gathers the owners' state):
+    the loss history and final parameters match one process training on the global batch up to
+    the dW summation order (the two ranks' partials are summed, not reduced in one tile)."""
+    import cvae_amd
+    from cvae_amd.train import train
+    n, batch, epochs = 300, 64, 3
+    out = str(tmp_path / "r0.pt")
+    port = _port()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_train_worker, args=(r, 2, port, n, batch, epochs, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert codes == [0, 0], codes
+    got = torch.load(out, weights_only=True)
+    torch.manual_seed(0)
+    m = cvae_amd.ConditionalTrajectoryVAE(S, D, Z)
+    m.attach(dtype="bf16", max_batch=2 * batch, device="cuda:0", seed=4321)
+    model, hist, _ = train(_data(n).numpy(), S, D, Z, batch_size=2 * batch, epochs=epochs, dtype="bf16",
+                           eps="philox", model=m, log=None)
+    for k in hist:
+        np.testing.assert_allclose(got["hist"][k], hist[k], rtol=1e-3, atol=1e-6)
+    sd = model.state_dict()
+    for k, v in got["sd"].items():
+        ref = sd[k].detach().cpu()
+        err = float((v - ref).norm() / max(float(ref.norm()), 1e-30))
+        assert err < 1e-3, (k, err)

@@ -485,6 +485,44 @@ def test_ring_chain_matches_fast_and_emulation(cvae, monkeypatch, B):
         assert rel_l2(g1[k], ge[k]) < 2e-2, (k, rel_l2(g1[k], ge[k]))
 
 
+@pytest.mark.parametrize("B", [37, 1024])
+def test_ring_chain_fp32_rows_relative_transform(cvae, monkeypatch, B):
+    """The ring chain on fp32 rows (CVAE_X_F32: what the train loop hands it — real data with
+    ~200 m absolute coordinates): the start point is subtracted in fp32 and the offsets rounded to
+    bf16 once, as the generic interpreter does (CVAE_GENERIC=1).  Same rounding points: losses
+    rtol 1e-3, gradients rel-L2 < 1e-2 (fp32 summation orders differ); against bf16 rows of the same
+    data the relative offsets differ (rounded absolute coordinates), so the fp32 path is closer to
+    the fp32 oracle."""
+    torch.manual_seed(0)
+    ref = OracleCVAE(100, 6, 8)
+    monkeypatch.delenv("CVAE_GENERIC", raising=False)
+    m1, e1 = _model(cvae, 100, 6, 8, sd=ref.state_dict(), dtype="bf16", max_batch=max(B, 32))
+    monkeypatch.setenv("CVAE_GENERIC", "1")
+    m2, e2 = _model(cvae, 100, 6, 8, sd=ref.state_dict(), dtype="bf16", max_batch=max(B, 32))
+    monkeypatch.delenv("CVAE_GENERIC")
+    assert e1.train_kernel == "ring" and e2.train_kernel == "generic"
+    gen = torch.Generator().manual_seed(B)
+    x = torch.randn(B, 100, 6, generator=gen)
+    x[:, :, 1] += 180.0 + 40.0 * torch.rand(B, 1, generator=gen)   # absolute world coordinates
+    x[:, :, 2] -= 150.0 + 40.0 * torch.rand(B, 1, generator=gen)
+    eps = torch.randn(B, 8, generator=gen)
+    for e in (e1, e2):
+        e.keep_f32 = True
+    xd = e1.as_input(x, keep_f32=True)
+    assert xd.dtype == torch.float32
+    l1 = e1.forward_backward(xd, eps=eps).cpu().numpy()
+    l2 = e2.forward_backward(xd, eps=eps).cpu().numpy()
+    np.testing.assert_allclose(l1, l2, rtol=1e-3, atol=1e-6)
+    g1, g2 = _grads(m1, e1), _grads(m2, e2)
+    for k in g1:
+        assert rel_l2(g1[k], g2[k]) < 1e-2, (k, rel_l2(g1[k], g2[k]))
+    rel, start = relative(x)
+    r, mu, lv, hc = ref(rel, start, eps)
+    want = np.array([float(v) for v in oracle_loss(r, rel, mu, lv, hc, 0.1, 0.1, 1.0, 1.0)])
+    lb = e1.forward_backward(e1.as_input(x.to(torch.bfloat16)), eps=eps).cpu().numpy()
+    assert np.abs(l1 - want).sum() < np.abs(lb - want).sum(), (l1, lb, want)
+
+
 def test_ring_chain_philox_training_and_determinism(cvae, monkeypatch):
     """In-kernel Philox eps keyed by the global row: the ring chain draws fastchain's noise (same
     losses up to summation order); five training steps (device counters, dW ⊕ Adam behind each
