@@ -30,6 +30,30 @@ __global__ __launch_bounds__(512) void regld(const char* W, int tot, unsigned* s
   if ((acc[0] ^ acc[1] ^ acc[2] ^ acc[3]) == 0x12345678u) sink[0] = 1;
 }
 
+// the same stream with workgroup b starting ROT·b bytes further into its slice (wrapping): the 64
+// workgroups no longer request the same lines at the same moment (hot L2 channels); PRIV: each
+// workgroup streams its own copy of the buffer (no sharing at all)
+template <int PF, bool PRIV>
+__global__ __launch_bounds__(512) void regld_rot(const char* W, int tot, int rot, unsigned* sink) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int per_wave = tot / 8;
+  const char* p = W + (PRIV ? (size_t)blockIdx.x * tot : 0) + (size_t)wave * per_wave + lane * 16;
+  const int r0 = (int)(((long)blockIdx.x * rot) % per_wave) & ~1023;
+  u32x4 acc = {0, 0, 0, 0};
+  for (int off = 0; off < per_wave; off += PF * 1024) {
+    u32x4 v[PF];
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      int o = off + u * 1024 + r0;
+      o = o >= per_wave ? o - per_wave : o;
+      v[u] = *(const G u32x4*)(p + o);
+    }
+#pragma unroll
+    for (int u = 0; u < PF; ++u) acc ^= v[u];
+  }
+  if ((acc[0] ^ acc[1] ^ acc[2] ^ acc[3]) == 0x12345678u) sink[0] = 1;
+}
+
 template <int L>
 __global__ __launch_bounds__(64 * L) void glds(const char* W, int tot, unsigned* sink) {
   __shared__ __attribute__((aligned(16))) char ring[65536];
@@ -83,6 +107,9 @@ int main() {
   char *W, *out;
   unsigned* sink;
   hipMalloc(&W, TOT);
+  char* WP;
+  hipMalloc(&WP, (size_t)TOT * 64);
+  hipMemset(WP, 1, (size_t)TOT * 64);
   hipMalloc(&out, (size_t)STOT * 64);
   hipMalloc(&sink, 4);
   hipMemset(W, 1, TOT);
@@ -95,6 +122,16 @@ int main() {
   rep("regld PF=8", timeit([&] { hipLaunchKernelGGL(regld<8>, dim3(64), dim3(512), 0, 0, W, TOT, sink); }), TOT);
   rep("regld PF=16", timeit([&] { hipLaunchKernelGGL(regld<16>, dim3(64), dim3(512), 0, 0, W, TOT, sink); }), TOT);
   rep("regld PF=8 x256 WG", timeit([&] { hipLaunchKernelGGL(regld<8>, dim3(256), dim3(512), 0, 0, W, TOT, sink); }), TOT);
+  for (int rot : {1024, 4096, 16384, 40960})
+    for (int pf : {4, 8}) {
+      char name[64];
+      snprintf(name, sizeof name, "regld PF=%d rot %d KB/WG", pf, rot / 1024);
+      rep(name, timeit([&] {
+            if (pf == 4) hipLaunchKernelGGL((regld_rot<4, false>), dim3(64), dim3(512), 0, 0, W, TOT, rot, sink);
+            else hipLaunchKernelGGL((regld_rot<8, false>), dim3(64), dim3(512), 0, 0, W, TOT, rot, sink);
+          }), TOT);
+    }
+  rep("regld PF=8 private copies", timeit([&] { hipLaunchKernelGGL((regld_rot<8, true>), dim3(64), dim3(512), 0, 0, WP, TOT, 0, sink); }), TOT);
   rep("glds L=1", timeit([&] { hipLaunchKernelGGL(glds<1>, dim3(64), dim3(64), 0, 0, W, TOT, sink); }), TOT);
   rep("glds L=2", timeit([&] { hipLaunchKernelGGL(glds<2>, dim3(64), dim3(128), 0, 0, W, TOT, sink); }), TOT);
   rep("glds L=4", timeit([&] { hipLaunchKernelGGL(glds<4>, dim3(64), dim3(256), 0, 0, W, TOT, sink); }), TOT);
