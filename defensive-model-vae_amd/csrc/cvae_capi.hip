@@ -1292,10 +1292,11 @@ struct PxBlob {
 };
 constexpr int PX_MAGIC = 0x43505831;  // "CPX1"
 int px_tiles(const cvae_handle*) { return fchain::Tiles<19>::total(); }
-// bound of every exchange wait: CVAE_PX_TIMEOUT_MS (default 2000 ms), in s_memrealtime ticks
+// bound of every exchange wait: CVAE_PX_TIMEOUT_MS (default 10000 ms: ranks of a real
+// multi-GPU job may enter their first exchange seconds apart), in s_memrealtime ticks
 uint64_t px_timeout_ticks() {
   const char* e = std::getenv("CVAE_PX_TIMEOUT_MS");
-  const double ms = e ? std::atof(e) : 2000.0;
+  const double ms = e ? std::atof(e) : 10000.0;
   return (uint64_t)(std::max(1.0, ms) * 1e5);
 }
 

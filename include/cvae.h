@@ -332,7 +332,7 @@ int cvae_px_probe(cvae_handle* h, int* ok);
 /* This rank's exchange wait statistics since set-up or the last reset, in 10-ns ticks: out[0] the
  * longest owner-tile wait for the other ranks' partials, out[1] the longest end-of-launch wait for
  * the other owners' operand copies, out[2] the sum and out[3] the number of owner-tile waits.
- * Every wait is bounded by CVAE_PX_TIMEOUT_MS (default 2000); a time-out sets the fault word to 2
+ * Every wait is bounded by CVAE_PX_TIMEOUT_MS (default 10000); a time-out sets the fault word to 2
  * (owner tile) or 3 (end of launch).  Synchronises the device. */
 int cvae_px_stats(cvae_handle* h, uint64_t* out, int reset);
 
