@@ -21,6 +21,7 @@
 // that each operand copy is written as whole 16-B MFMA fragments (1 KB per wave instruction)
 // instead of 2-B element stores scattered over the fragment layout.
 #pragma once
+#include <type_traits>
 #include "cvae_device.h"
 #include "cvae_peer.h"
 
@@ -396,15 +397,24 @@ struct SplitK {
   int pw;             // floats per partial (0: 32·TW + 32 of the tile)
 };
 
+// A wait inside the launch before the arena rows are read (cvae_fusedring.h): gate() returns false
+// on a time-out (the block then skips its update).  NoGate: the rows are final at launch.
+struct NoGate {
+  static constexpr bool gated = false;
+  __device__ bool operator()() const { return true; }
+};
+
 // One workgroup = tile td of layer L: 32 outputs × 32·NI inputs (NI = 2: two 32-wide input tiles
 // sharing the G rows).  loss_block: this workgroup also finishes the loss (S, D, Z: its shape).
 // SC1: the arena rows were handed over inside the launch (fused_step_kernel): every load of them
-// is an sc1 buffer load.
-template <typename T, int MODE, bool SC1 = false, int NI = 1>
+// is an sc1 buffer load.  gate (gated): called after the master-state loads are issued, before
+// any operand load; the step's Adam scalars are then read after it (sc1), not first.
+template <typename T, int MODE, bool SC1 = false, int NI = 1, class Gate = NoGate>
 __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td, int Bk, AdamArgs aa,
                                            const LossArgs& la, bool loss_block, int S, int D, int Z,
                                            float* red, float* dbp, SplitK sk = SplitK{1, 0, nullptr, nullptr, 0},
-                                           const PeerArgs* px = nullptr) {
+                                           const PeerArgs* px = nullptr, Gate&& gate = Gate{}) {
+  constexpr bool GATED = std::remove_reference_t<Gate>::gated;
   using V = typename Op<T>::V;
   constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC;
   constexpr int NX = 2 * NI, TW = 32 * NI, LD = TW + 4;  // X fragments per chunk, tile width, image stride
@@ -419,8 +429,8 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
   using VE = typename VecF<EPT>::T;
   const int o = tid / TPR, iv = (tid % TPR) * EPT;
 
-  WSTAMP(0);
-  const adam_f32x2 t_step = MODE == PM_ADAM ? adam_step_load(aa) : adam_f32x2{0.f, 0.f};
+  if (!GATED) WSTAMP(0);  // gated: the stamp marks the end of the wait
+  adam_f32x2 t_step = MODE == PM_ADAM && !GATED ? adam_step_load(aa) : adam_f32x2{0.f, 0.f};
   f32x4 acc[2][NX];
 #pragma unroll
   for (int m = 0; m < 2; ++m)
@@ -474,6 +484,13 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
   if (tid < 32 * TPR) st = loadn<MODE, EPT>(L, td.o0 + o, td.i0 + iv, aa);
   PreB sb = {0.f, 0.f, 0.f, -1};
   if (bias_tile && tid < 32) sb = loadb<MODE>(L, td.o0 + tid, aa);
+  if constexpr (GATED) {
+    if (!gate()) return;  // block-uniform
+    WSTAMP(0);
+    if (MODE == PM_ADAM && aa.ctr)
+      t_step = __builtin_bit_cast(adam_f32x2, __hip_atomic_load((const uint64_t*)(aa.ctr + 2), __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_AGENT));
+  }
 #pragma unroll
   for (int u = 0; u < PF; ++u) load(u, u);
   // device-counter path: this step's Adam scalars (double pow), computed while the operands load

@@ -287,6 +287,17 @@ int cvae_bench_kernels(cvae_handle* h, const void* x, const int64_t* idx, int ba
  * the device. */
 int cvae_sync_words(cvae_handle* h, unsigned* out);
 
+/* The one-launch training step of the reference architecture at S = 100 (the ring chain, every
+ * dW ⊕ Adam tile and the loss block in ONE kernel; replaces the chain + dW pair of
+ * cvae_train_step when enabled — CVAE_FUSE_RING at handle creation):
+ * *launches = the kernels one cvae_train_step launches on this handle (1 or 2). */
+int cvae_step_launches(const cvae_handle* h, int* launches);
+
+/* Its ten self-resetting hand-off words, copied to `out` (host, 10 entries): the 8 replicas of the
+ * ready counter, the done counter, the sticky time-out flag.  Between launches the first nine are
+ * zero.  Synchronises the device. */
+int cvae_ring_sync_words(cvae_handle* h, unsigned* out);
+
 /* The handle's sticky fault word.  A kernel that waits on a hand-off (the fused launch's tiles, the
  * peer exchange) waits a bounded time; on a time-out it skips its update and sets this word in
  * pinned host memory.  Every later training call (cvae_train_step[s], cvae_train_fwd_bwd, cvae_adam)
