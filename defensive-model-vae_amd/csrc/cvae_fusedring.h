@@ -83,7 +83,8 @@ __global__ __launch_bounds__(NT, 4) void fused_ring_kernel(char* arena, const vo
   using TL = fchain::Tiles<19>;
   constexpr int NTL = TL::total();
   static_assert(sizeof(WgradLds<1>) + 16 <= A::L_TOTAL, "the tiles' reduction image fits the chain's LDS");
-  int tb = (int)blockIdx.x - f.nchain;
+  // blocks nchain .. NTL-1: tiles 0 .. NTL-nchain-1; block NTL: the loss block (tb == NTL)
+  int tb = (int)blockIdx.x == NTL ? NTL : (int)blockIdx.x - f.nchain;
   if ((int)blockIdx.x < f.nchain) {
     RowArgs ra = a;
     ra.x = x;

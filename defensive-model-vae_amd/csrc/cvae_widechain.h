@@ -1137,7 +1137,8 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   if (pub) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lbar();
-    if (CVAE_DIAG_STAMPS && tid == 0 && stamp_i < 64) STAMPS[stamp_i++] = __builtin_amdgcn_s_memrealtime();
+    if (CVAE_DIAG_STAMPS && tid == 0 && stamp_i < 64) STAMPS[stamp_i] = __builtin_amdgcn_s_memrealtime();
+    if (CVAE_DIAG_STAMPS) ++stamp_i;
     if (tid < 8) __hip_atomic_fetch_add(pub + 32 * tid, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (CVAE_DIAG_STAMPS && a.stamps && tid < 64)
