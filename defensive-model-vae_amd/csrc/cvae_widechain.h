@@ -232,6 +232,18 @@ struct Plan {
 #ifndef CVAE_RING_SKIP
 #define CVAE_RING_SKIP 1
 #endif
+#ifndef CVAE_DIAG_NOPHILOX
+#define CVAE_DIAG_NOPHILOX 0  // timing only: eps = 0 without the Philox draws
+#endif
+#ifndef CVAE_EPS_W0
+#define CVAE_EPS_W0 1  // small latent (SZ): only wave 0 (whose lanes hold mu, logvar) draws eps
+#endif
+#ifndef CVAE_EPS_PRO
+#define CVAE_EPS_PRO 1  // small latent (SZ): the eps draw in the prologue, not in the encoder-L1 GEMM
+#endif
+#ifndef CVAE_WARM
+#define CVAE_WARM 0  // A/B option: prologue L2 warm-up of E0's (1) and the last decoder layer's (2) fragments
+#endif
 template <int P>
 struct Ring {
   bf16x8 r[P];
@@ -589,7 +601,36 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   const uint64_t rng_off = a.ctr ? *(const __attribute__((address_space(4))) uint64_t*)a.ctr : a.offset;
 
   Ring<P> ring;
+  uint32_t warm = 0;  // CVAE_WARM only
   float s_recon = 0.f, s_kl = 0.f, s_start = 0.f, s_t0 = 0.f, s_relu = 0.f;
+
+  // eps of the reparameterisation (:199-206), per mu tile k of this lane (latent j, rows 4q..4q+3):
+  // host-given (loaded unconditionally — rows clamped into the batch, any valid address when eps
+  // is drawn in-kernel — a load under a branch drains the weight stream) or Philox keyed by the
+  // global row (data parallelism: eps_row0 = the rank's first row).  The Philox draws (integer
+  // multiplies and transcendentals, ~0.3 us of VALU per wave) run inside the stream-bound
+  // encoder-L1 GEMM, or (SZ, CVAE_EPS_PRO) in the prologue while the x tile is in flight.
+  // SZ: one tile of latents, held by wave 0's lanes n16 < Z (CVAE_EPS_W0: only wave 0 draws)
+  constexpr int NZT = A::SZ ? 1 : Z / 128;
+  f32x4 ep[NZT];
+  const int rowq = 4 * q + (n16 & 3);  // the row this lane draws (4 latents) before the quad transpose
+  auto eps_j0 = [&](int k) { return A::SZ ? min(4 * (n16 >> 2), Z - 4) : 16 * (wave + NW * k) + 4 * (n16 >> 2); };
+  auto eps_load = [&](int k) {
+    const int j0 = eps_j0(k);
+    const float* const ebase = a.eps ? a.eps : (const float*)(AR + A::bias_base);  // global memory either way
+    const int erow = a.eps ? min(b0 + rowq, max(a.batch - 1, 0)) : 0;
+    return gld<f32x4>(ebase + (a.eps ? (size_t)erow * Z + j0 : 0));
+  };
+  auto eps_make = [&](auto kk, f32x4 eh) {
+    constexpr int k = decltype(kk)::value;
+    const int j0 = eps_j0(k);
+    f32x4 e = a.eps ? eh : philox_normal4(a.seed, rng_off, (uint32_t)(a.eps_row0 + b0 + rowq), (uint32_t)j0);
+    if (rowq >= nrows) e = f32x4{0.f, 0.f, 0.f, 0.f};
+    ep[k] = quad_t(e);
+  };
+  auto draw_eps = [&](auto kk) { eps_make(kk, eps_load(decltype(kk)::value)); };
+  constexpr bool EPS_PRO = A::SZ && CVAE_EPS_PRO;  // the draw sits in the prologue
+  const bool eps_mine = !A::SZ || !CVAE_EPS_W0 || wave == 0;  // wave-uniform
 
   // ---- prologue: x tile (relative transform, Training_VAE.py:345-348), biases, LDS pads
   // x_f32 (CVAE_X_F32: real data with ~200 m absolute coordinates): fp32 rows, the start point
@@ -636,6 +677,9 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
         }
       }
     }
+    // EPS_PRO: the host-eps load right behind the x tile (the x wait then covers it)
+    f32x4 eh0 = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (EPS_PRO) eh0 = eps_load(0);
     constexpr int NB4 = A::nbias / 4, UB = (NB4 + NT - 1) / NT;
     f32x4 bv[UB];
 #pragma unroll
@@ -663,6 +707,24 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     }
     // the weight stream queues behind the x tile and the biases (vmcnt retires in order)
     ring_fill<A, P>(ring, AR, wave, lane);
+    if constexpr (EPS_PRO) {  // the Philox VALU issues while the x tile is in flight
+      if (CVAE_DIAG_NOPHILOX || !eps_mine) ep[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+      else eps_make(integral_constant<int, 0>{}, eh0);
+    }
+    if constexpr (CVAE_WARM > 0) {
+      // L2 warm-up (A/B option): the Adam step rewrote every operand copy, so each XCD's L2 meets
+      // the stream's first lines cold.  The 8 blocks of an XCD (blk ≡ x mod 8) touch one dword per
+      // 128-B line of the big GEMMs' fragments, 1/8 each, one lane per line, behind the ring fill
+      // (in-order vmcnt: no earlier wait covers them); the value is kept live to the kernel's end
+      auto touch = [&](int64_t lo, int64_t bytes) {
+        const int nl = (int)((bytes + 127) / 128), j = (blk >> 3) & 7, per = (nl + 7) / 8;
+        const int l0 = j * per, n = min(per, nl - l0);
+        for (int k = lane; k < n; k += 64) warm |= gld<uint32_t>((const uint32_t*)(AR + lo + 128LL * (l0 + k)));
+      };
+      if (wave == 0) touch(A::wf(A::LE0), 2LL * A::Np(A::LE0) * A::Kp(A::LE0));
+      if (CVAE_WARM > 1 && wave == 1) touch(A::wf(A::LDL), 2LL * A::Np(A::LDL) * A::Kp(A::LDL));
+      if (CVAE_WARM > 1 && wave == 2) touch(A::wb(A::LDL), 2LL * A::Np(A::LDL) * A::Kp(A::LDL));
+    }
     // device counters: this launch begins optimizer step ctr[1] + 1 and precomputes its Adam
     // scalars for the dW kernel behind it.  Wave 0 of block 0, wave-uniformly, while it waits for
     // the x tile: the step count by scalar load, the f64 pow on every lane, one lane stores (at
@@ -759,29 +821,14 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   constexpr int XR = (2 * Ip + NT - 1) / NT;
   static_assert(XR <= 5 && NE >= 4, "the x_rel copy runs over C0|E0, C1|E1, E2, E3");
 
-  // eps of the reparameterisation (:199-206), per mu tile k of this lane (latent j, rows 4q..4q+3):
-  // host-given (loaded unconditionally — rows clamped into the batch, any valid address when eps
-  // is drawn in-kernel — a load under a branch drains the weight stream) or Philox keyed by the
-  // global row (data parallelism: eps_row0 = the rank's first row).  The Philox draws (integer
-  // multiplies, ~1 us of VALU per wave) run inside the stream-bound encoder-L1 GEMM.
-  // SZ: one tile of latents, held by wave 0's lanes n16 < Z (every wave draws; only wave 0's count)
-  constexpr int NZT = A::SZ ? 1 : Z / 128;
-  f32x4 ep[NZT];
-  const int rowq = 4 * q + (n16 & 3);  // the row this lane draws (4 latents) before the quad transpose
-  auto draw_eps = [&](auto kk) {
-    constexpr int k = decltype(kk)::value;
-    const int j0 = A::SZ ? min(4 * (n16 >> 2), Z - 4) : 16 * (wave + NW * k) + 4 * (n16 >> 2);
-    const float* const ebase = a.eps ? a.eps : (const float*)(AR + A::bias_base);  // global memory either way
-    const int erow = a.eps ? min(b0 + rowq, max(a.batch - 1, 0)) : 0;
-    const f32x4 eh = gld<f32x4>(ebase + (a.eps ? (size_t)erow * Z + j0 : 0));
-    f32x4 e = a.eps ? eh : philox_normal4(a.seed, rng_off, (uint32_t)(a.eps_row0 + b0 + rowq), (uint32_t)j0);
-    if (rowq >= nrows) e = f32x4{0.f, 0.f, 0.f, 0.f};
-    ep[k] = quad_t(e);
-  };
   constexpr int ES = PL::step(PL::sE0).F8 ? 4 : 8;  // encoder-L1 K items between two draws
   auto eps_side = [&](auto cc) {
     constexpr int c = decltype(cc)::value;
-    if constexpr (c % ES == 2 && c / ES < NZT) draw_eps(integral_constant<int, c / ES>{});
+    if constexpr (!EPS_PRO && c % ES == 2 && c / ES < NZT) {
+      if (CVAE_DIAG_NOPHILOX) ep[c / ES] = f32x4{0.f, 0.f, 0.f, 0.f};  // timing only
+      else if (eps_mine) draw_eps(integral_constant<int, c / ES>{});
+      else ep[c / ES] = f32x4{0.f, 0.f, 0.f, 0.f};  // SZ: only wave 0's lanes hold the latents
+    }
   };
   static_assert(ES * (NZT - 1) + 2 < PL::step(PL::sE0).KC, "the eps draws fit in the encoder-L1 GEMM");
 
@@ -1134,6 +1181,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     __hip_atomic_store((unsigned*)(a.partials + blk * 8 + tid), __builtin_bit_cast(unsigned, s), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);  // sc1: the fused step's loss block reads it
   }
+  if constexpr (CVAE_WARM > 0) asm volatile("" ::"v"(warm));
   if (pub) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lbar();
