@@ -241,6 +241,9 @@ struct Plan {
 #ifndef CVAE_EPS_PRO
 #define CVAE_EPS_PRO 1  // small latent (SZ): the eps draw in the prologue, not in the encoder-L1 GEMM
 #endif
+#ifndef CVAE_DIAG_NOADAMPRE
+#define CVAE_DIAG_NOADAMPRE 0  // timing only: no Adam-scalar precompute in block 0
+#endif
 #ifndef CVAE_WARM
 #define CVAE_WARM 0  // A/B option: prologue L2 warm-up of E0's (1) and the last decoder layer's (2) fragments
 #endif
@@ -248,6 +251,25 @@ template <int P>
 struct Ring {
   bf16x8 r[P];
 };
+
+#ifndef CVAE_RING_BUF
+#define CVAE_RING_BUF 1
+#endif
+// one 16-B piece of fragment item at byte offset `off` from the arena base.  CVAE_RING_BUF: a
+// buffer load — lane·16 is a loop-invariant voffset, the item's offset a scalar soffset (2-3 SALU
+// per item); the 64-bit global address cost 3 VALU (one a 64-bit shift-add) + ~7 SALU per item
+// (cfg2 step 26.6 -> 26.0 us, profiles/r03g).  Not in the e4m3 form (F8): there the buffer-load
+// build failed the wide fp8 chain's run-to-run repeatability test (two runs of two, the global-load
+// build passing), cause not found — kept on global loads
+template <bool F8>
+__device__ __forceinline__ bf16x8 wload(const char* AR, int64_t off, int lane) {
+  if constexpr (CVAE_RING_BUF && !F8) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)AR, (short)0, 0x7fffffff, 0x00020000);
+    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, (int)off, 0));
+  } else {
+    return gld<bf16x8>(AR + off + lane * 16);
+  }
+}
 
 // stream item G of this wave → ring slot G % P (no-op past the end of the stream)
 template <class A, int P, int G>
@@ -267,13 +289,13 @@ __device__ __forceinline__ void ring_load(Ring<P>& ring, const char* AR, int wav
     const int64_t frag = st.KS ? w + NW * kc : t * st.KC + kc;  // KS: tile 0, chunk = wave + 8·item
     if constexpr (st.KS && NW * (kc + 1) > A::FC_KCH) {
       // a K chunk past the layer (wave-uniform): no load, and gemm skips its MFMA
-      if (w + NW * kc < A::FC_KCH) ring.r[G % P] = gld<bf16x8>(AR + base + frag * 1024 + lane * 16);
+      if (w + NW * kc < A::FC_KCH) ring.r[G % P] = wload<A::F8>(AR, base + frag * 1024, lane);
     } else if constexpr (CVAE_RING_SKIP && !st.KS && NW * (slot + 1) > st.NTL) {
       // a slot past the layer's tiles: no load (wave-uniform); the stale ring register feeds an
       // MFMA whose result the epilogue drops
-      if (w + NW * slot < st.NTL) ring.r[G % P] = gld<bf16x8>(AR + base + frag * 1024 + lane * 16);
+      if (w + NW * slot < st.NTL) ring.r[G % P] = wload<A::F8>(AR, base + frag * 1024, lane);
     } else {
-      ring.r[G % P] = CVAE_DIAG_NOWLOAD ? bf16x8{} : gld<bf16x8>(AR + base + frag * 1024 + lane * 16);
+      ring.r[G % P] = CVAE_DIAG_NOWLOAD ? bf16x8{} : wload<A::F8>(AR, base + frag * 1024, lane);
     }
   }
 }
@@ -729,10 +751,10 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     // scalars for the dW kernel behind it.  Wave 0 of block 0, wave-uniformly, while it waits for
     // the x tile: the step count by scalar load, the f64 pow on every lane, one lane stores (at
     // the kernel's end, one lane's f64 pow delays the chain's completion)
-    if (a.ctr && blk == 0 && wave == 0) {
+    if (a.ctr && blk == 0 && wave == NW - 1) {  // wave 0 draws eps (EPS_PRO): another SIMD
       const uint64_t t = *(const __attribute__((address_space(4))) uint64_t*)(a.ctr + 1) + 1;
       float s0 = 0.f, s1 = 0.f;
-      if (a.adam_pre) adam_scalars(a.lr, a.beta1, a.beta2, (double)t, s0, s1);
+      if (a.adam_pre && !CVAE_DIAG_NOADAMPRE) adam_scalars(a.lr, a.beta1, a.beta2, (double)t, s0, s1);
       if (lane == 0) {  // write-through (sc1): the fused step's dW tiles on other XCDs read them
         __hip_atomic_store(a.ctr + 1, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (a.adam_pre)

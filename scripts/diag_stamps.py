@@ -61,7 +61,12 @@ if os.environ.get("RING") == "1":  # the reference architecture on the ring chai
     if os.environ.get("CVAE_FUSE_RING") == "1":  # the one-launch step: E1b|C1b ends at the drain stamp
         names = names[:-2] + ["E1b|C1b+drain"]
 for i in range(k - 1):
-    print(f"{names[i]:>14s} {i:2d}: median {np.median(d[:, i]) / 1000:7.3f} us   max {d[:, i].max() / 1000:7.3f} us")
+    print(f"{names[i]:>14s} {i:2d}: median {np.median(d[:, i]) / 1000:7.3f} us   max {d[:, i].max() / 1000:7.3f} us"
+          f"   block0 {d[0, i] / 1000:7.3f} us")
+ends = (st[:, k - 1] - t0) * 10 / 1000
+starts = (st[:, 0] - t0) * 10 / 1000
+print(f"block ends (us after the first start): block0 {ends[0]:.2f}  median {np.median(ends):.2f}  max {ends.max():.2f}"
+      f" (block {int(ends.argmax())});  block0 start {starts[0]:.2f}")
 
 w = wbuf.view(NT, 8).cpu().numpy().astype(np.int64)
 wid = np.nonzero(w[:, 0] > 0)[0]  # fused launch: tile blocks follow the row-chain blocks
