@@ -252,6 +252,9 @@ struct Ring {
   bf16x8 r[P];
 };
 
+#ifndef CVAE_RING_SADDR
+#define CVAE_RING_SADDR 1  // e4m3 form: scalar-base global loads (see wload)
+#endif
 #ifndef CVAE_RING_BUF
 #define CVAE_RING_BUF 1
 #endif
@@ -260,12 +263,19 @@ struct Ring {
 // per item); the 64-bit global address cost 3 VALU (one a 64-bit shift-add) + ~7 SALU per item
 // (cfg2 step 26.6 -> 26.0 us, profiles/r03g).  Not in the e4m3 form (F8): there the buffer-load
 // build failed the wide fp8 chain's run-to-run repeatability test (two runs of two, the global-load
-// build passing), cause not found — kept on global loads
+// build passing), cause not found.  F8 (CVAE_RING_SADDR): global loads with a scalar 64-bit base
+// and a 32-bit lane offset where the compiler keeps that form (2 SALU, 0 VALU per item): chain
+// 41.4 -> 40.5 us at cfg5 fp8, repeatability tests green (profiles/r03g/saddr_ab.txt)
 template <bool F8>
 __device__ __forceinline__ bf16x8 wload(const char* AR, int64_t off, int lane) {
   if constexpr (CVAE_RING_BUF && !F8) {
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)AR, (short)0, 0x7fffffff, 0x00020000);
     return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, (int)off, 0));
+  } else if constexpr (CVAE_RING_SADDR) {  // global_load with a scalar base + a 32-bit lane offset
+    typedef const __attribute__((address_space(1))) char* gchar;
+    gchar p = (gchar)(AR + off);
+    asm volatile("" : "+s"(p));
+    return *(const __attribute__((address_space(1))) bf16x8*)(p + (uint32_t)(lane * 16));
   } else {
     return gld<bf16x8>(AR + off + lane * 16);
   }

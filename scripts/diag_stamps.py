@@ -58,6 +58,10 @@ if WIDE:
 if os.environ.get("RING") == "1":  # the reference architecture on the ring chain (CVAE_KERNEL_RING)
     names = (["prologue", "C0|E0", "C1|E1", "E2", "E3", "FC", "reparam", "D0", "D1", "D2", "D3+loss", "fixup",
               "D3b", "D2b", "D1b", "D0b", "FCb", "E3b", "E2b", "E1b|C1b", "partials"])
+    if os.environ.get("SUB") == "1":  # CVAE_DIAG_STAMPS=2: stamps inside the prologue, C0|E0 and FCb
+        names = (["pro:issue", "pro:transform", "pro:bar", "C0+copies", "E0 gemm", "E0 epi", "C1|E1", "E2", "E3",
+                  "FC", "reparam", "D0", "D1", "D2", "D3+loss", "fixup", "D3b", "D2b", "D1b", "D0b", "FCb gemm",
+                  "FCb epi", "E3b", "E2b", "E1b|C1b", "partials"])
     if os.environ.get("CVAE_FUSE_RING") == "1":  # the one-launch step: E1b|C1b ends at the drain stamp
         names = names[:-2] + ["E1b|C1b+drain"]
 for i in range(k - 1):
