@@ -252,6 +252,15 @@ struct Ring {
   bf16x8 r[P];
 };
 
+#ifndef CVAE_PRE_FILL
+// ring items issued in front of the x-tile wait, the rest after the transform: fewer weight lines
+// compete with the x tile's (cfg2 step -0.25 us against the whole fill in front, 0 in front -0.1;
+// profiles/r03g/prologue_ab.txt)
+#define CVAE_PRE_FILL 4
+#endif
+#ifndef CVAE_X0_8B
+#define CVAE_X0_8B 1  // the start point of a row by an 8-B load (elements 0..3) instead of 16 B
+#endif
 #ifndef CVAE_RING_SADDR
 #define CVAE_RING_SADDR 1  // e4m3 form: scalar-base global loads (see wload)
 #endif
@@ -633,6 +642,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   const uint64_t rng_off = a.ctr ? *(const __attribute__((address_space(4))) uint64_t*)a.ctr : a.offset;
 
   Ring<P> ring;
+  constexpr int PF0 = CVAE_PRE_FILL < P ? CVAE_PRE_FILL : P;  // ring items issued before the x-tile wait
   uint32_t warm = 0;  // CVAE_WARM only
   float s_recon = 0.f, s_kl = 0.f, s_start = 0.f, s_t0 = 0.f, s_relu = 0.f;
 
@@ -701,11 +711,17 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const bf16x8 v = gld<bf16x8>(xg + gr[u] * I + cc[u] * 8);
-        const bf16x8 v0 = gld<bf16x8>(xg + gr[u] * I);  // the row's start point x[:,0,1:3] (Training_VAE.py:345)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          xv[u][e] = (float)v[e];
-          x0[u][e] = (float)v0[e];
+        for (int e = 0; e < 8; ++e) xv[u][e] = (float)v[e];
+        // the row's start point x[:,0,1:3] (Training_VAE.py:345): elements 0..3 (8 B) or 0..7 (16 B)
+        if constexpr (CVAE_X0_8B) {
+          const bf16x4 v0 = gld<bf16x4>(xg + gr[u] * I);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x0[u][e] = e < 4 ? (float)v0[e & 3] : 0.f;
+        } else {
+          const bf16x8 v0 = gld<bf16x8>(xg + gr[u] * I);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x0[u][e] = (float)v0[e];
         }
       }
     }
@@ -738,7 +754,8 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
       if (tid < 2 * A::Np(A::LCE) * A::Kp(A::LCE) / 16) tab = gld<u32x4>(AR + A::wf(A::LCE) + 16 * tid);
     }
     // the weight stream queues behind the x tile and the biases (vmcnt retires in order)
-    ring_fill<A, P>(ring, AR, wave, lane);
+    // the first PF0 items of the stream here, the rest after the x-tile transform (CVAE_PRE_FILL)
+    sfor<0, PF0>([&](auto g) { ring_load<A, P, decltype(g)::value>(ring, AR, wave, lane); });
     if constexpr (EPS_PRO) {  // the Philox VALU issues while the x tile is in flight
       if (CVAE_DIAG_NOPHILOX || !eps_mine) ep[0] = f32x4{0.f, 0.f, 0.f, 0.f};
       else eps_make(integral_constant<int, 0>{}, eh0);
@@ -820,6 +837,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
       }
     }
   }
+  sfor<PF0, P>([&](auto g) { ring_load<A, P, decltype(g)::value>(ring, AR, wave, lane); });
   sub();
   bar();
   if constexpr (A::CLS) {
