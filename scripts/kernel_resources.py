@@ -12,7 +12,7 @@ import sys
 import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, "defensive-model-vae_amd", "cvae_amd", "libcvae_hip.so")
+LIB = os.environ.get("CVAE_LIB") or os.path.join(ROOT, "defensive-model-vae_amd", "cvae_amd", "libcvae_hip.so")
 LLVM = "/opt/rocm/lib/llvm/bin"
 
 
@@ -34,9 +34,11 @@ def code_objects(blob):
     return out
 
 
-def main():
-    pats = sys.argv[1:]
-    blob = open(LIB, "rb").read()
+def resources(lib=LIB, pats=()):
+    """[{name, demangled, vgpr, sgpr, lds, scratch, wg}] of every kernel (whose mangled name contains
+    one of `pats`, when given) in the library's gfx950 code objects."""
+    blob = open(lib, "rb").read()
+    out = []
     for co in code_objects(blob):
         with tempfile.NamedTemporaryFile(suffix=".co") as f:
             f.write(co)
@@ -46,12 +48,19 @@ def main():
             name = re.search(r"\.name:\s+(\S+)", k)
             if not name or (pats and not any(p in name.group(1) for p in pats)):
                 continue
-            g = lambda key: (re.search(rf"\.{key}:\s+(\S+)", k) or [None, "?"])[1]  # noqa: E731
+            g = lambda key: (re.search(rf"\.{key}:\s+(\S+)", k) or [None, "-1"])[1]  # noqa: E731
             dem = subprocess.run(["c++filt"], input=name.group(1), capture_output=True,
                                  text=True).stdout.strip()
-            print(f"vgpr {g('vgpr_count'):>4} agpr {k.split()[0] if k.split() else '?':>4} sgpr {g('sgpr_count'):>3} "
-                  f"lds {g('group_segment_fixed_size'):>6} scratch {g('private_segment_fixed_size'):>5} "
-                  f"wg {g('max_flat_workgroup_size'):>4}  {dem[:150]}")
+            out.append({"name": name.group(1), "demangled": dem, "vgpr": int(g("vgpr_count")),
+                        "sgpr": int(g("sgpr_count")), "lds": int(g("group_segment_fixed_size")),
+                        "scratch": int(g("private_segment_fixed_size")), "wg": int(g("max_flat_workgroup_size"))})
+    return out
+
+
+def main():
+    for r in resources(LIB, sys.argv[1:]):
+        print(f"vgpr {r['vgpr']:>4} sgpr {r['sgpr']:>3} lds {r['lds']:>6} scratch {r['scratch']:>5} "
+              f"wg {r['wg']:>4}  {r['demangled'][:150]}")
 
 
 if __name__ == "__main__":
