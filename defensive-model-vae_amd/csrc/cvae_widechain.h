@@ -244,6 +244,12 @@ struct Plan {
 #ifndef CVAE_DIAG_NOADAMPRE
 #define CVAE_DIAG_NOADAMPRE 0  // timing only: no Adam-scalar precompute in block 0
 #endif
+#ifndef CVAE_EPS_PRO_WIDE
+// wide latent: eps draws per wave moved from the E0 GEMM to the prologue — 2 of 4 in the e4m3 form
+// (half the E0 bytes: its GEMM is VALU-bound, step 54.8 -> 54.2 us), none in bf16 (its E0 is
+// stream-bound; the prologue only grows: +0.3-0.9 us; profiles/r03i/epswide_ab_*.txt)
+#define CVAE_EPS_PRO_WIDE (A::F8 ? 2 : 0)
+#endif
 #ifndef CVAE_WARM
 #define CVAE_WARM 0  // A/B option: prologue L2 warm-up of E0's (1) and the last decoder layer's (2) fragments
 #endif
@@ -672,6 +678,8 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   };
   auto draw_eps = [&](auto kk) { eps_make(kk, eps_load(decltype(kk)::value)); };
   constexpr bool EPS_PRO = A::SZ && CVAE_EPS_PRO;  // the draw sits in the prologue
+  // wide latent (NZT tiles per wave): draws 0 .. NPRO-1 in the prologue, the rest in the E0 GEMM
+  constexpr int NPRO = EPS_PRO ? 1 : A::SZ ? 0 : (CVAE_EPS_PRO_WIDE < NZT ? CVAE_EPS_PRO_WIDE : NZT);
   const bool eps_mine = !A::SZ || !CVAE_EPS_W0 || wave == 0;  // wave-uniform
 
   // ---- prologue: x tile (relative transform, Training_VAE.py:345-348), biases, LDS pads
@@ -726,8 +734,8 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
       }
     }
     // EPS_PRO: the host-eps load right behind the x tile (the x wait then covers it)
-    f32x4 eh0 = {0.f, 0.f, 0.f, 0.f};
-    if constexpr (EPS_PRO) eh0 = eps_load(0);
+    f32x4 eh0[NPRO > 0 ? NPRO : 1];
+    sfor<0, NPRO>([&](auto kk) { eh0[decltype(kk)::value] = eps_load(decltype(kk)::value); });
     constexpr int NB4 = A::nbias / 4, UB = (NB4 + NT - 1) / NT;
     f32x4 bv[UB];
 #pragma unroll
@@ -756,10 +764,11 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     // the weight stream queues behind the x tile and the biases (vmcnt retires in order)
     // the first PF0 items of the stream here, the rest after the x-tile transform (CVAE_PRE_FILL)
     sfor<0, PF0>([&](auto g) { ring_load<A, P, decltype(g)::value>(ring, AR, wave, lane); });
-    if constexpr (EPS_PRO) {  // the Philox VALU issues while the x tile is in flight
-      if (CVAE_DIAG_NOPHILOX || !eps_mine) ep[0] = f32x4{0.f, 0.f, 0.f, 0.f};
-      else eps_make(integral_constant<int, 0>{}, eh0);
-    }
+    sfor<0, NPRO>([&](auto kk) {  // the Philox VALU issues while the x tile is in flight
+      constexpr int k = decltype(kk)::value;
+      if (CVAE_DIAG_NOPHILOX || !eps_mine) ep[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+      else eps_make(kk, eh0[k]);
+    });
     if constexpr (CVAE_WARM > 0) {
       // L2 warm-up (A/B option): the Adam step rewrote every operand copy, so each XCD's L2 meets
       // the stream's first lines cold.  The 8 blocks of an XCD (blk ≡ x mod 8) touch one dword per
@@ -874,7 +883,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   constexpr int ES = PL::step(PL::sE0).F8 ? 4 : 8;  // encoder-L1 K items between two draws
   auto eps_side = [&](auto cc) {
     constexpr int c = decltype(cc)::value;
-    if constexpr (!EPS_PRO && c % ES == 2 && c / ES < NZT) {
+    if constexpr (c % ES == 2 && c / ES >= NPRO && c / ES < NZT) {
       if (CVAE_DIAG_NOPHILOX) ep[c / ES] = f32x4{0.f, 0.f, 0.f, 0.f};  // timing only
       else if (eps_mine) draw_eps(integral_constant<int, c / ES>{});
       else ep[c / ES] = f32x4{0.f, 0.f, 0.f, 0.f};  // SZ: only wave 0's lanes hold the latents
