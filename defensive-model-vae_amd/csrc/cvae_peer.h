@@ -28,6 +28,40 @@
 #include "cvae_device.h"
 
 constexpr int PX_MAX = 16;                 // ranks
+
+// CVAE_PX_SC (default): the partials' hand-off without cache maintenance — the system-scope
+// analogue of MI355X_MICROARCH.md's sc1 form: every partial store write-through at system scope
+// (sc0 sc1), every storing wave drains them, a barrier, ONE relaxed system-scope flag add; the
+// owner polls with relaxed system-scope loads and reads the partials with sc0 sc1 loads.  0: a
+// system-scope release fence (L2 write-back) per pushing block and acquire loads / an acquire fence
+// on the owner — the split-K ticket with the agent-scope form of those fences ran 10x slower at
+// B = 16384 (profiles/r03i).  The owner's broadcast of the new operand copies keeps its release.
+#ifndef CVAE_PX_SC
+#define CVAE_PX_SC 1
+#endif
+// 4- or 8-B pieces of a partial: system-scope relaxed atomic stores / loads (sc0 sc1)
+template <typename V>
+__device__ __forceinline__ void px_st(float* dst, V v) {
+  static_assert(sizeof(V) % 8 == 0, "partial vectors of 8 or 16 B");
+#pragma unroll
+  for (int c = 0; c < (int)(sizeof(V) / 8); ++c) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 h = f2{v[2 * c], v[2 * c + 1]};
+    __hip_atomic_store((uint64_t*)dst + c, __builtin_bit_cast(uint64_t, h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+template <typename V>
+__device__ __forceinline__ V px_ld(const float* src) {
+  V v;
+#pragma unroll
+  for (int c = 0; c < (int)(sizeof(V) / 8); ++c) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 h = __builtin_bit_cast(f2, __hip_atomic_load((const uint64_t*)src + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    v[2 * c] = h[0];
+    v[2 * c + 1] = h[1];
+  }
+  return v;
+}
 constexpr int PX_PW = 32 * 32 + 32;        // floats of one tile's partial: dW [32][32], then db [32]
 
 struct PeerArgs {
@@ -63,7 +97,7 @@ __device__ __forceinline__ bool px_wait(const uint64_t* w, uint64_t target, unsi
                                         unsigned code = 2, uint64_t* stats = nullptr, int kind = 0) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   uint64_t dt = 0;
-  while (__hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
+  while (__hip_atomic_load(w, CVAE_PX_SC ? __ATOMIC_RELAXED : __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
     __builtin_amdgcn_s_sleep(4);
     dt = __builtin_amdgcn_s_memrealtime() - t0;
     if (dt > timeout) {
@@ -93,9 +127,17 @@ template <typename V>
 __device__ __forceinline__ void px_push(const PeerArgs& p, int tile, int o, int iv, V g, float db, bool bias_tile) {
   const int tid = threadIdx.x, owner = px_owner(tile, p.world);
   float* dst = px_inbox(p, p.mbox[owner], tile, p.rank);
-  *(V*)(dst + o * 32 + iv) = g;
-  if (bias_tile && tid < 32) dst[1024 + tid] = db;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: the partial is in the owner's memory first
+  if (CVAE_PX_SC) {
+    px_st(dst + o * 32 + iv, g);
+    if (bias_tile && tid < 32)
+      __hip_atomic_store((unsigned*)(dst + 1024 + tid), __builtin_bit_cast(unsigned, db), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every piece in the owner's memory before the flag
+  } else {
+    *(V*)(dst + o * 32 + iv) = g;
+    if (bias_tile && tid < 32) dst[1024 + tid] = db;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: the partial is in the owner's memory first
+  }
   __syncthreads();
   if (tid == 0) __hip_atomic_fetch_add(px_flag(p.mbox[owner], tile), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -111,7 +153,7 @@ __device__ __forceinline__ bool px_gather(const PeerArgs& p, const uint64_t* ctr
                       px_stats(p), 0) ? 1 : 0;
   __syncthreads();
   if (!*ok_lds) return false;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  if (!CVAE_PX_SC) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   V s = {};
   float sb = 0.f;
   for (int r = 0; r < p.world; ++r) {
@@ -122,8 +164,15 @@ __device__ __forceinline__ bool px_gather(const PeerArgs& p, const uint64_t* ctr
       vb = db;
     } else {
       const float* src = px_inbox(p, p.mbox[p.rank], tile, r);
-      v = *(const V*)(src + o * 32 + iv);
-      if (bias_tile && tid < 32) vb = src[1024 + tid];
+      if (CVAE_PX_SC) {
+        v = px_ld<V>(src + o * 32 + iv);
+        if (bias_tile && tid < 32)
+          vb = __builtin_bit_cast(float, __hip_atomic_load((const unsigned*)(src + 1024 + tid), __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_SYSTEM));
+      } else {
+        v = *(const V*)(src + o * 32 + iv);
+        if (bias_tile && tid < 32) vb = src[1024 + tid];
+      }
     }
     if (p.ragged) {
       v = v * p.c[r];

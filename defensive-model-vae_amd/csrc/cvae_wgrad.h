@@ -255,7 +255,25 @@ __device__ __forceinline__ float apply_bias(const LayerDev& L, int o, PreB b, fl
 // (n-tile t, chunk kc) lane ln holds elements (16t + (ln & 15), KC·kc + frag_k(ln >> 4, e)) at
 // ((t·Kp/KC + kc)·64 + ln)·EPL (frag_off), so a tile is 2 n-tiles × 32/KC chunks of contiguous
 // 1-KB blocks per copy.
-template <typename T, int NTHR, int LD = WT_LD>
+// SYS (the peer exchange's broadcast into another rank's arena): every piece a system-scope
+// write-through store (relaxed system atomics, 8 B each), so a drain, not a cache write-back, puts
+// it in that rank's memory
+template <bool SYS, typename V>
+__device__ __forceinline__ void op_st(void* base, size_t byte_off, V v) {
+  if constexpr (SYS) {
+    static_assert(sizeof(V) % 8 == 0, "8- or 16-B fragments");
+    typedef unsigned long long u64v __attribute__((ext_vector_type(sizeof(V) / 8)));
+    const u64v w = __builtin_bit_cast(u64v, v);
+#pragma unroll
+    for (int c = 0; c < (int)(sizeof(V) / 8); ++c)
+      __hip_atomic_store((uint64_t*)((char*)base + byte_off) + c, (uint64_t)w[c], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+  } else {
+    st_wt(base, byte_off, v);
+  }
+}
+
+template <typename T, int NTHR, int LD = WT_LD, bool SYS = false>
 __device__ __forceinline__ void store_operands(const LayerDev& L, int o0, int i0, const float* wt) {
   using V = typename Op<T>::V;
   constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC, CPT = 32 / KC;
@@ -273,7 +291,7 @@ __device__ __forceinline__ void store_operands(const LayerDev& L, int o0, int i0
     if (wb) {  // Wb = Wᵀ: rows = inputs i, K = outputs o
 #pragma unroll
       for (int e = 0; e < EPL; ++e) val[e] = to_t<T>(wt[(kl + frag_k<T>(q, e)) * LD + nl]);
-      st_wt(L.Wb, ((size_t)(((i0 >> 4) + bt) * (L.Np / KC) + (o0 + kl) / KC) * 64 + ln) * EPL * sizeof(T), val);
+      op_st<SYS>(L.Wb, ((size_t)(((i0 >> 4) + bt) * (L.Np / KC) + (o0 + kl) / KC) * 64 + ln) * EPL * sizeof(T), val);
     } else if (EPL == 8 && L.f8) {  // CVAE_FP8: e4m3(s·W), 8 B per lane into its K-pair fragment
       const float sc = f8_header(L.Wf)->s;
       float f[8];
@@ -283,7 +301,9 @@ __device__ __forceinline__ void store_operands(const LayerDev& L, int o0, int i0
 #pragma unroll
         for (int c = 0; c < 4; ++c) f[e + c] = v4[c] * sc;
       }
-      gst<long>((long*)((char*)L.Wf + f8_wf_off(o0 + bt * 16, (i0 + kl) / 32, L.Kp) + (size_t)ln * 16), f8x8(f));
+      const size_t off = f8_wf_off(o0 + bt * 16, (i0 + kl) / 32, L.Kp) + (size_t)ln * 16;
+      if constexpr (SYS) op_st<true>(L.Wf, off, f8x8(f));
+      else gst<long>((long*)((char*)L.Wf + off), f8x8(f));
     } else {
 #pragma unroll
       for (int e = 0; e < EPL; e += 4) {  // 4 consecutive K positions per half-fragment
@@ -291,7 +311,7 @@ __device__ __forceinline__ void store_operands(const LayerDev& L, int o0, int i0
 #pragma unroll
         for (int c = 0; c < 4; ++c) val[e + c] = to_t<T>(v4[c]);
       }
-      st_wt(L.Wf, ((size_t)(((o0 >> 4) + bt) * (L.Kp / KC) + (i0 + kl) / KC) * 64 + ln) * EPL * sizeof(T), val);
+      op_st<SYS>(L.Wf, ((size_t)(((o0 >> 4) + bt) * (L.Kp / KC) + (i0 + kl) / KC) * 64 + ln) * EPL * sizeof(T), val);
     }
   }
 }
@@ -336,10 +356,16 @@ __device__ __forceinline__ void px_broadcast(const PeerArgs& p, const LayerDev& 
     LayerDev Lr = L;
     Lr.Wf = (char*)L.Wf + d;
     Lr.Wb = (char*)L.Wb + d;
-    store_operands<T, NTHR>(Lr, o0, i0, wt);
-    if (i0 == 0 && tid < 32 && o0 + tid < L.Np) *(float*)((char*)(L.bias + o0 + tid) + d) = nb;
+    store_operands<T, NTHR, WT_LD, (bool)CVAE_PX_SC>(Lr, o0, i0, wt);
+    if (i0 == 0 && tid < 32 && o0 + tid < L.Np) {
+      float* const bd = (float*)((char*)(L.bias + o0 + tid) + d);
+      if (CVAE_PX_SC) __hip_atomic_store((unsigned*)bd, __builtin_bit_cast(unsigned, nb), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_SYSTEM);
+      else *bd = nb;
+    }
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  if (CVAE_PX_SC) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every piece in the peers' memory first
+  else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   __syncthreads();
   if (tid < p.world && tid != p.rank)
     __hip_atomic_fetch_add(px_done(p, p.mbox[tid]), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
