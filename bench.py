@@ -366,6 +366,13 @@ def main():
 
     run(args.warmup)
     torch.cuda.synchronize(dev)
+    verified = None
+    if dp.px is not None:  # the exchange's results checked once, before anything is timed
+        verified = dp.verify_exchange()
+        if verified is not True:
+            prepared = None  # run() now steps through the RCCL all-reduce
+            run(args.warmup)
+            torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -470,6 +477,8 @@ def main():
                "flop_per_traj": fl["total"]}
         if px_stats is not None:
             res["exchange_waits_rank0"] = px_stats
+        if verified is not None:  # the peer exchange's warm-up self-check (PeerExchange.verify)
+            res["exchange_verified"] = verified
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(B, S, D, Z, H, args.cpu_seconds, NE, ND,
                                                data=data_cpu if wl == "cfg1" else None)

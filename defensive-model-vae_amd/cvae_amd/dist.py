@@ -171,6 +171,20 @@ class DataParallelStep:
         if self.px is not None:
             self.px.gather_state()
 
+    def verify_exchange(self):
+        """The peer exchange's warm-up self-check (``PeerExchange.verify``); on a failure every rank
+        closes it together and continues on the RCCL all-reduce (the master state was made whole by
+        the check, so the ranks agree).  Returns True or the failure, which ``exchange_note`` keeps."""
+        if self.px is None:
+            return True
+        ok = self.px.verify()
+        if ok is not True:
+            self.px.close()
+            self.px = None
+            self.exchange = "rccl"
+            self.exchange_note = f"peer exchange failed its warm-up check ({ok}); rccl"
+        return ok
+
     def close(self):
         if self.px is not None:
             self.px.close()

@@ -150,6 +150,45 @@ class PeerExchange:
         return {"owner_wait_max_us": out[0] / 100.0, "end_wait_max_us": out[1] / 100.0,
                 "owner_wait_mean_us": out[2] / 100.0 / max(out[3], 1), "owner_waits": int(out[3])}
 
+    def verify(self, rows=64):
+        """Self-check after warm-up, outside any timed region; collective over the group.  The
+        operand copies the owners wrote into this rank's workspace must equal, bit for bit, the ones
+        packed from the whole master state: a forward pass over the same seeded rows (eps = 0)
+        before and after ``gather_state()`` must give identical outputs, and no rank's fault word
+        may be set.  Returns True, or the first failing rank's reason (the same value on every
+        rank; a local error becomes a reason, so no rank is left in a collective)."""
+        eng = self.engine
+        S, D, Z = eng.shape[:3]
+        rows = min(int(rows), eng.max_batch)
+        reason = before = None
+
+        def outs(probe, eps):
+            return torch.cat([t.flatten() for t in eng.forward(probe, eps=eps, batch=rows, offset=0)])
+        try:
+            torch.cuda.synchronize(eng.device)
+            f = eng.fault()
+            if f:
+                reason = f"fault word {f:#x} (a bounded wait gave up)"
+            else:
+                probe = eng.as_input(torch.randn(rows, S, D, generator=torch.Generator().manual_seed(7)))
+                eps = torch.zeros(rows, Z, device=eng.device, dtype=torch.float32)
+                before = outs(probe, eps)
+        except Exception as e:  # noqa: BLE001
+            reason = f"{type(e).__name__}: {e}"
+        self.gather_state()
+        if reason is None:
+            try:
+                after = outs(probe, eps)
+                if not torch.equal(before, after):
+                    n = int((before != after).sum())
+                    reason = f"{n} forward outputs differ between the broadcast and the repacked operand copies"
+            except Exception as e:  # noqa: BLE001
+                reason = f"{type(e).__name__}: {e}"
+        reasons = [None] * self.world
+        dist.all_gather_object(reasons, reason, group=self.group)
+        bad = [(r, v) for r, v in enumerate(reasons) if v]
+        return True if not bad else f"rank {bad[0][0]}: {bad[0][1]}"
+
     def gather_state(self):
         """Whole fp32 params / Adam moments on every rank (each element from its owner), and the
         operand copies repacked from them."""

@@ -62,12 +62,13 @@ def _worker(rank, world, port, sizes, steps, out):
         torch.cuda.synchronize()
         fault = eng.fault()
         print(f"rank {rank}: fault {fault}, waits {dp.px.stats()}", flush=True)
-        dp.sync_state()
+        # the warm-up self-check bench.py runs (it makes the state whole, as sync_state does)
+        verified = dp.verify_exchange()
         acc = dp.epoch_loss_sums()
         torch.cuda.synchronize()
         if rank == 0:
             torch.save({"params": eng.params.cpu(), "m": eng.m.cpu(), "v": eng.v.cpu(),
-                        "counters": eng.counters.cpu(), "acc": acc.cpu(), "fault": fault}, out)
+                        "counters": eng.counters.cpu(), "acc": acc.cpu(), "fault": fault, "verified": verified}, out)
         dp.close()
     finally:
         dist.destroy_process_group()
@@ -131,6 +132,7 @@ def test_peer_exchange_equals_split_step(sizes, tmp_path):
     assert codes == [0] * len(sizes), codes
     got = torch.load(out, weights_only=True)
     assert got["fault"] == 0
+    assert got["verified"] is True, got["verified"]
     ref = _reference(sizes, steps)
     for k in ("params", "m", "v", "counters"):
         assert torch.equal(got[k], ref[k]), (k, float((got[k].double() - ref[k].double()).abs().max()))
