@@ -382,6 +382,9 @@ def main():
     if world > 1:
         dist.barrier()
     t = time.perf_counter() - t0
+    if eng.fault():  # a bounded in-kernel wait gave up inside the timed steps: no valid number
+        raise RuntimeError(f"rank {rank}: fault word {eng.fault():#x} set during the timed steps "
+                           f"({dp.exchange} exchange); the measurement is invalid")
     # kernel durations for the roofline: the same K steps again with HIP events recorded on the
     # launch stream between kernels (events inside the timed pass would add ~10 us per step;
     # graph replays record none, so this pass runs eagerly)
