@@ -382,7 +382,24 @@ def main():
     if world > 1:
         dist.barrier()
     t = time.perf_counter() - t0
-    if eng.fault():  # a bounded in-kernel wait gave up inside the timed steps: no valid number
+    verified_after = None
+    if dp.px is not None:
+        # the exchange checked again over the state the timed steps left (collective; every rank's
+        # fault word, every rank's operand-copy checksum against the others' and against the repack
+        # from the gathered master state): a failure invalidates the number
+        verified_after = dp.verify_exchange(fallback=False)
+        if verified_after is not True:  # no number: the line says why, the exit status says so too
+            if rank == 0:
+                print(json.dumps({"metric": "trajectories/sec per ELBO step, batch=1024 seq_len=100; 1/2/4/8 MI355X",
+                                  "value": None, "unit": "trajectories/s", "n_gpus": world, "steps": args.steps,
+                                  "warmup": args.warmup, "higher_is_better": True, "scaling": "weak",
+                                  "exchange_verified": verified, "exchange_verified_after": verified_after,
+                                  "invalid": f"the peer exchange failed its check after the timed steps: "
+                                             f"{verified_after}"}), file=out, flush=True)
+            dp.close()
+            dist.destroy_process_group()
+            sys.exit(3)
+    elif eng.fault():  # a bounded in-kernel wait gave up inside the timed steps: no valid number
         raise RuntimeError(f"rank {rank}: fault word {eng.fault():#x} set during the timed steps "
                            f"({dp.exchange} exchange); the measurement is invalid")
     # kernel durations for the roofline: the same K steps again with HIP events recorded on the
@@ -480,8 +497,13 @@ def main():
                "flop_per_traj": fl["total"]}
         if px_stats is not None:
             res["exchange_waits_rank0"] = px_stats
+            k_gpu, g_blocks = dp.px.layout()
+            res["exchange_layout"] = {"ranks_on_gpu": k_gpu, "tile_blocks": g_blocks,
+                                      "operand_checksum": f"{dp.px.last_checksum:#018x}"}
         if verified is not None:  # the peer exchange's warm-up self-check (PeerExchange.verify)
             res["exchange_verified"] = verified
+        if verified_after is not None:  # the same check after the timed steps (a failure exits above)
+            res["exchange_verified_after"] = verified_after
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(B, S, D, Z, H, args.cpu_seconds, NE, ND,
                                                data=data_cpu if wl == "cfg1" else None)

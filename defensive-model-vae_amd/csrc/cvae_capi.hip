@@ -71,7 +71,6 @@ struct cvae_handle {
   float* splitk_ws = nullptr;
   unsigned* splitk_tickets = nullptr;
   char* arena = nullptr;    // weight copies + activations
-  unsigned* d_sync = nullptr;  // fused launch hand-off words (fchain::FusedArgs::sync), zero between launches
   // sticky fault word in pinned, device-mapped host memory: a kernel that gives up a bounded spin
   // sets it (system scope); the next training call reads it WITHOUT synchronising and fails
   unsigned* fault_host = nullptr;
@@ -85,7 +84,10 @@ struct cvae_handle {
   char* px_mb[PX_MAX] = {};
   bool px_ready = false;
   uint64_t px_base = 0;
-  bool fused = false;          // training steps run as one fused_step_kernel launch
+  int px_share = 1;            // ranks of the exchange on this rank's GPU (cvae_px_import)
+  int px_grid = 0;             // tile blocks of px_wgrad_kernel (the residency precondition, cvae_peer.h)
+  // one-shot outputs of the next training row chain (cvae_tap_outputs): recon, mu, logvar
+  float* tap[3] = {nullptr, nullptr, nullptr};
   // the reference architecture's training step as ONE launch (cvae_fusedring.h: ring chain + dW
   // tiles + loss block); its self-resetting hand-off words
   bool fring = false;
@@ -414,7 +416,6 @@ int alloc_arena(cvae_handle* h) {
   for (int l = 0; l < n.n_layers; ++l) maxnp = std::max(maxnp, std::max(n.L[l].Np, n.L[l].Kp));
   const int64_t zb_off = take((int64_t)maxnp * 4);
   const int64_t part_off = take((int64_t)h->max_row_tiles * 8 * 4);
-  const int64_t sync_off = take(256);
   const int64_t rsync_off = take(wchain::RF_WORDS * 4);  // fused ring step: zero between launches
   // split-K for batches of >= 8192 rows: up to 16 splits of >= 2048 rows (cvae_wgrad.h SplitK)
   h->splitk_max = std::max(1, std::min(16, rup_i(h->cfg.max_batch, 32) / 2048));
@@ -447,7 +448,6 @@ int alloc_arena(cvae_handle* h) {
   n.zbias = (const float*)(h->arena + zb_off);
   n.bias_all = (const float*)(h->arena + bias_base);
   h->d_partials = (float*)(h->arena + part_off);
-  h->d_sync = (unsigned*)(h->arena + sync_off);
   h->d_rsync = (unsigned*)(h->arena + rsync_off);
   if (h->splitk_max > 1) {  // tickets start at zero (the arena memset) and return to zero after every launch
     h->splitk_ws = (float*)(h->arena + skw_off);
@@ -661,15 +661,7 @@ int plan_fast(cvae_handle* h) {
     if (nki == 19) {
       HIPCK(hipFuncSetAttribute((const void*)fchain::fastchain_kernel<19>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lp.total));
-      HIPCK(hipFuncSetAttribute((const void*)fchain::fused_step_kernel<19>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lp.total));
     }
-    // CVAE_FUSE=1: one fused_step_kernel launch per training step instead of two.  Correct, and
-    // measured slower at B = 1024 (32.1 vs 29.2 us per step): the chain's per-group drains and the
-    // waiting tiles' polls cost it ~3 us, and the encoder tiles (112 after the chain's last step)
-    // queue for CUs behind the decoder tiles — DESIGN.md §fused launch.
-    const char* fu = std::getenv("CVAE_FUSE");
-    h->fused = fu && fu[0] == '1';
   }
   return CVAE_OK;
 }
@@ -701,7 +693,7 @@ bool wide_layout_matches(const cvae_handle* h) {
 // weight-stream chain (cvae_widechain.h, small-latent form) instead of fastchain_kernel's per-step
 // register prefetch: the per-CU L2 stream stays busy across step barriers.  The default for this
 // shape (row chain 17.8 vs 18.35 us at B = 1024); CVAE_RING=0 at creation keeps
-// fastchain_kernel.  The fused single launch (CVAE_FUSE=1) is fastchain's.
+// fastchain_kernel.
 int plan_ring(cvae_handle* h) {
   using A = wchain::Cfg2;
   const cvae_config& c = h->cfg;
@@ -711,6 +703,8 @@ int plan_ring(cvae_handle* h) {
   if (!wide_layout_matches<A>(h) || h->arena_bytes >= ((int64_t)1 << 31)) return CVAE_OK;
   HIPCK(hipFuncSetAttribute((const void*)wchain::widechain_kernel<A>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             A::L_TOTAL));
+  HIPCK(hipFuncSetAttribute((const void*)wchain::widechain_kernel<A, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, A::L_TOTAL));
   h->ring = true;
   h->ring_lds = A::L_TOTAL;
   // the one-launch step (cvae_fusedring.h): CVAE_FUSE_RING=0 at creation keeps two launches
@@ -829,6 +823,19 @@ template <typename T>
 int launch_train_chain(cvae_handle* h, RowArgs ra, hipStream_t s) {
   int rc = tmark(h, s, "rowchain");
   if (rc) return rc;
+  const bool tap = h->tap[0] || h->tap[1] || h->tap[2];
+  if (tap) {  // one-shot (cvae_tap_outputs): this launch only
+    ra.recon_out = h->tap[0];
+    ra.mu_out = h->tap[1];
+    ra.lv_out = h->tap[2];
+    h->tap[0] = h->tap[1] = h->tap[2] = nullptr;
+    if (!(std::is_same<T, __bf16>::value && ring_ok(h, ra)))
+      return fail(CVAE_E_INVALID, "cvae_tap_outputs: only the ring chain (seq_len 100, dim 6, bf16) writes them");
+    ra.stamps = h->d_stamps;
+    const int grid = rup_i(ra.batch, 32) / wchain::R;
+    return klaunch(h, wchain::widechain_kernel<wchain::Cfg2, true>, dim3(grid), dim3(wchain::NT), h->ring_lds, s,
+                   h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra.ctr, ra);
+  }
   if (std::is_same<T, __bf16>::value && ring_ok(h, ra)) {
     ra.stamps = h->d_stamps;
     const int grid = rup_i(ra.batch, 32) / wchain::R;
@@ -935,44 +942,9 @@ __global__ void step_skip_kernel(uint64_t* c, double lr, double b1, double b2) {
   c[0] = c[0] + 1;
 }
 
-// device counters, fused launch: its chain blocks do not bump the step (its dW tiles read it in the
-// same launch), so the step begins with this one-lane kernel; the loss tile advances the offset
-// after every chain block has published (read) it
-__global__ void counter_bump_kernel(uint64_t* c, double lr, double b1, double b2) {
-  adam_precompute(c, lr, b1, b2, true);
-}
-
-// one training step as a single fused_step_kernel launch (fast configuration, 16-B aligned x)
-int launch_fused(cvae_handle* h, RowArgs ra, const AdamArgs& aa, float* loss_out, double* loss_accum,
-                 hipStream_t s) {
-  ra.stamps = h->d_stamps;
-  fchain::FusedArgs f{};
-  f.aa = aa;
-  f.la = make_loss(h, ra, loss_out, loss_accum);
-  f.sync = h->d_sync;
-  f.fault = h->fault_dev;
-  f.Bk = bk_of(h, ra.batch);
-  f.nchain = rup_i(ra.batch, 32) / fchain::R;
-  const int nt = fchain::Tiles<19>::total();
-  // the group counters start every launch at zero (stream-ordered; the sticky time-out flag stays)
-  HIPCK(hipMemsetAsync(h->d_sync, 0, 4 * sizeof(unsigned), s));
-  if (ra.ctr) {
-    hipLaunchKernelGGL(counter_bump_kernel, dim3(1), dim3(1), 0, s, ra.ctr, ra.lr, ra.beta1, ra.beta2);
-    HIPCK(hipGetLastError());
-  }
-  int rc = tmark(h, s, "fused_step");
-  if (rc) return rc;
-  return klaunch(h, fchain::fused_step_kernel<19>, dim3(f.nchain + nt), dim3(fchain::NT), h->fast_lds, s,
-                 fchain::FastNet{h->arena, h->net.Bp, h->net.S, h->net.D, h->net.I}, ra, f);
-}
-
-bool use_fused(const cvae_handle* h, const RowArgs& ra) {
-  return h->fused && h->fast_nki == 19 && fast_ok(h, ra);
-}
-
 // one training step as ONE launch: ring chain + every dW tile + the loss block (cvae_fusedring.h)
 bool use_fused_ring(const cvae_handle* h, const RowArgs& ra) {  // its chain blocks also take tiles
-  return h->fring && !h->fused && ring_ok(h, ra) && ra.batch >= 1 &&
+  return h->fring && ring_ok(h, ra) && ra.batch >= 1 &&
          rup_i(ra.batch, 32) / wchain::R <= fchain::Tiles<19>::total();
 }
 int launch_fused_ring(cvae_handle* h, RowArgs ra, const AdamArgs& aa, float* loss_out, double* loss_accum,
@@ -1026,7 +998,6 @@ int train_step_impl(cvae_handle* h, const CallX& c, float* params, float* m, flo
   CallX ca = c;
   ca.adam = adam;
   const RowArgs ra = row_args(h, ca);
-  if (use_fused(h, ra)) return launch_fused(h, ra, aa, loss_out, loss_accum, s);
   if (use_fused_ring(h, ra)) return launch_fused_ring(h, ra, aa, loss_out, loss_accum, s);
   int rc = is16(h) ? launch_train_chain<__bf16>(h, ra, s) : launch_train_chain<float>(h, ra, s);
   if (rc) return rc;
@@ -1112,7 +1083,7 @@ int cvae_workspace_bytes(const cvae_handle* h, int64_t* bytes) {
 
 int cvae_train_kernel(const cvae_handle* h, int* kind) {
   if (!h || !kind) return fail(CVAE_E_INVALID, "null argument");
-  *kind = (h->ring && !h->fused) || h->ring_cls ? CVAE_KERNEL_RING
+  *kind = h->ring || h->ring_cls ? CVAE_KERNEL_RING
            : h->fast_nki > 0      ? CVAE_KERNEL_FAST
            : h->wide              ? CVAE_KERNEL_WIDE
                                   : CVAE_KERNEL_GENERIC;
@@ -1325,9 +1296,11 @@ namespace {
 struct PxBlob {
   int magic, world, rank, nt;
   int64_t arena_bytes, mbox_bytes;
+  int pci_domain, pci_bus, pci_device, cus;  // which GPU (ranks sharing one: the residency precondition)
+  int chain_blocks, pad;                     // row-chain workgroups at the batch capacity
   hipIpcMemHandle_t arena, mbox;
 };
-constexpr int PX_MAGIC = 0x43505831;  // "CPX1"
+constexpr int PX_MAGIC = 0x43505832;  // "CPX2"
 int px_tiles(const cvae_handle*) { return fchain::Tiles<19>::total(); }
 // bound of every exchange wait: CVAE_PX_TIMEOUT_MS (default 10000 ms: ranks of a real
 // multi-GPU job may enter their first exchange seconds apart), in s_memrealtime ticks
@@ -1388,6 +1361,11 @@ int cvae_px_export(cvae_handle* h, int world, int rank, void* blob) {
   PxBlob b{};
   b.magic = PX_MAGIC; b.world = world; b.rank = rank; b.nt = nt;
   b.arena_bytes = h->arena_bytes; b.mbox_bytes = h->px_mbox_bytes;
+  hipDeviceProp_t prop;
+  HIPCK(hipGetDeviceProperties(&prop, h->device));
+  b.pci_domain = prop.pciDomainID; b.pci_bus = prop.pciBusID; b.pci_device = prop.pciDeviceID;
+  b.cus = prop.multiProcessorCount;
+  b.chain_blocks = rup_i(h->cfg.max_batch, 32) / wchain::R;
   HIPCK(hipIpcGetMemHandle(&b.arena, h->arena));
   HIPCK(hipIpcGetMemHandle(&b.mbox, h->px_mbox));
   std::memcpy(blob, &b, sizeof(b));
@@ -1401,11 +1379,25 @@ int cvae_px_import(cvae_handle* h, const void* blobs, uint64_t base) {
   if (!h || !blobs || !h->px_mbox) return fail(CVAE_E_INVALID, "peer exchange: export first");
   const PxBlob* b = (const PxBlob*)blobs;
   HIPCK(hipSetDevice(h->device));
-  for (int r = 0; r < h->px_world; ++r) {
+  for (int r = 0; r < h->px_world; ++r)
     if (b[r].magic != PX_MAGIC || b[r].world != h->px_world || b[r].rank != r || b[r].nt != px_tiles(h) ||
         b[r].arena_bytes != h->arena_bytes || b[r].mbox_bytes != h->px_mbox_bytes)
       return fail(CVAE_E_INVALID, "peer exchange: rank " + std::to_string(r) +
                                       "'s blob does not match this configuration (same model, batch capacity, world)");
+  // the residency precondition (cvae_peer.h): the k ranks on this rank's GPU share its 2·CUs slots
+  const PxBlob& me = b[h->px_rank];
+  int share = 0;
+  for (int r = 0; r < h->px_world; ++r)
+    share += b[r].pci_domain == me.pci_domain && b[r].pci_bus == me.pci_bus && b[r].pci_device == me.pci_device;
+  const int slots = PX_SLOTS_PER_CU * me.cus / std::max(share, 1);
+  const int nt = px_tiles(h);
+  if (share > 1 && me.chain_blocks > slots)
+    return fail(CVAE_E_INVALID, "peer exchange: " + std::to_string(share) + " ranks share one GPU; each may hold " +
+                                    std::to_string(slots) + " resident workgroups, its row chain needs " +
+                                    std::to_string(me.chain_blocks) + " (lower max_batch or the ranks per GPU)");
+  h->px_share = std::max(share, 1);
+  h->px_grid = share > 1 ? std::max(1, std::min(nt, slots - 1)) : nt;
+  for (int r = 0; r < h->px_world; ++r) {
     if (r == h->px_rank) {
       h->px_arena[r] = h->arena;
       h->px_mb[r] = h->px_mbox;
@@ -1529,8 +1521,71 @@ int cvae_px_train_step(cvae_handle* h, const void* x, const int64_t* idx, int ba
   }
   const AdamArgs aa = make_adam(params, nullptr, m, v, 0, *adam, rank_scales ? 1.f : 1.f / (float)px.world, counters);
   if ((rc = tmark(h, s, "px_wgrad"))) return rc;
+  const int grid = h->px_grid > 0 ? h->px_grid : nt;
+  if (grid < nt)  // ranks sharing this GPU: fewer blocks, each looping over its tiles (cvae_peer.h)
+    return klaunch(h, fchain::px_wgrad_kernel<19, true>, dim3(grid + 1), dim3(WG_THREADS), 0, s, h->arena, params,
+                   m, v, h->net.Bp, bk_of(h, batch), h->net.S, h->net.D, h->net.I, aa, la, px);
   return klaunch(h, fchain::px_wgrad_kernel<19>, dim3(nt + 1), dim3(WG_THREADS), 0, s, h->arena, params, m, v,
                  h->net.Bp, bk_of(h, batch), h->net.S, h->net.D, h->net.I, aa, la, px);
+}
+
+int cvae_px_layout(const cvae_handle* h, int* ranks_on_gpu, int* tile_blocks) {
+  if (!h || !ranks_on_gpu || !tile_blocks) return fail(CVAE_E_INVALID, "null argument");
+  if (!h->px_ready) return fail(CVAE_E_INVALID, "peer exchange not set up");
+  *ranks_on_gpu = h->px_share;
+  *tile_blocks = h->px_grid;
+  return CVAE_OK;
+}
+
+int cvae_px_reset(cvae_handle* h, uint64_t base) {
+  if (!h) return fail(CVAE_E_INVALID, "null argument");
+  if (!h->px_ready) return fail(CVAE_E_INVALID, "peer exchange not set up");
+  HIPCK(hipSetDevice(h->device));
+  HIPCK(hipDeviceSynchronize());
+  // arrival flags, the done counter and the probe words; the wait statistics stay
+  HIPCK(hipMemset(h->px_mbox, 0, h->px_done_off + PX_STATS_OFF));
+  HIPCK(hipDeviceSynchronize());
+  h->px_base = base;
+  if (h->fault_host) __atomic_store_n(h->fault_host, 0u, __ATOMIC_RELEASE);
+  return CVAE_OK;
+}
+
+int cvae_tap_outputs(cvae_handle* h, float* recon, float* mu, float* logvar) {
+  if (!h) return fail(CVAE_E_INVALID, "null handle");
+  h->tap[0] = recon;
+  h->tap[1] = mu;
+  h->tap[2] = logvar;
+  return CVAE_OK;
+}
+
+namespace {
+// Σ over the 8-B words w_i of the operand copies of splitmix64(w_i ^ i·φ) (mod 2^64): order-free,
+// so the block sums may meet in any order, and any change of any word moves it
+__global__ __launch_bounds__(256) void checksum_kernel(const uint64_t* __restrict__ w, int64_t n,
+                                                      unsigned long long* out) {
+  unsigned long long s = 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    uint64_t z = w[i] ^ ((uint64_t)i * 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    s += z ^ (z >> 31);
+  }
+  for (int k = 32; k > 0; k >>= 1) s += __shfl_xor(s, k, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(out, s);
+}
+}  // namespace
+
+int cvae_operand_checksum(cvae_handle* h, uint64_t* out, void* stream) {
+  if (!h || !out) return fail(CVAE_E_INVALID, "null argument");
+  hipStream_t s = (hipStream_t)stream;
+  // the operand copies (Wf, Wb of every layer, padding included) and the padded biases: the arena's
+  // head up to the end of the bias block (alloc_arena)
+  const int64_t bytes = (const char*)(h->net.bias_all + h->net.nbias) - h->arena;
+  HIPCK(hipMemsetAsync(out, 0, sizeof(uint64_t), s));
+  hipLaunchKernelGGL(checksum_kernel, dim3(64), dim3(256), 0, s, (const uint64_t*)h->arena, bytes / 8,
+                     (unsigned long long*)out);
+  HIPCK(hipGetLastError());
+  return CVAE_OK;
 }
 
 int cvae_fault(const cvae_handle* h, unsigned* word) {
@@ -1546,16 +1601,9 @@ int cvae_clear_fault(cvae_handle* h) {
   return CVAE_OK;
 }
 
-int cvae_sync_words(cvae_handle* h, unsigned* out) {
-  if (!h || !out) return fail(CVAE_E_INVALID, "null argument");
-  HIPCK(hipDeviceSynchronize());
-  HIPCK(hipMemcpy(out, h->d_sync, 5 * sizeof(unsigned), hipMemcpyDeviceToHost));
-  return CVAE_OK;
-}
-
 int cvae_step_launches(const cvae_handle* h, int* launches) {
   if (!h || !launches) return fail(CVAE_E_INVALID, "null argument");
-  *launches = h->fused || h->fring ? 1 : 2;
+  *launches = h->fring ? 1 : 2;
   return CVAE_OK;
 }
 

@@ -192,16 +192,9 @@ __device__ __forceinline__ f32x4 quad_all(float v) {
 
 __device__ __forceinline__ void lbar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// The row chain of batch tile `blk`.  pub (the fused launch, fused_step_kernel): after the steps
-// that finish a group of layers' arena rows, every wave drains its (sc1, write-through) stores,
-// the step barrier follows, and one lane adds 1 to pub[group] (agent scope) — the dW tiles of
-// those layers wait for all row tiles' adds.  Groups: 0 after S11 (D0 D1 D2), 1 after S13 (D3 FC
-// E3 C1), 2 at the end (E2 E1 E0 C0 and the loss partials).  Every weight load of the chain is
-// issued before S11, so the drain at group 0 also retires them: the tiles may then overwrite the
-// operand copies.
+// The row chain of batch tile `blk`.
 template <int NKI>
-__device__ __forceinline__ void chain_body(const FastNet& net, const RowArgs& a, char* smem, unsigned* pub,
-                                           int blk) {
+__device__ __forceinline__ void chain_body(const FastNet& net, const RowArgs& a, char* smem, int blk) {
   constexpr int Ip = NKI * 32, NG3 = NKI * 2;                 // D3 output n-tiles
   constexpr int G3 = (NG3 + NW - 1) / NW;                     // D3 n-tiles per wave (max)
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
@@ -321,8 +314,7 @@ __device__ __forceinline__ void chain_body(const FastNet& net, const RowArgs& a,
     wload_part<0, NKI / 2>(wE0, Wf(LE0), Ip, wave);
     // device counters: this launch begins optimizer step ctr[1] + 1 and precomputes its Adam scalars
     // (the dW kernel behind it reads them); one lane of block 0, while its wave waits for the x tile.
-    // The fused launch (pub) does this in a kernel before it: its dW tiles run beside the chain.
-    if (a.ctr && blk == 0 && tid == 0 && !pub) adam_precompute(a.ctr, a.lr, a.beta1, a.beta2, a.adam_pre);
+    if (a.ctr && blk == 0 && tid == 0) adam_precompute(a.ctr, a.lr, a.beta1, a.beta2, a.adam_pre);
     stamp();
     // eps: 8 latents × 16 rows, 4 per thread (host-given, or Philox as philox_normal), on the last
     // wave: it has one x-tile task fewer than waves 0-2
@@ -640,9 +632,7 @@ __device__ __forceinline__ void chain_body(const FastNet& net, const RowArgs& a,
     arena4(GT(LD0), LY::Np(LD0), n, b0, q, h);
   }
   copy_round(2, GT(LD3), LY::Np(LD3));
-  if (pub) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   lbar();
-  if (pub && tid == 0) __hip_atomic_fetch_add(pub + 0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   stamp();
   {  // S12: D0ᵀ: [dz ‖ dh_c(decoder share)]; dz → KL/reparameterisation backward → G_fc
 #pragma unroll
@@ -689,9 +679,7 @@ __device__ __forceinline__ void chain_body(const FastNet& net, const RowArgs& a,
     arena4(GT(LC1), LY::Np(LC1), n, b0, q, hc);
   }
   copy_round(4, GT(LD3), LY::Np(LD3));
-  if (pub) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   lbar();
-  if (pub && tid == 0) __hip_atomic_fetch_add(pub + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   stamp();
   {  // S14: E3ᵀ
     const bf16x4 h = masked(mm(A0, wE3b), ME2, n);
@@ -731,12 +719,7 @@ __device__ __forceinline__ void chain_body(const FastNet& net, const RowArgs& a,
     float s = 0.f;
     for (int w = 0; w < NW; ++w) s += PART[w * 8 + tid];
     __hip_atomic_store((unsigned*)(a.partials + blk * 8 + tid), __builtin_bit_cast(unsigned, s), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);  // sc1: read by a dW tile of the fused launch
-  }
-  if (pub) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lbar();
-    if (tid == 0) __hip_atomic_fetch_add(pub + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                       __HIP_MEMORY_SCOPE_AGENT);
   }
   if (CVAE_DIAG_STAMPS && a.stamps && tid < 64) {
     stamp();
@@ -759,11 +742,11 @@ __global__ __launch_bounds__(NT) void fastchain_kernel(char* arena, const void* 
   const int reps = Bp > 0 ? 2 : 1;
 #pragma nounroll
   for (int it = 0; it < reps; ++it) {
-    chain_body<NKI>(FastNet{arena, Bp, S, D, I}, ra, smem, nullptr, blockIdx.x);
+    chain_body<NKI>(FastNet{arena, Bp, S, D, I}, ra, smem, blockIdx.x);
     __syncthreads();
   }
 #else
-  chain_body<NKI>(FastNet{arena, Bp, S, D, I}, ra, smem, nullptr, blockIdx.x);
+  chain_body<NKI>(FastNet{arena, Bp, S, D, I}, ra, smem, blockIdx.x);
 #endif
 }
 

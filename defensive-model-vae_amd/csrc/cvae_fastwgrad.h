@@ -173,11 +173,17 @@ __global__ __launch_bounds__(WG_THREADS) void fastwgrad_kernel(char* arena, floa
 // fastwgrad_kernel's tiles with cvae_peer.h's exchange: tile b is owned by rank b mod world (its
 // block runs the Adam epilogue and broadcasts the operand copies), every other rank's block for b
 // pushes its partial to the owner.  The last block finishes this rank's loss, then waits until
-// every tile the other ranks own has arrived (px.n_remote per step).  grid = tiles + 1.
-// Two workgroups per CU (4 waves per SIMD, <= 128 VGPRs): every block of the launch is resident at
-// once with room to spare, so waiting owner blocks can never hold the slots their pushers need —
-// also when several ranks share one GPU (tests/test_gpu_peer.py).
-template <int NKI>
+// every tile the other ranks own has arrived (px.n_remote per step).
+// grid = G + 1: tile block b takes tiles b, b + G, b + 2G, .. — every one it PUSHES first, then the
+// ones it OWNS (the only ones that wait).  One rank per GPU: G = tiles (one tile per block, every
+// block resident: 281 blocks in 512 slots).  Ranks sharing a GPU (cvae_px_import counts them): G is
+// cut so that Σ over those ranks of max(row-chain blocks, G + 1) <= the GPU's workgroup slots (two
+// per CU at <= 128 VGPRs and these LDS sizes) — every block of every sharing rank can then be
+// resident at once, so a waiting owner never holds a slot a pusher of another rank needs, and no
+// push waits at all (cvae_peer.h, residency precondition).
+// SHARED = false: one tile per block (G = tiles); true: the loop over tiles b, b + G, .. (ranks
+// sharing a GPU — a rehearsal, not the measured path)
+template <int NKI, bool SHARED = false>
 __global__ __launch_bounds__(WG_THREADS, 4) void px_wgrad_kernel(char* arena, float* params, float* mst, float* vst,
                                                                int Bp, int Bk, int S, int D, int I, AdamArgs a,
                                                                LossArgs la, PeerArgs px) {
@@ -187,7 +193,8 @@ __global__ __launch_bounds__(WG_THREADS, 4) void px_wgrad_kernel(char* arena, fl
   aa.m = mst;
   aa.v = vst;
   constexpr int NTL = Tiles<NKI>::total();
-  if ((int)blockIdx.x == NTL) {
+  const int G = SHARED ? (int)gridDim.x - 1 : NTL;
+  if ((int)blockIdx.x == G) {
     if (threadIdx.x < 64 && la.partials) finish_loss(la, fn.S, fn.D, Z);
     if (threadIdx.x == 0)
       px_wait(px_done(px, px.mbox[px.rank]), (uint64_t)px.n_remote * px_epoch(px, aa.ctr), px.fault, px.timeout, 3,
@@ -195,127 +202,30 @@ __global__ __launch_bounds__(WG_THREADS, 4) void px_wgrad_kernel(char* arena, fl
     return;
   }
   __shared__ __attribute__((aligned(16))) WgradLds<1> sh;
-  SplitK sk{1, 0, nullptr, nullptr, (int)blockIdx.x, 0};
-  TileDesc td;
-  LayerDev L;
-  decode_tile<NKI>(sk.tile, fn.arena, fn.Bp, fn.I, td, L);
   static_assert(Tiles<NKI>::ni_max() == 1, "the exchange's partial is one 32 x 32 tile");
-  if (px_owner(sk.tile, px.world) == px.rank)  // block-uniform
-    wgrad_body<__bf16, PM_ADAM, false, 1>(L, td, Bk, aa, la, false, fn.S, fn.D, Z, sh.red, sh.dbp, sk, &px);
-  else
-    wgrad_body<__bf16, PM_GRAD, false, 1>(L, td, Bk, aa, la, false, fn.S, fn.D, Z, sh.red, sh.dbp, sk, &px);
-}
-
-// ---------------------------------------------------------------- the fused training step
-// One launch = the row chain (blocks 0 .. nchain-1) and every dW ⊕ Adam tile (blocks nchain ..).
-// The tiles are listed in the order their arena rows become final (chain_body's groups), so the
-// tile blocks resident beside the chain are the ones its backward pass releases first: the
-// decoder's and fc's dW overlap the encoder's backward steps instead of following the whole chain,
-// and the launch boundary between the two kernels disappears.
-//   group 0 (after S11): D0 D1 D2 | group 1 (after S13): D3 FC E3 C1 | group 2 (end): E2 E1 E0 C0
-// Visibility (MI355X_MICROARCH.md, inter-workgroup hand-off, sc1 form): the chain stores every
-// arena row and loss partial sc1 and drains them before its per-group agent-scope add; a tile
-// block polls its group's counter (one lane, relaxed sc1 loads, bounded), joins a workgroup
-// barrier, then reads the rows with sc1 loads only.  Deadlock-free: tiles wait only on chain
-// blocks, which have the lowest indices and are dispatched first; the spin gives up after ~0.5 s
-// (flag sync[4]; the tile then skips its update) rather than hang.  The host zeroes the counters
-// before every launch (stream-ordered memset).
-__host__ __device__ constexpr int ready_layer(int k) {
-  return k == 0 ? LD0 : k == 1 ? LD1 : k == 2 ? LD2 : k == 3 ? LD3 : k == 4 ? LFC : k == 5 ? LE3
-       : k == 6 ? LC1 : k == 7 ? LE2 : k == 8 ? LE1 : k == 9 ? LE0 : LC0;
-}
-__host__ __device__ constexpr int ready_group(int l) {
-  return (l == LD0 || l == LD1 || l == LD2) ? 0 : (l == LD3 || l == LFC || l == LE3 || l == LC1) ? 1 : 2;
-}
-
-template <int NKI>
-struct ReadyTiles {
-  using T = Tiles<NKI>;
-  static constexpr int NL = Layout<NKI>::NL;
-  __host__ __device__ static constexpr int start(int k) {
-    int t = 0;
-    for (int j = 0; j < k; ++j) t += T::count(ready_layer(j));
-    return t;
-  }
-  __host__ __device__ static TileDesc at(int tb) {
-#ifdef __HIP_DEVICE_COMPILE__
-    int k = 0;
-#pragma unroll
-    for (int j = 1; j < NL; ++j) k += tb >= start(j) ? 1 : 0;
-    const int l = (int)pick<NL>(k, [](int j) { return (int64_t)ready_layer(j); });
-    const int loc = tb - (int)pick<NL>(k, [](int j) { return (int64_t)start(j); });
-    const int sh = (int)pick<NL>(k, [](int j) { return (int64_t)T::log2i(T::inner(ready_layer(j))); });
-    const bool io = pick<NL>(k, [](int j) { return (int64_t)T::i_outer(ready_layer(j)); }) != 0;
-    const int w = 32 * (int)pick<NL>(k, [](int j) { return (int64_t)T::ni(ready_layer(j)); });
-    const int a = loc >> sh, c = loc & ((1 << sh) - 1);
-#else
-    int k = 0;
-    while (k + 1 < NL && tb >= start(k + 1)) ++k;
-    const int l = ready_layer(k), loc = tb - start(k), a = loc / T::inner(l), c = loc % T::inner(l);
-    const bool io = T::i_outer(l);
-    const int w = 32 * T::ni(l);
-#endif
-    return TileDesc{l, 32 * (io ? c : a), w * (io ? a : c), 0};
-  }
-};
-
-struct FusedArgs {
-  AdamArgs aa;
-  LossArgs la;
-  unsigned* sync;  // [0..2] group counters (zeroed by the host before the launch), [3] unused, [4] sticky spin time-out flag
-  unsigned* fault; // the handle's fault word (pinned host memory): set on a time-out, fails the next training call
-  int Bk;          // batch rows rounded to the dW K chunk
-  int nchain;      // row-chain blocks
-};
-
-#ifndef FUSED_SLEEP
-#define FUSED_SLEEP 32
-#endif
-template <int NKI>
-__global__ __launch_bounds__(NT) void fused_step_kernel(FastNet fn, RowArgs a, FusedArgs f) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  if ((int)blockIdx.x < f.nchain) {
-    chain_body<NKI>(fn, a, smem, f.sync, blockIdx.x);
-    return;
-  }
-  constexpr int NTL = Tiles<NKI>::total();
-  const int tb = blockIdx.x - f.nchain;
-  const TileDesc td = ReadyTiles<NKI>::at(tb);
-#ifdef FUSED_DIAG  // diagnostic builds: 1 = tiles exit at once, 2 = tiles exit after their wait
-  if (FUSED_DIAG == 1) return;
-#endif
-  // one lane polls its group's counter (bounded); on a time-out the tile sets the sticky flag
-  // sync[4] and SKIPS its update (reading unfinished rows would corrupt params, m and v), so a
-  // failed step leaves the old parameters of its tiles and cvae_sync_words reports it
-  __shared__ int timed_out;
-  if (threadIdx.x == 0) {
-    unsigned* cnt = f.sync + ready_group(td.layer);
-    int to = 0;
-    for (unsigned spins = 0;
-         __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)f.nchain;) {
-      __builtin_amdgcn_s_sleep(FUSED_SLEEP);  // ~FUSED_SLEEP·64 cycles: ~200 pollers must not load the fabric
-      if (++spins == (1u << 24) / FUSED_SLEEP) {
-        __hip_atomic_store(f.sync + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (f.fault) __hip_atomic_store(f.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        to = 1;
-        break;
+  auto tile = [&](int t, bool owned) {
+    SplitK sk{1, 0, nullptr, nullptr, t, 0};
+    TileDesc td;
+    LayerDev L;
+    decode_tile<NKI>(t, fn.arena, fn.Bp, fn.I, td, L);
+    if (owned)
+      wgrad_body<__bf16, PM_ADAM, false, 1>(L, td, Bk, aa, la, false, fn.S, fn.D, Z, sh.red, sh.dbp, sk, &px);
+    else
+      wgrad_body<__bf16, PM_GRAD, false, 1>(L, td, Bk, aa, la, false, fn.S, fn.D, Z, sh.red, sh.dbp, sk, &px);
+  };
+  if constexpr (!SHARED) {
+    tile(blockIdx.x, px_owner(blockIdx.x, px.world) == px.rank);  // block-uniform
+  } else {
+#pragma nounroll
+    for (int owned = 0; owned < 2; ++owned) {  // pushes first, then the owner tiles (which wait)
+#pragma nounroll
+      for (int t = blockIdx.x; t < NTL; t += G) {
+        if ((px_owner(t, px.world) == px.rank) != (owned == 1)) continue;  // block-uniform
+        __syncthreads();  // several tiles per block: the previous one's LDS is free
+        tile(t, owned == 1);
       }
     }
-    timed_out = to;
   }
-  __syncthreads();
-  if (timed_out) return;
-#ifdef FUSED_DIAG
-  if (FUSED_DIAG == 2) return;
-#endif
-  const LayerDev L = fast_layer<NKI>(td.layer, fn.arena, fn.Bp, fn.I);
-  __shared__ __attribute__((aligned(16))) WgradLds<Tiles<NKI>::ni_max()> sh;
-  if (Tiles<NKI>::ni(td.layer) == 2)
-    wgrad_body<__bf16, PM_ADAM, true, 2>(L, td, f.Bk, f.aa, f.la, tb == NTL - 1, fn.S, fn.D, Z, sh.red, sh.dbp);
-  else
-    wgrad_body<__bf16, PM_ADAM, true, 1>(L, td, f.Bk, f.aa, f.la, tb == NTL - 1, fn.S, fn.D, Z, sh.red, sh.dbp);
-  // the group counters are zeroed by the host before every fused launch (hipMemsetAsync on the
-  // same stream), never inside the kernel: a reset here could race chain blocks still adding
 }
 
 }  // namespace fchain

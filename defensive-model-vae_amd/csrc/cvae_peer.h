@@ -20,14 +20,23 @@
 // Bytes per link and step at N = 8: 35 partials in + 35 tiles' Wf/Wb out ≈ 2 × 140 KB.
 // Deadlock-free: non-owner blocks never wait, owners wait only on other ranks' non-owner blocks
 // and the loss block only on owners; every wait is bounded (CVAE_PX_TIMEOUT_MS of s_memrealtime,
-// default 2 s) and a time-out sets the handle's fault word and skips the update (cvae_fault; the
-// next training call fails).  Mailboxes are uncached fine-grained allocations mapped into every rank through IPC;
+// default 10 s) and a time-out sets the handle's fault word and skips the update (cvae_fault; the
+// next training call fails; cvae_px_reset re-arms the mailbox after the state is made whole).
+// Residency precondition: a waiting owner holds a workgroup slot, so every pusher must find one
+// without waiting for a waiter to finish.  One rank per GPU: the 281 blocks of a launch fit the
+// 512 slots (two per CU).  k ranks sharing a GPU: Σ over them of max(row-chain blocks, exchange
+// blocks) <= 512 — cvae_px_import counts the ranks on each GPU (PCI address in the blobs), gives
+// each 512/k − 1 tile blocks (each pushing all its tiles before it waits on any it owns) and
+// refuses a configuration whose row chain alone exceeds 512/k blocks.  Round 3's 4-rank stall
+// (281 blocks per rank, 1,124 against 512 slots) ran without this bound.
+// Mailboxes are uncached fine-grained allocations mapped into every rank through IPC;
 // flags and counters are system-scope atomics; ragged global batches weight the partials by
 // c_r = B_r / B_global, equal shares sum and then scale by 1/N (the RCCL path's grad_scale).
 #pragma once
 #include "cvae_device.h"
 
 constexpr int PX_MAX = 16;                 // ranks
+constexpr int PX_SLOTS_PER_CU = 2;         // workgroups of the row chain / exchange launch one CU holds
 
 // CVAE_PX_SC (default): the partials' hand-off without cache maintenance — the system-scope
 // analogue of MI355X_MICROARCH.md's sc1 form: every partial store write-through at system scope

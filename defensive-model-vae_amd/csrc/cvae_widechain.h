@@ -229,70 +229,52 @@ struct Plan {
                 "step plan");
 };
 
-#ifndef CVAE_RING_SKIP
-#define CVAE_RING_SKIP 1
-#endif
 #ifndef CVAE_DIAG_NOPHILOX
 #define CVAE_DIAG_NOPHILOX 0  // timing only: eps = 0 without the Philox draws
 #endif
-#ifndef CVAE_EPS_W0
-#define CVAE_EPS_W0 1  // small latent (SZ): only wave 0 (whose lanes hold mu, logvar) draws eps
-#endif
-#ifndef CVAE_EPS_PRO
-#define CVAE_EPS_PRO 1  // small latent (SZ): the eps draw in the prologue, not in the encoder-L1 GEMM
-#endif
 #ifndef CVAE_DIAG_NOADAMPRE
 #define CVAE_DIAG_NOADAMPRE 0  // timing only: no Adam-scalar precompute in block 0
-#endif
-#ifndef CVAE_EPS_PRO_WIDE
-// wide latent: eps draws per wave moved from the E0 GEMM to the prologue — 2 of 4 in the e4m3 form
-// (half the E0 bytes: its GEMM is VALU-bound, step 54.8 -> 54.2 us), none in bf16 (its E0 is
-// stream-bound; the prologue only grows: +0.3-0.9 us; profiles/r03i/epswide_ab_*.txt)
-#define CVAE_EPS_PRO_WIDE (A::F8 ? 2 : 0)
-#endif
-#ifndef CVAE_WARM
-#define CVAE_WARM 0  // A/B option: prologue L2 warm-up of E0's (1) and the last decoder layer's (2) fragments
 #endif
 template <int P>
 struct Ring {
   bf16x8 r[P];
 };
 
-#ifndef CVAE_PRE_FILL
-// ring items issued in front of the x-tile wait, the rest after the transform: fewer weight lines
-// compete with the x tile's (cfg2 step -0.25 us against the whole fill in front, 0 in front -0.1;
-// profiles/r03g/prologue_ab.txt)
-#define CVAE_PRE_FILL 4
-#endif
-#ifndef CVAE_X0_8B
-#define CVAE_X0_8B 1  // the start point of a row by an 8-B load (elements 0..3) instead of 16 B
-#endif
-#ifndef CVAE_RING_SADDR
-#define CVAE_RING_SADDR 1  // e4m3 form: scalar-base global loads (see wload)
-#endif
-#ifndef CVAE_RING_BUF
-#define CVAE_RING_BUF 1
-#endif
-// one 16-B piece of fragment item at byte offset `off` from the arena base.  CVAE_RING_BUF: a
+// Measured choices of the prologue and the stream, kept as constants (the A/B numbers are in DESIGN
+// §5; the losing forms were removed in round 4):
+//  * kPreFill ring items are issued in front of the x-tile wait, the rest after the transform: fewer
+//    weight lines compete with the x tile's (cfg2 step -0.25 us against the whole fill in front, 0 in
+//    front -0.1; profiles/r03g/prologue_ab.txt);
+//  * the start point of a row is one 8-B load (elements 0..3), not 16 B (-0.08 us);
+//  * small latent (SZ): only wave 0 (whose lanes hold mu, logvar) draws eps, in the prologue while
+//    the x tile is in flight (C0 ‖ E0 2.44 -> 1.80 us, profiles/r03g/eps_ab.txt);
+//  * wide latent: kEpsProWide of each wave's eps draws move from the E0 GEMM to the prologue — 2 of
+//    4 in the e4m3 form (its E0 streams half the bytes and is VALU-bound: step 54.8 -> 54.2 us), none
+//    in bf16 (its E0 is stream-bound; the prologue only grows: +0.3-0.9 us;
+//    profiles/r03i/epswide_ab_*.txt);
+//  * an L2 warm-up of E0's fragments in the prologue measured +0.7-1.0 us (profiles/r03g/warm_ab.txt)
+//    and is not built.
+constexpr int kPreFill = 4;
+template <class A>
+constexpr int kEpsProWide = A::F8 ? 2 : 0;
+// one 16-B piece of fragment item at byte offset `off` from the arena base.  bf16: a
 // buffer load — lane·16 is a loop-invariant voffset, the item's offset a scalar soffset (2-3 SALU
 // per item); the 64-bit global address cost 3 VALU (one a 64-bit shift-add) + ~7 SALU per item
 // (cfg2 step 26.6 -> 26.0 us, profiles/r03g).  Not in the e4m3 form (F8): there the buffer-load
 // build failed the wide fp8 chain's run-to-run repeatability test (two runs of two, the global-load
-// build passing), cause not found.  F8 (CVAE_RING_SADDR): global loads with a scalar 64-bit base
+// build passing), cause not found.  F8: global loads with a scalar 64-bit base
 // and a 32-bit lane offset where the compiler keeps that form (2 SALU, 0 VALU per item): chain
 // 41.4 -> 40.5 us at cfg5 fp8, repeatability tests green (profiles/r03g/saddr_ab.txt)
 template <bool F8>
 __device__ __forceinline__ bf16x8 wload(const char* AR, int64_t off, int lane) {
-  if constexpr (CVAE_RING_BUF && !F8) {
+  if constexpr (!F8) {
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)AR, (short)0, 0x7fffffff, 0x00020000);
     return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, (int)off, 0));
-  } else if constexpr (CVAE_RING_SADDR) {  // global_load with a scalar base + a 32-bit lane offset
+  } else {  // global_load with a scalar base + a 32-bit lane offset
     typedef const __attribute__((address_space(1))) char* gchar;
     gchar p = (gchar)(AR + off);
     asm volatile("" : "+s"(p));
     return *(const __attribute__((address_space(1))) bf16x8*)(p + (uint32_t)(lane * 16));
-  } else {
-    return gld<bf16x8>(AR + off + lane * 16);
   }
 }
 
@@ -315,7 +297,7 @@ __device__ __forceinline__ void ring_load(Ring<P>& ring, const char* AR, int wav
     if constexpr (st.KS && NW * (kc + 1) > A::FC_KCH) {
       // a K chunk past the layer (wave-uniform): no load, and gemm skips its MFMA
       if (w + NW * kc < A::FC_KCH) ring.r[G % P] = wload<A::F8>(AR, base + frag * 1024, lane);
-    } else if constexpr (CVAE_RING_SKIP && !st.KS && NW * (slot + 1) > st.NTL) {
+    } else if constexpr (!st.KS && NW * (slot + 1) > st.NTL) {
       // a slot past the layer's tiles: no load (wave-uniform); the stale ring register feeds an
       // MFMA whose result the epilogue drops
       if (w + NW * slot < st.NTL) ring.r[G % P] = wload<A::F8>(AR, base + frag * 1024, lane);
@@ -495,9 +477,6 @@ __device__ __forceinline__ void ring_fill(Ring<P>& ring, const char* AR, int wav
 // (MI355X_MICROARCH.md, store tail: 16-B stores halve it against the 8-B-per-lane epilogue
 // stores of a lane's 4 rows), and they leave the epilogue's critical path.  Write-through (sc1):
 // the lines leave L2 now, for the dW kernel behind, not at the kernel-end writeback.
-#ifndef CVAE_WIDE_SC1
-#define CVAE_WIDE_SC1 1
-#endif
 // The arena as a buffer resource: the 16-B stores are buffer_store_dwordx4 with the sc1 cache
 // policy (aux 16 on gfx950) through the builtin, so the compiler sees their operands.  (They were
 // an inline-asm global_store: with a one-lane f64 block added to the prologue, the stores of a
@@ -511,7 +490,7 @@ __device__ __forceinline__ ArenaDst arena_dst(const char* AR) {
 }
 __device__ __forceinline__ void st16(const ArenaDst& d, const void* p, u32x4 v) {
   if (CVAE_DIAG_NOSTORE) return;
-  __builtin_amdgcn_raw_buffer_store_b128(v, d.rs, (int)((const char*)p - d.base), 0, CVAE_WIDE_SC1 ? 16 : 0);
+  __builtin_amdgcn_raw_buffer_store_b128(v, d.rs, (int)((const char*)p - d.base), 0, 16);  // sc1
 }
 
 // rounds [R0, R1) of the 16-B copy of features [0, NF) of an LDS image (ioff layout) to the arena
@@ -538,7 +517,10 @@ __device__ __forceinline__ void img_copy(const __bf16* img, const ArenaDst& dst,
 
 // pub (the fused step, cvae_fusedring.h): after its last arena store the block drains every store
 // (all sc1) and adds 1 to each of the 8 replicas of the ready counter (pub[32 r], a line each)
-template <class A, int P>
+// TAP (parity tests only, cvae_tap_outputs): the chain also writes what its epilogues computed —
+// recon (the last decoder layer's output before the loss, fp32 (batch, S, D)), mu and logvar (fp32
+// (batch, Z)) — to a.recon_out / a.mu_out / a.lv_out: the training step's own rounding points
+template <class A, int P, bool TAP = false>
 __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const RowArgs& a, char* smem, int blk,
                                           unsigned* pub = nullptr) {
   using PL = Plan<A>;
@@ -648,8 +630,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   const uint64_t rng_off = a.ctr ? *(const __attribute__((address_space(4))) uint64_t*)a.ctr : a.offset;
 
   Ring<P> ring;
-  constexpr int PF0 = CVAE_PRE_FILL < P ? CVAE_PRE_FILL : P;  // ring items issued before the x-tile wait
-  uint32_t warm = 0;  // CVAE_WARM only
+  constexpr int PF0 = kPreFill < P ? kPreFill : P;  // ring items issued before the x-tile wait
   float s_recon = 0.f, s_kl = 0.f, s_start = 0.f, s_t0 = 0.f, s_relu = 0.f;
 
   // eps of the reparameterisation (:199-206), per mu tile k of this lane (latent j, rows 4q..4q+3):
@@ -657,8 +638,8 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   // is drawn in-kernel — a load under a branch drains the weight stream) or Philox keyed by the
   // global row (data parallelism: eps_row0 = the rank's first row).  The Philox draws (integer
   // multiplies and transcendentals, ~0.3 us of VALU per wave) run inside the stream-bound
-  // encoder-L1 GEMM, or (SZ, CVAE_EPS_PRO) in the prologue while the x tile is in flight.
-  // SZ: one tile of latents, held by wave 0's lanes n16 < Z (CVAE_EPS_W0: only wave 0 draws)
+  // encoder-L1 GEMM, or (SZ) in the prologue while the x tile is in flight.
+  // SZ: one tile of latents, held by wave 0's lanes n16 < Z (only wave 0 draws)
   constexpr int NZT = A::SZ ? 1 : Z / 128;
   f32x4 ep[NZT];
   const int rowq = 4 * q + (n16 & 3);  // the row this lane draws (4 latents) before the quad transpose
@@ -677,10 +658,10 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     ep[k] = quad_t(e);
   };
   auto draw_eps = [&](auto kk) { eps_make(kk, eps_load(decltype(kk)::value)); };
-  constexpr bool EPS_PRO = A::SZ && CVAE_EPS_PRO;  // the draw sits in the prologue
+  constexpr bool EPS_PRO = A::SZ;  // the draw sits in the prologue
   // wide latent (NZT tiles per wave): draws 0 .. NPRO-1 in the prologue, the rest in the E0 GEMM
-  constexpr int NPRO = EPS_PRO ? 1 : A::SZ ? 0 : (CVAE_EPS_PRO_WIDE < NZT ? CVAE_EPS_PRO_WIDE : NZT);
-  const bool eps_mine = !A::SZ || !CVAE_EPS_W0 || wave == 0;  // wave-uniform
+  constexpr int NPRO = EPS_PRO ? 1 : (kEpsProWide<A> < NZT ? kEpsProWide<A> : NZT);
+  const bool eps_mine = !A::SZ || wave == 0;  // wave-uniform
 
   // ---- prologue: x tile (relative transform, Training_VAE.py:345-348), biases, LDS pads
   // x_f32 (CVAE_X_F32: real data with ~200 m absolute coordinates): fp32 rows, the start point
@@ -721,16 +702,10 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
         const bf16x8 v = gld<bf16x8>(xg + gr[u] * I + cc[u] * 8);
 #pragma unroll
         for (int e = 0; e < 8; ++e) xv[u][e] = (float)v[e];
-        // the row's start point x[:,0,1:3] (Training_VAE.py:345): elements 0..3 (8 B) or 0..7 (16 B)
-        if constexpr (CVAE_X0_8B) {
-          const bf16x4 v0 = gld<bf16x4>(xg + gr[u] * I);
+        // the row's start point x[:,0,1:3] (Training_VAE.py:345): elements 0..3, one 8-B load
+        const bf16x4 v0 = gld<bf16x4>(xg + gr[u] * I);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) x0[u][e] = e < 4 ? (float)v0[e & 3] : 0.f;
-        } else {
-          const bf16x8 v0 = gld<bf16x8>(xg + gr[u] * I);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) x0[u][e] = (float)v0[e];
-        }
+        for (int e = 0; e < 8; ++e) x0[u][e] = e < 4 ? (float)v0[e & 3] : 0.f;
       }
     }
     // EPS_PRO: the host-eps load right behind the x tile (the x wait then covers it)
@@ -762,27 +737,13 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
       if (tid < 2 * A::Np(A::LCE) * A::Kp(A::LCE) / 16) tab = gld<u32x4>(AR + A::wf(A::LCE) + 16 * tid);
     }
     // the weight stream queues behind the x tile and the biases (vmcnt retires in order)
-    // the first PF0 items of the stream here, the rest after the x-tile transform (CVAE_PRE_FILL)
+    // the first PF0 items of the stream here, the rest after the x-tile transform (kPreFill)
     sfor<0, PF0>([&](auto g) { ring_load<A, P, decltype(g)::value>(ring, AR, wave, lane); });
     sfor<0, NPRO>([&](auto kk) {  // the Philox VALU issues while the x tile is in flight
       constexpr int k = decltype(kk)::value;
       if (CVAE_DIAG_NOPHILOX || !eps_mine) ep[k] = f32x4{0.f, 0.f, 0.f, 0.f};
       else eps_make(kk, eh0[k]);
     });
-    if constexpr (CVAE_WARM > 0) {
-      // L2 warm-up (A/B option): the Adam step rewrote every operand copy, so each XCD's L2 meets
-      // the stream's first lines cold.  The 8 blocks of an XCD (blk ≡ x mod 8) touch one dword per
-      // 128-B line of the big GEMMs' fragments, 1/8 each, one lane per line, behind the ring fill
-      // (in-order vmcnt: no earlier wait covers them); the value is kept live to the kernel's end
-      auto touch = [&](int64_t lo, int64_t bytes) {
-        const int nl = (int)((bytes + 127) / 128), j = (blk >> 3) & 7, per = (nl + 7) / 8;
-        const int l0 = j * per, n = min(per, nl - l0);
-        for (int k = lane; k < n; k += 64) warm |= gld<uint32_t>((const uint32_t*)(AR + lo + 128LL * (l0 + k)));
-      };
-      if (wave == 0) touch(A::wf(A::LE0), 2LL * A::Np(A::LE0) * A::Kp(A::LE0));
-      if (CVAE_WARM > 1 && wave == 1) touch(A::wf(A::LDL), 2LL * A::Np(A::LDL) * A::Kp(A::LDL));
-      if (CVAE_WARM > 1 && wave == 2) touch(A::wb(A::LDL), 2LL * A::Np(A::LDL) * A::Kp(A::LDL));
-    }
     // device counters: this launch begins optimizer step ctr[1] + 1 and precomputes its Adam
     // scalars for the dW kernel behind it.  Wave 0 of block 0, wave-uniformly, while it waits for
     // the x tile: the step count by scalar load, the f64 pow on every lane, one lane stores (at
@@ -972,6 +933,10 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
         const float sd = __expf(0.5f * lv[0][i]);
         z[i] = mu[0][i] + ep[0][i] * sd;
         if (4 * q + i < nrows) s_kl += 1.f + lv[0][i] - mu[0][i] * mu[0][i] - __expf(lv[0][i]);
+        if (TAP && 4 * q + i < nrows) {
+          if (a.mu_out) a.mu_out[(size_t)(b0 + 4 * q + i) * Z + j] = mu[0][i];
+          if (a.lv_out) a.lv_out[(size_t)(b0 + 4 * q + i) * Z + j] = lv[0][i];
+        }
       }
       img(DCAT, j, to_bf4(z));
     }
@@ -989,6 +954,10 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
       const float sd = __expf(0.5f * lv[k][i]);
       z[i] = mu[k][i] + ep[k][i] * sd;
       if (4 * q + i < nrows) s_kl += 1.f + lv[k][i] - mu[k][i] * mu[k][i] - __expf(lv[k][i]);
+      if (TAP && 4 * q + i < nrows) {
+        if (a.mu_out) a.mu_out[(size_t)(b0 + 4 * q + i) * Z + j] = mu[k][i];
+        if (a.lv_out) a.lv_out[(size_t)(b0 + 4 * q + i) * Z + j] = lv[k][i];
+      }
     }
     img2(IDC{}, j, to_bf4(z));
   }, scl(integral_constant<int, PL::sFC>{}));
@@ -1046,6 +1015,12 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
         const f32x2 g01 = d01 * cr * inv_BSD, g23 = d23 * cr * inv_BSD;  // w_recon·2·diff / (B·S·D)
         gi = f32x4{g01[0], g01[1], g23[0], g23[1]};
         const f32x4 r = {r01[0], r01[1], r23[0], r23[1]};
+        if constexpr (TAP) {
+          if (a.recon_out)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              if (4 * q + i < nrows) a.recon_out[(size_t)(b0 + 4 * q + i) * I + f] = r[i];
+        }
         if (16 * t < D) {  // wave-uniform: only these n-tiles hold timestep-0 features
           const f32x4 df = {d01[0], d01[1], d23[0], d23[1]};
 #pragma unroll
@@ -1240,7 +1215,6 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     __hip_atomic_store((unsigned*)(a.partials + blk * 8 + tid), __builtin_bit_cast(unsigned, s), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);  // sc1: the fused step's loss block reads it
   }
-  if constexpr (CVAE_WARM > 0) asm volatile("" ::"v"(warm));
   if (pub) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lbar();
@@ -1271,7 +1245,7 @@ constexpr int RING = CVAE_WIDE_RING;
 // ctr (the device step counters) rides in the preloaded kernel-argument SGPRs beside the x-tile
 // arguments: read from RowArgs, the Philox-offset load waited for a kernel-argument fetch before
 // the first x load could issue
-template <class A>
+template <class A, bool TAP = false>
 __global__ __launch_bounds__(NT) void widechain_kernel(char* arena, const void* x, const int64_t* idx, int Bp,
                                                        int batch, uint64_t* ctr, RowArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1280,7 +1254,7 @@ __global__ __launch_bounds__(NT) void widechain_kernel(char* arena, const void* 
   ra.idx = idx;
   ra.batch = batch;
   ra.ctr = ctr;
-  wide_body<A, A::SZ ? CVAE_RING_P : RING>(arena, Bp, ra, smem, blockIdx.x);
+  wide_body<A, A::SZ ? CVAE_RING_P : RING, TAP>(arena, Bp, ra, smem, blockIdx.x);
 }
 
 }  // namespace wchain

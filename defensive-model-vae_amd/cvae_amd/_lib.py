@@ -70,7 +70,6 @@ _SIGS = {
     "cvae_train_steps": (_i, [_v, _v, _v, _v, _i, _i, _i, _v, _u64, _u64, _i64, _W, _v, _v, _v, _i64, _A, _v, _v,
                               _v, _v]),
     "cvae_bench_kernels": (_i, [_v, _v, _v, _i, _i, _v, _v, _v, _i64, C.POINTER(_f), _v]),
-    "cvae_sync_words": (_i, [_v, C.POINTER(C.c_uint)]),
     "cvae_step_launches": (_i, [_v, C.POINTER(C.c_int)]),
     "cvae_ring_sync_words": (_i, [_v, C.POINTER(C.c_uint)]),
     "cvae_fault": (_i, [_v, C.POINTER(C.c_uint)]),
@@ -83,6 +82,10 @@ _SIGS = {
     "cvae_px_probe": (_i, [_v, C.POINTER(_i)]),
     "cvae_px_close": (_i, [_v]),
     "cvae_px_stats": (_i, [_v, C.POINTER(C.c_uint64), _i]),
+    "cvae_px_layout": (_i, [_v, C.POINTER(_i), C.POINTER(_i)]),  # h, ranks_on_gpu, tile_blocks
+    "cvae_px_reset": (_i, [_v, _u64]),                            # h, base
+    "cvae_operand_checksum": (_i, [_v, _v, _v]),                  # h, out (device u64), stream
+    "cvae_tap_outputs": (_i, [_v, _v, _v, _v]),                   # h, recon, mu, logvar
     # h, x, idx, batch, xflags, eps, seed, eps_row0, w, params, m, v, adam, rank_scales, loss_out, loss_accum,
     # counters, stream
     "cvae_px_train_step": (_i, [_v, _v, _v, _i, _i, _v, _u64, _i64, _W, _v, _v, _v, _A, _v, _v, _v, _v, _v]),

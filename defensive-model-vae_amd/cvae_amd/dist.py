@@ -113,9 +113,11 @@ class DataParallelStep:
             dist.broadcast(self.engine.params, src, group=self.group)
             self.engine.pack()
 
-    def step(self, x, idx=None, eps=None, batch=None, global_batch=None, weights=None, row0=None, classes=None):
+    def step(self, x, idx=None, eps=None, batch=None, global_batch=None, weights=None, row0=None, classes=None,
+             sizes=None):
         """One data-parallel training step; ``batch`` = this rank's rows, ``global_batch`` = Σ over
-        ranks, ``row0`` = this rank's first row in the global batch (default: rank · batch)."""
+        ranks, ``row0`` = this rank's first row in the global batch (default: rank · batch);
+        ``sizes`` = every rank's rows (peer exchange; default: ``split_rows`` shares)."""
         eng = self.engine
         if batch is None:
             batch = idx.numel() if idx is not None else x.shape[0]
@@ -123,12 +125,12 @@ class DataParallelStep:
         if global_batch is None:
             global_batch = batch * self.world_size
         if row0 is None:
-            row0 = self.rank * batch
+            row0 = self.rank * batch if sizes is None else sum(sizes[:self.rank])
         if self.px is not None:
             if classes is not None:
                 raise ValueError("the peer exchange serves the reference model (no class embedding)")
             return self.px.step(x, idx=idx, eps=eps, batch=batch, global_batch=global_batch, weights=weights,
-                                row0=row0)
+                                row0=row0, sizes=sizes)
         if not self.split:
             if batch > 0:
                 eng.train_step(x, idx=idx, eps=eps, batch=batch, weights=weights, row0=row0,
@@ -171,16 +173,25 @@ class DataParallelStep:
         if self.px is not None:
             self.px.gather_state()
 
-    def verify_exchange(self):
-        """The peer exchange's warm-up self-check (``PeerExchange.verify``); on a failure every rank
-        closes it together and continues on the RCCL all-reduce (the master state was made whole by
-        the check, so the ranks agree).  Returns True or the failure, which ``exchange_note`` keeps."""
+    def counters_changed(self):
+        """The device step counter was set from outside the step (a resume, a restore): the peer
+        exchange counts its flag epochs from it and must be re-armed (collective)."""
+        if self.px is not None:
+            self.px.reset()
+
+    def verify_exchange(self, fallback=True):
+        """The peer exchange's self-check (``PeerExchange.verify``).  On a failure with ``fallback``
+        every rank closes it together, clears its fault word and continues on the RCCL all-reduce:
+        the master state was made whole by the check, so the ranks agree, and a fault word left set
+        would fail the RCCL path's first call.  Returns True or the failure, which
+        ``exchange_note`` keeps."""
         if self.px is None:
             return True
         ok = self.px.verify()
-        if ok is not True:
+        if ok is not True and fallback:
             self.px.close()
             self.px = None
+            self.engine.clear_fault()
             self.exchange = "rccl"
             self.exchange_note = f"peer exchange failed its warm-up check ({ok}); rccl"
         return ok

@@ -378,6 +378,28 @@ class CVAEEngine:
         self._last_batch = B
         return self.loss
 
+    def forward_backward_outputs(self, x, idx=None, eps=None, batch=None, weights=None, row0=0):
+        """``forward_backward`` whose row chain also returns what its epilogues computed — recon
+        (B,S,D), mu and logvar (B,Z), fp32 — at the training step's own rounding points
+        (cvae_tap_outputs; the ring chain only).  Parity checks of the bf16 headline path."""
+        S, D, Z = self.shape[:3]
+        B = int(batch if batch is not None else (len(idx) if idx is not None else x.shape[0]))
+        kw = dict(device=self.device, dtype=torch.float32)
+        recon, mu, lv = torch.empty(B, S, D, **kw), torch.empty(B, Z, **kw), torch.empty(B, Z, **kw)
+        check(lib().cvae_tap_outputs(self._h, ptr(recon), ptr(mu), ptr(lv)), "cvae_tap_outputs")
+        try:
+            self.forward_backward(x, idx=idx, eps=eps, batch=B, weights=weights, row0=row0)
+        finally:
+            lib().cvae_tap_outputs(self._h, None, None, None)  # one-shot even if the call failed early
+        return recon, mu, lv
+
+    def operand_checksum(self):
+        """cvae_operand_checksum of the device operand copies (W, Wᵀ, biases) as a Python int
+        (synchronises): equal on every rank of the peer exchange, and to its value after a repack."""
+        out = torch.zeros(1, device=self.device, dtype=torch.int64)
+        check(lib().cvae_operand_checksum(self._h, ptr(out), self._stream()), "cvae_operand_checksum")
+        return int(out.item()) & (2 ** 64 - 1)
+
     def wgrad_rest(self, batch=None):
         """The second dW bucket (condition encoder, encoder, fc) of the batch the last
         ``forward_backward(parts=CHAIN|DW_DEC)`` ran."""
@@ -514,13 +536,6 @@ class CVAEEngine:
                                        ptr(self.v), self.step_count + 1, ms, self._stream()), "cvae_bench_kernels")
         self.step_count = self.step_count + 2 * int(reps)
         return {"rowchain": ms[0], "wgrad_adam": ms[1], "step": ms[2]}
-
-    def sync_words(self):
-        """The fused launch's hand-off words (cvae_sync_words): [group0, group1, group2, unused,
-        sticky time-out flag]; the counters are zeroed before every launch."""
-        out = (C.c_uint * 5)()
-        check(lib().cvae_sync_words(self._h, out), "cvae_sync_words")
-        return list(out)
 
     def ring_sync_words(self):
         """The one-launch step's hand-off words (cvae_ring_sync_words): 8 ready-counter replicas,

@@ -87,20 +87,57 @@ class PeerExchange:
         self.owned = torch.frombuffer(bytearray(mask), dtype=torch.uint8).to(engine.device).bool()
         self._open = True
 
-    def step(self, x, idx=None, eps=None, batch=None, global_batch=None, weights=None, row0=None, accumulate=True):
-        """One data-parallel step: this rank's ``batch`` rows (0 allowed) of a global batch."""
+    def layout(self):
+        """(ranks on this rank's GPU, tile blocks of the exchange launch) — cvae_px_layout: the
+        residency precondition the launch was sized for (csrc/cvae_peer.h)."""
+        k, g = C.c_int(), C.c_int()
+        check(lib().cvae_px_layout(self.engine._h, C.byref(k), C.byref(g)), "cvae_px_layout")
+        return k.value, g.value
+
+    def reset(self):
+        """Re-arm the exchange (collective): after a resume or a restore changed the device step
+        counter, or after a bounded wait timed out (the fault word; make the state whole first —
+        ``gather_state``).  Every rank synchronises, meets a barrier, zeroes its arrival flags and
+        done counter, counts the step epoch from the current counters[1] (which must agree on every
+        rank) and clears its fault word; a second barrier keeps anyone from pushing early."""
+        eng = self.engine
+        torch.cuda.synchronize(eng.device)
+        base = eng.sync_counters()[1]
+        steps = [None] * self.world
+        dist.all_gather_object(steps, base, group=self.group)
+        if len(set(steps)) != 1:
+            raise RuntimeError(f"peer exchange reset: optimizer steps differ across ranks {steps}")
+        dist.barrier(group=self.group)
+        check(lib().cvae_px_reset(eng._h, int(base)), "cvae_px_reset")
+        dist.barrier(group=self.group)
+
+    def step(self, x, idx=None, eps=None, batch=None, global_batch=None, weights=None, row0=None, accumulate=True,
+             sizes=None):
+        """One data-parallel step: this rank's ``batch`` rows (0 allowed) of a global batch.
+
+        ``sizes``: every rank's row count.  Without it the shares are the ones ``dist.split_rows``
+        gives (as every rank computes them alike: no collective); a rank whose batch differs from
+        its share there raises instead of weighting its partial wrongly."""
         eng = self.engine
         if batch is None:
             batch = idx.numel() if idx is not None else x.shape[0]
         batch = int(batch)
         if global_batch is None:
             global_batch = batch * self.world
+        global_batch = int(global_batch)
+        if sizes is None:
+            q, r = divmod(global_batch, self.world)
+            sizes = [q + (1 if k < r else 0) for k in range(self.world)]
+            if sizes[self.rank] != batch:
+                raise ValueError(f"rank {self.rank}: batch {batch} is not its split_rows share {sizes[self.rank]} of "
+                                 f"global batch {global_batch}; pass sizes= (every rank's rows)")
+        sizes = [int(s) for s in sizes]
+        if len(sizes) != self.world or sum(sizes) != global_batch or sizes[self.rank] != batch:
+            raise ValueError(f"sizes {sizes} do not describe rank {self.rank}'s batch {batch} of {global_batch}")
         if row0 is None:
-            row0 = self.rank * batch
+            row0 = sum(sizes[:self.rank])
         scales = None
-        if batch * self.world != global_batch:  # ragged: every rank needs every rank's weight
-            sizes = [None] * self.world
-            dist.all_gather_object(sizes, batch, group=self.group)
+        if any(s != sizes[0] for s in sizes):  # ragged: the partials are weighted by B_r / B_global
             scales = (C.c_float * self.world)(*[s / global_batch for s in sizes])
         xp = idxp = ep = None
         xfl = CVAE_X_OPERAND
@@ -151,16 +188,21 @@ class PeerExchange:
                 "owner_wait_mean_us": out[2] / 100.0 / max(out[3], 1), "owner_waits": int(out[3])}
 
     def verify(self, rows=64):
-        """Self-check after warm-up, outside any timed region; collective over the group.  The
-        operand copies the owners wrote into this rank's workspace must equal, bit for bit, the ones
-        packed from the whole master state: a forward pass over the same seeded rows (eps = 0)
-        before and after ``gather_state()`` must give identical outputs, and no rank's fault word
-        may be set.  Returns True, or the first failing rank's reason (the same value on every
-        rank; a local error becomes a reason, so no rank is left in a collective)."""
+        """Self-check outside any timed region (bench.py runs it after warm-up AND after the timed
+        steps); collective over the group.  Passes when
+          * no rank's fault word is set (no bounded wait gave up);
+          * every rank's operand copies — written by the tiles' owners — have the same checksum
+            (cvae_operand_checksum over every byte of W, Wᵀ and the biases), and that checksum is
+            unchanged by ``gather_state()``'s repack from the whole master state: the broadcast
+            delivered the owners' update, byte for byte, everywhere;
+          * a forward pass over seeded rows (eps = 0) gives identical outputs before and after.
+        Returns True, or the first failing rank's reason (the same value on every rank; a local
+        error becomes a reason, so no rank is left in a collective)."""
         eng = self.engine
         S, D, Z = eng.shape[:3]
         rows = min(int(rows), eng.max_batch)
         reason = before = None
+        ck_before = 0
 
         def outs(probe, eps):
             return torch.cat([t.flatten() for t in eng.forward(probe, eps=eps, batch=rows, offset=0)])
@@ -170,23 +212,34 @@ class PeerExchange:
             if f:
                 reason = f"fault word {f:#x} (a bounded wait gave up)"
             else:
+                ck_before = eng.operand_checksum()
                 probe = eng.as_input(torch.randn(rows, S, D, generator=torch.Generator().manual_seed(7)))
                 eps = torch.zeros(rows, Z, device=eng.device, dtype=torch.float32)
                 before = outs(probe, eps)
         except Exception as e:  # noqa: BLE001
             reason = f"{type(e).__name__}: {e}"
+        cks = [None] * self.world
+        dist.all_gather_object(cks, ck_before, group=self.group)
+        if reason is None and len(set(cks)) != 1:
+            reason = f"operand-copy checksums differ across ranks {[hex(c) for c in cks]}"
         self.gather_state()
         if reason is None:
             try:
-                after = outs(probe, eps)
-                if not torch.equal(before, after):
-                    n = int((before != after).sum())
-                    reason = f"{n} forward outputs differ between the broadcast and the repacked operand copies"
+                ck_after = eng.operand_checksum()
+                if ck_after != ck_before:
+                    reason = (f"operand-copy checksum {ck_before:#x} (broadcast) != {ck_after:#x} (repacked from "
+                              f"the gathered master state)")
+                else:
+                    after = outs(probe, eps)
+                    if not torch.equal(before, after):
+                        n = int((before != after).sum())
+                        reason = f"{n} forward outputs differ between the broadcast and the repacked operand copies"
             except Exception as e:  # noqa: BLE001
                 reason = f"{type(e).__name__}: {e}"
         reasons = [None] * self.world
         dist.all_gather_object(reasons, reason, group=self.group)
         bad = [(r, v) for r, v in enumerate(reasons) if v]
+        self.last_checksum = cks[0]
         return True if not bad else f"rank {bad[0][0]}: {bad[0][1]}"
 
     def gather_state(self):

@@ -180,6 +180,7 @@ def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidd
         loss_history = {k: list(ck["loss_history"][k]) for k in LOSS_KEYS}
         first = ck["epoch"]
         step.broadcast_params()
+        step.counters_changed()  # the peer exchange counts its flag epochs from the device step counter
     for epoch in range(first, epochs):
         for rows in loader:                               # (:340) one global batch
             g = rows.numel()

@@ -280,13 +280,6 @@ int cvae_kernel_times(cvae_handle* h, char* names, int names_len, float* ms, int
 int cvae_bench_kernels(cvae_handle* h, const void* x, const int64_t* idx, int batch, int reps,
                        float* params, float* m, float* v, int64_t step0, float* ms, void* stream);
 
-/* The five hand-off words of the fused training launch (three group counters, finished tiles, spin
- * time-out flag), copied to `out` (host, 5 entries).  The counters are zeroed before every fused
- * launch; a non-zero time-out flag means a tile gave up waiting and skipped its update (that
- * step's parameters are incomplete: the caller must treat the step as failed).  Synchronises
- * the device. */
-int cvae_sync_words(cvae_handle* h, unsigned* out);
-
 /* The one-launch training step of the reference architecture at S = 100 (the ring chain, every
  * dW ⊕ Adam tile and the loss block in ONE kernel; replaces the chain + dW pair of
  * cvae_train_step when enabled — CVAE_FUSE_RING at handle creation):
@@ -306,6 +299,20 @@ int cvae_ring_sync_words(cvae_handle* h, unsigned* out);
  * cvae_clear_fault resets it (after the caller restored consistent parameters). */
 int cvae_fault(const cvae_handle* h, unsigned* word);
 int cvae_clear_fault(cvae_handle* h);
+
+/* Checksum of the handle's device operand copies (every layer's padded W and Wᵀ in the operand
+ * dtype and the padded fp32 biases — what the row chain multiplies by): Σ over their 8-B words w_i
+ * of splitmix64(w_i ^ i·0x9E3779B97F4A7C15) mod 2^64, written to the DEVICE word `out`.  Under the
+ * peer exchange every rank's copies are written by the tiles' owners: equal checksums on every
+ * rank, and equal to the checksum after a repack from the gathered master state, show the
+ * broadcast delivered every byte.  Queued on `stream`. */
+int cvae_operand_checksum(cvae_handle* h, uint64_t* out, void* stream);
+
+/* Parity taps (tests): the NEXT training call's row chain also writes what its epilogues computed
+ * at the training step's own rounding points — recon fp32 (batch,S,D) (the last decoder layer's
+ * output, Training_VAE.py:215, before the loss), mu and logvar fp32 (batch,Z) (:195-196); any may be
+ * NULL.  One-shot.  Served by the ring chain (CVAE_KERNEL_RING) only; another chain fails that call. */
+int cvae_tap_outputs(cvae_handle* h, float* recon, float* mu, float* logvar);
 
 /* ---- Data parallelism over xGMI without a collective library (Training_VAE.py:362-363
  * across ranks): the "peer exchange".  One process per GPU; every rank's workspace and a mailbox
@@ -336,6 +343,19 @@ int cvae_px_train_step(cvae_handle* h, const void* x, const int64_t* idx, int ba
                        const cvae_adam_config* adam, const float* rank_scales, float* loss_out, double* loss_accum,
                        uint64_t* counters, void* stream);
 int cvae_px_close(cvae_handle* h);
+/* The residency precondition (csrc/cvae_peer.h): a waiting owner block holds a workgroup slot, so
+ * the blocks of every rank on one GPU must fit that GPU's slots together.  cvae_px_import counts
+ * the ranks on this rank's GPU (PCI address in the blobs) and sizes the exchange launch: one rank
+ * per GPU runs one block per tile; k sharing ranks run 2·CUs/k − 1 tile blocks each (a block
+ * pushes all its tiles before it waits on any it owns), and import fails when the row chain alone
+ * needs more than 2·CUs/k blocks.  *ranks_on_gpu = k, *tile_blocks = the launch's tile blocks. */
+int cvae_px_layout(const cvae_handle* h, int* ranks_on_gpu, int* tile_blocks);
+/* Re-arm the exchange after every rank synchronised and met a barrier (collective by contract):
+ * zero this rank's arrival flags and done counter, count the step epoch from `base` (= counters[1]
+ * now, the same on every rank: after a resume or a restore) and clear the fault word.  A timed-out
+ * step leaves the flag epochs short; restore consistent state (gather it), then call this on every
+ * rank before the next step.  Synchronises the device. */
+int cvae_px_reset(cvae_handle* h, uint64_t base);
 /* Set-up check after cvae_px_import (every rank calls it once, concurrently): each rank stores a
  * tagged word into every peer's mailbox and waits (bounded, ~1 s) for theirs; *ok = 1 when every
  * peer's tag arrived intact.  Synchronises the device. */

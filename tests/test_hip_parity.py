@@ -231,8 +231,10 @@ def _cfg2(cvae, dtype, B, seed=0):
 # bf16 vs the fp32 reference: the CPU bf16 emulation (tests/golden-free, oracle/cvae_np.py q=bf16)
 # shows rel-L2 up to 0.081 (encoder L1 weight, B=64) / 0.031 (B=1024) from operand rounding
 # alone; the tolerances below bound that, and the emulation test above pins the kernel tightly.
-@pytest.mark.parametrize("dtype,B,ltol,gtol", [("fp32", 64, 2e-5, 1e-4), ("bf16", 64, 2e-2, 1.2e-1),
-                                               ("bf16", 1024, 2e-2, 6e-2)])
+# Loss terms: SURVEY §8c's ELBO tolerance (rel <= 1e-2); the emulation's own distance from fp32 is
+# <= 3.5e-3 (KL and start terms) at B = 64 and 1024.
+@pytest.mark.parametrize("dtype,B,ltol,gtol", [("fp32", 64, 2e-5, 1e-4), ("bf16", 64, 1e-2, 1.2e-1),
+                                               ("bf16", 1024, 1e-2, 6e-2)])
 def test_cfg2_shape_vs_oracle(cvae, golden, dtype, B, ltol, gtol):
     ref, m, eng, x, eps = _cfg2(cvae, dtype, B)
     if dtype == "bf16":
@@ -249,6 +251,44 @@ def test_cfg2_shape_vs_oracle(cvae, golden, dtype, B, ltol, gtol):
     g = _grads(m, eng)
     for k, p in ref.named_parameters():
         assert rel_l2(g[k], p.grad.numpy()) < gtol, (k, rel_l2(g[k], p.grad.numpy()))
+
+
+@pytest.mark.parametrize("B", [37, 1024])
+def test_ring_chain_reconstruction_bf16_vs_oracle(cvae, B):
+    """north_star: "reconstructions and ELBO match the reference CPU VAE within a stated fp
+    tolerance" at the headline dtype — recon (Training_VAE.py:215), mu and logvar (:195-196) as the
+    TRAINING step's ring chain computes them (cvae_tap_outputs: its own epilogue values, bf16
+    operands and activations, fp32 accumulation), and the five loss terms (:240-267), on the same
+    bf16-rounded inputs and eps.
+    Against the fp32 oracle: recon rel-L2 <= 2e-2, ELBO terms rel <= 1e-2, mu / logvar
+    rel-L2 <= 1e-2.  Against the CPU emulation of the chain's rounding points (cvae_np q=bf16):
+    recon / mu / logvar rel-L2 <= 5e-3, losses rel <= 2e-3.  The tapped launch equals the untapped
+    one bit for bit (the tap adds stores, not rounding points)."""
+    ref, m, eng, x, eps = _cfg2(cvae, "bf16", B)
+    assert eng.train_kernel == "ring"
+    x = x.to(torch.bfloat16).float()
+    recon, mu, lv = eng.forward_backward_outputs(x, eps=eps)
+    loss = eng.loss.cpu().numpy()
+    g_tap = eng.grads.clone()
+    eng.forward_backward(x, eps=eps)
+    torch.cuda.synchronize()
+    assert np.array_equal(eng.loss.cpu().numpy(), loss) and torch.equal(eng.grads, g_tap)
+    recon, mu, lv = recon.cpu().numpy(), mu.cpu().numpy(), lv.cpu().numpy()
+    rel, start = relative(x)
+    with torch.no_grad():
+        r32, mu32, lv32, hc32 = ref(rel, start, eps)
+        want = np.array([float(v) for v in oracle_loss(r32, rel, mu32, lv32, hc32, **WD)])
+    dev = {"recon": rel_l2(recon, r32.numpy()), "mu": rel_l2(mu, mu32.numpy()), "logvar": rel_l2(lv, lv32.numpy())}
+    lrel = np.abs(loss - want) / np.abs(want)
+    print(f"bf16 ring chain B={B} vs fp32 oracle: {dev}, loss rel {lrel}")
+    assert dev["recon"] <= 2e-2 and dev["mu"] <= 1e-2 and dev["logvar"] <= 1e-2, dev
+    np.testing.assert_allclose(loss, want, rtol=1e-2, atol=1e-7)
+    p = {k: v.numpy() for k, v in ref.state_dict().items()}
+    re, mue, lve, _, c = cvae_np.forward(p, x.numpy(), eps.numpy(), q=cvae_np.bf16)
+    de = {"recon": rel_l2(recon, re), "mu": rel_l2(mu, mue), "logvar": rel_l2(lv, lve)}
+    print(f"  vs bf16 emulation: {de}")
+    assert max(de.values()) <= 5e-3, de
+    np.testing.assert_allclose(loss, cvae_np.losses(re, c["rel"], mue, lve), rtol=2e-3, atol=1e-7)
 
 
 def test_bf16_training_decreases_loss_full_size(cvae):
@@ -380,36 +420,6 @@ def test_train_steps_equals_repeated_train_step(cvae):
         torch.cuda.synchronize()
         assert torch.equal(e1.params, e2.params), dtype
         assert torch.equal(e1.loss, e2.loss) and torch.equal(e1.loss_accum, e2.loss_accum), dtype
-
-
-def test_fused_step_equals_two_launch_step(cvae, monkeypatch):
-    """The fused training launch (row chain and dW ⊕ Adam tiles in one kernel, hand-off through
-    counters; CVAE_FUSE=1 at handle creation) == the two-launch step, bit for bit over several
-    steps, ragged batch included, with the device step counters; the host zeroes the hand-off
-    counters before every launch, so after the last one each group counter holds that launch's
-    chain-block count and the time-out flag is clear."""
-    S, D = 100, 6
-    torch.manual_seed(0)
-    ref = OracleCVAE(S, D, 8)
-    monkeypatch.delenv("CVAE_FUSE", raising=False)
-    monkeypatch.setenv("CVAE_RING", "0")  # the fused launch runs fastchain's body: compare with it
-    m1, e1 = _model(cvae, S, D, 8, sd=ref.state_dict(), dtype="bf16", max_batch=200)
-    monkeypatch.delenv("CVAE_RING")
-    assert e1.train_kernel == "fast"
-    monkeypatch.setenv("CVAE_FUSE", "1")
-    m2, e2 = _model(cvae, S, D, 8, sd=ref.state_dict(), dtype="bf16", max_batch=200)
-    monkeypatch.delenv("CVAE_FUSE")
-    data = torch.randn(400, S, D).cuda()
-    for i, B in enumerate((200, 200, 77, 160)):
-        idx = torch.randint(0, 400, (B,), generator=torch.Generator().manual_seed(i)).cuda()
-        e1.train_step(data, idx=idx)
-        e2.train_step(data, idx=idx)
-        torch.cuda.synchronize()
-        assert torch.equal(e1.params, e2.params), B
-        assert torch.equal(e1.m, e2.m) and torch.equal(e1.v, e2.v), B
-        assert torch.equal(e1.loss, e2.loss) and torch.equal(e1.loss_accum, e2.loss_accum), B
-    assert e2.sync_words() == [10, 10, 10, 0, 0]  # B=160: 10 chain blocks published each group
-    assert torch.equal(e1.counters, e2.counters)
 
 
 def _fring_pair(cvae, monkeypatch, max_batch=1024):
