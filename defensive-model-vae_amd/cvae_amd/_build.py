@@ -49,5 +49,33 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return LIB
 
 
+def build_asan(out_dir, verbose=False) -> tuple:
+    """The C-ABI with its HOST code under AddressSanitizer (tests/test_capi_asan.py):
+    ``-Xarch_host -fsanitize=address`` (GPU AddressSanitizer is not available here; the device code
+    is built as usual, uninstrumented), plus the host-side checker tests/asan/capi_host_check.c
+    linked against it.  Rebuilt when a source is newer.  Returns (library, checker) paths."""
+    root = os.path.dirname(os.path.dirname(HERE))
+    os.makedirs(out_dir, exist_ok=True)
+    so = os.path.join(out_dir, "libcvae_asan.so")
+    exe = os.path.join(out_dir, "capi_host_check")
+    drv = os.path.join(root, "tests", "asan", "capi_host_check.c")
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    if not os.path.exists(so) or any(os.path.getmtime(f) > os.path.getmtime(so) for f in _inputs()):
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-O1", "-g", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
+               "-Wno-pass-failed", "-mllvm", "-amdgpu-mfma-vgpr-form", "-Xarch_host", "-fsanitize=address",
+               "-Xarch_host", "-fno-omit-frame-pointer", "-o", so + ".tmp", os.path.join(CSRC, "cvae_capi.hip")]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True, cwd=CSRC)
+        os.replace(so + ".tmp", so)
+    if not os.path.exists(exe) or max(os.path.getmtime(so), os.path.getmtime(drv)) > os.path.getmtime(exe):
+        clang = os.path.join(os.path.dirname(os.path.realpath(hipcc)), "..", "llvm", "bin", "clang")
+        if not os.path.exists(clang):
+            clang = "/opt/rocm/llvm/bin/clang"
+        subprocess.run([clang, "-g", "-O1", "-fsanitize=address", "-fno-omit-frame-pointer", "-o", exe, drv,
+                        "-L" + out_dir, "-lcvae_asan", "-Wl,-rpath," + out_dir], check=True)
+    return so, exe
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
