@@ -20,6 +20,7 @@
 #include "cvae_loss.h"
 #include "cvae_fastwgrad.h"
 #include "cvae_widechain.h"
+#include "cvae_widewgrad.h"
 #include "cvae_fusedring.h"
 #include "cvae_extract.h"
 #include "cvae_mpc.h"
@@ -104,6 +105,7 @@ struct cvae_handle {
   int fast_nki = 0;         // > 0: bf16 training runs fchain::fastchain_kernel<fast_nki>
   int fast_lds = 0;
   bool wide = false;        // bf16 training at BASELINE cfg5's shape runs wchain::widechain_kernel<Cfg5>
+  bool wide_dw = false;     // ... and its dW ⊕ Adam runs wchain::widewgrad_kernel (compile-time tile decode)
   int wide_lds = 0;
   bool ring = false;        // the fast configuration's training chain runs wchain::widechain_kernel<Cfg2>
   bool ring_cls = false;    // cfg4 (class embedding) at cfg2's shape: widechain_kernel<Cfg4>, generic dW
@@ -736,6 +738,29 @@ int plan_ring_cls(cvae_handle* h) {
   return CVAE_OK;
 }
 
+// the compile-time dW decode of the wide shape (cvae_widewgrad.h) restates the handle's 32 × 64 tile
+// list and layer table exactly (CVAE_DW_NI2=0 or any other difference keeps the generic kernel)
+template <class A>
+bool wide_dw_matches(const cvae_handle* h) {
+  using WT = wchain::WTiles<A>;
+  if (!h->wtiles_ni2 || (int)h->wtiles.size() != WT::total()) return false;
+  for (int b = 0; b < WT::total(); ++b) {
+    const TileDesc t = WT::at(b), u = h->wtiles[b];
+    if (t.layer != u.layer || t.o0 != u.o0 || t.i0 != u.i0 || t.ni != u.ni) return false;
+  }
+  for (int l = 0; l < A::NL; ++l) {
+    const LayerDev& L = h->net.L[l];
+    const LayerDev F = wchain::wide_layer<A>(l, h->arena, h->net.Bp);
+    if (F.K != L.K || F.N != L.N || F.Kp != L.Kp || F.Np != L.Np || F.relu != L.relu || F.nseg != L.nseg ||
+        F.seg_rows0 != L.seg_rows0 || F.f8 != L.f8 || F.wt != L.wt || F.has_bias != L.has_bias || F.Wf != L.Wf ||
+        F.Wb != L.Wb || F.bias != L.bias || F.xT != L.xT || F.gT != L.gT)
+      return false;
+    for (int g = 0; g < 2; ++g)
+      if (F.pw[g] != L.pw[g] || F.pb[g] != L.pb[g]) return false;
+  }
+  return true;
+}
+
 template <class A>
 int plan_wide_as(cvae_handle* h) {
   // the wide chain stores to the arena through a buffer resource of 2^31 - 1 bytes
@@ -744,6 +769,8 @@ int plan_wide_as(cvae_handle* h) {
                             A::L_TOTAL));
   h->wide = true;
   h->wide_lds = A::L_TOTAL;
+  const char* g = std::getenv("CVAE_GENERIC_DW");  // "1": the generic tile-list dW kernel (A/B)
+  h->wide_dw = !(g && g[0] == '1') && wide_dw_matches<A>(h);
   return CVAE_OK;
 }
 
@@ -907,6 +934,16 @@ int launch_wgrad(cvae_handle* h, int batch, const AdamArgs& aa, const LossArgs& 
                    (const TileDesc*)h->d_tiles_part[k], bk_of(h, batch), aa, la, sk);
   }
   const int nt = (int)h->wtiles.size();
+  if (h->wide_dw) {  // BASELINE cfg5: the compile-time tile decode (cvae_widewgrad.h)
+    sk.pw = 32 * 64 + 32;
+    const int g = wchain::WTiles<wchain::Cfg5>::total() * sk.S + 1;
+    static_assert(wchain::WTiles<wchain::Cfg5>::total() == wchain::WTiles<wchain::Cfg5F8>::total(), "tile lists");
+    if (h->cfg.dtype == CVAE_FP8)
+      return klaunch(h, wchain::widewgrad_kernel<wchain::Cfg5F8, MODE>, dim3(g), dim3(WG_THREADS), 0, s, h->arena,
+                     aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), aa, la, sk);
+    return klaunch(h, wchain::widewgrad_kernel<wchain::Cfg5, MODE>, dim3(g), dim3(WG_THREADS), 0, s, h->arena,
+                   aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), aa, la, sk);
+  }
   if (h->fast_nki == 19)
     return klaunch(h, fchain::fastwgrad_kernel<19, MODE>, dim3(fchain::Tiles<19>::total() * sk.S + 1),
                    dim3(WG_THREADS), 0, s, h->arena, aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), h->net.S,

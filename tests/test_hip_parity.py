@@ -821,20 +821,53 @@ def test_wide_chain_repeatable_and_dw_tiles_bit_equal(cvae, monkeypatch, dtype):
         assert torch.equal(l, l0) and torch.equal(eng.grads, g0)
     e2.forward_backward(xd, eps=eps)
     assert torch.equal(e2.grads, g0)
-    # a fused training step (dW ⊕ Adam) on fresh engines (forward_backward advances the step count)
+    # a fused training step (dW ⊕ Adam) on fresh engines (forward_backward advances the step count):
+    # the compile-time tile decode of the wide shape (widewgrad_kernel, the default), the generic
+    # kernel over the same 32 x 64 tile list (CVAE_GENERIC_DW=1) and 32 x 32 tiles (CVAE_DW_NI2=0)
     fresh = []
-    for env in (None, "0"):
+    for env in (None, ("CVAE_DW_NI2", "0"), ("CVAE_GENERIC_DW", "1")):
         if env:
-            monkeypatch.setenv("CVAE_DW_NI2", env)
+            monkeypatch.setenv(*env)
         mm = cvae.ConditionalTrajectoryVAE(WIDE["S"], WIDE["D"], WIDE["Z"], 128, WIDE["n_enc"], WIDE["n_dec"])
         mm.load_state_dict(ref.state_dict())
         ee = mm.attach(dtype=dtype, max_batch=64, device="cuda:0")
-        monkeypatch.delenv("CVAE_DW_NI2", raising=False)
+        if env:
+            monkeypatch.delenv(env[0])
         ee.train_step(xd, eps=eps)
         fresh.append(ee)
     torch.cuda.synchronize()
-    a3, a4 = fresh
-    assert torch.equal(a3.params, a4.params) and torch.equal(a3.m, a4.m) and torch.equal(a3.v, a4.v)
+    a3 = fresh[0]
+    for a4 in fresh[1:]:
+        assert torch.equal(a3.params, a4.params) and torch.equal(a3.m, a4.m) and torch.equal(a3.v, a4.v)
+        assert torch.equal(a3.loss, a4.loss) and torch.equal(a3.counters, a4.counters)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp8"])
+def test_wide_dw_decode_split_k_equals_generic(cvae, monkeypatch, dtype):
+    """B = 8192 at the cfg5 shape: the dW launch splits K (the batch) over 4 blocks per tile with the
+    sc1 ticket hand-off; the compile-time tile decode (widewgrad_kernel) and the generic tile-list
+    kernel (CVAE_GENERIC_DW=1) give the same bits over two training steps (params, moments,
+    loss, counters)."""
+    B = 8192
+    torch.manual_seed(0)
+    ref = OracleCVAE(WIDE["S"], WIDE["D"], WIDE["Z"], 128, WIDE["n_enc"], WIDE["n_dec"])
+    engines = []
+    for env in (None, "1"):
+        if env:
+            monkeypatch.setenv("CVAE_GENERIC_DW", env)
+        mm = cvae.ConditionalTrajectoryVAE(WIDE["S"], WIDE["D"], WIDE["Z"], 128, WIDE["n_enc"], WIDE["n_dec"])
+        mm.load_state_dict(ref.state_dict())
+        engines.append(mm.attach(dtype=dtype, max_batch=B, device="cuda:0"))
+        monkeypatch.delenv("CVAE_GENERIC_DW", raising=False)
+    xd = torch.randn(B, WIDE["S"], WIDE["D"], generator=torch.Generator().manual_seed(11)).to("cuda", torch.bfloat16)
+    for _ in range(2):
+        for e in engines:
+            e.train_step(xd)
+    torch.cuda.synchronize()
+    a, b = engines
+    assert torch.isfinite(a.loss).all()
+    assert torch.equal(a.params, b.params) and torch.equal(a.m, b.m) and torch.equal(a.v, b.v)
+    assert torch.equal(a.loss, b.loss) and torch.equal(a.counters, b.counters)
 
 
 def test_wide_chain_philox_and_training_match_generic(cvae, monkeypatch):
