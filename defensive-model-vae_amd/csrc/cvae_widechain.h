@@ -92,17 +92,26 @@ struct Arch {
   static_assert(I % 8 == 0 && D >= 3, "x rows load as 16-B vectors; channels 0..2 = t, x, y");
   // the layers the fp8 form runs in e4m3 (cvae_capi.hip build_plan: padded K % 64 == 0)
   static constexpr bool f8(int l) { return F8 && Kp(l) % 64 == 0; }
+  // the layers whose dX GEMM the fp8 form runs in e4m3 (cvae_capi.hip build_plan, LayerDev::f8b):
+  // e4m3 forward operand, backward K (= Np) pairing up, a dX at all (not C0 / E0), and large enough
+  // for the halved stream to matter — at cfg5 the last decoder layer, decoder L0 and fc
+  static constexpr bool f8b(int l) {
+    return f8(l) && Np(l) % 64 == 0 && l != LC0 && l != LE0 && (Np(l) >= 512 || Kp(l) >= 512);
+  }
   // the arena as alloc_arena (cvae_capi.hip) lays it out, bf16 operands: byte offsets from its base;
   // an e4m3 layer's Wf region starts with its 256-B F8Scale header
   static constexpr int64_t r256(int64_t b) { return (b + 255) / 256 * 256; }
   static constexpr int64_t hdr(int l) { return f8(l) ? (int64_t)sizeof(F8Scale) : 0; }
+  // per layer: Wf (bf16, or e4m3 behind its F8Scale header), Wb (bf16), and where f8b: Wb8 (e4m3)
   static constexpr int64_t region(int l) {
     int64_t o = 0;
-    for (int k = 0; k < l; ++k) o += r256(2LL * Np(k) * Kp(k) + hdr(k)) + r256(2LL * Np(k) * Kp(k));
+    for (int k = 0; k < l; ++k)
+      o += r256(2LL * Np(k) * Kp(k) + hdr(k)) + r256(2LL * Np(k) * Kp(k)) + (f8b(k) ? r256(1LL * Np(k) * Kp(k)) : 0);
     return o;
   }
   static constexpr int64_t wf(int l) { return region(l) + hdr(l); }
   static constexpr int64_t wb(int l) { return region(l) + r256(2LL * Np(l) * Kp(l) + hdr(l)); }
+  static constexpr int64_t wb8(int l) { return wb(l) + r256(2LL * Np(l) * Kp(l)); }
   static constexpr int bias_off(int l) {
     int o = 0;
     for (int k = 0; k < l; ++k) o += Np(k);
@@ -176,6 +185,10 @@ struct Plan {
     if (st.layer >= 0 && !st.bwd && A::f8(st.layer)) {  // e4m3: K pairs
       st.KC = st.KS ? st.KC : st.KC / 2;
       st.F8 = 1;
+    }
+    if (st.layer >= 0 && st.bwd && A::f8b(st.layer)) {  // e4m3 dX with MX row-block scales (gemm_mxb)
+      st.KC = (st.KC + 1) / 2;
+      st.F8 = 2;
     }
     return st;
   }
@@ -288,7 +301,7 @@ __device__ __forceinline__ void ring_load(Ring<P>& ring, const char* AR, int wav
     constexpr int j = G - PL::start(s);
     constexpr int NGR = st.GRP ? st.TS / st.GRP : 1, GS = st.GRP ? st.GRP : st.TS;  // groups, slots per group
     constexpr int grp = j / (st.KC * GS), kc = (j / GS) % st.KC, slot = grp + NGR * (j % GS);
-    constexpr int64_t base = st.bwd ? A::wb(st.layer) : A::wf(st.layer);
+    constexpr int64_t base = st.bwd ? (st.F8 ? A::wb8(st.layer) : A::wb(st.layer)) : A::wf(st.layer);
     int w = wave;
     asm volatile("" : "+s"(w));  // recomputed per item: hoisted, ~400 item addresses would be live SGPRs
     int t = w + NW * slot;
