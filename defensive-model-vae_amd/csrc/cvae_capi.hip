@@ -172,10 +172,14 @@ int build_plan(cvae_handle* h) {
     LayerDev& L = n.L[l];
     L.K = ld[l].K; L.N = ld[l].N; L.Kp = rup_i(L.K, 32); L.Np = rup_i(L.N, 32); L.relu = ld[l].relu;
     L.f8 = c.dtype == CVAE_FP8 && L.Kp % 64 == 0;  // fp8 forward GEMM where K pairs up (cvae_device.h)
+    // e4m3 copy of Wᵀ for the wide chain's MX dX GEMMs (wchain::Arch::f8b): the backward K pairs up,
+    // the layer has a dX, and it is one of the large ones
+    L.f8b = L.f8 && L.Np % 64 == 0 && l != lC0(n) && l != lE(n, 0) && (L.Np >= 512 || L.Kp >= 512) ? 1 : 0;
     L.has_bias = 1;
     L.wt = 0;
     if (n.n_cls && l == lCE(n)) {  // nn.Embedding(n_classes, class_dim).weight: [K][N], no bias
       L.f8 = 0;
+      L.f8b = 0;
       L.wt = 1;
       L.has_bias = 0;
       L.nseg = 1; L.seg_rows0 = L.N;
@@ -398,12 +402,13 @@ int alloc_arena(cvae_handle* h) {
   std::vector<int64_t> offs;
   int64_t total = 0;
   auto take = [&](int64_t bytes) { int64_t o = total; total += (bytes + 255) / 256 * 256; return o; };
-  struct Off { int64_t wf, wb, bias, xT, gT; };
+  struct Off { int64_t wf, wb, wb8, bias, xT, gT; };
   std::vector<Off> lo(n.n_layers);
   for (int l = 0; l < n.n_layers; ++l) {
     LayerDev& L = n.L[l];
     lo[l].wf = take((int64_t)L.Np * L.Kp * ts + (L.f8 ? (int64_t)sizeof(F8Scale) : 0));
     lo[l].wb = take((int64_t)L.Kp * L.Np * ts);
+    lo[l].wb8 = L.f8b ? take((int64_t)L.Kp * L.Np) : -1;
     lo[l].bias = n.bias_off[l];  // planned in build_plan
   }
   const int64_t bias_base = take((int64_t)n.nbias * 4);
@@ -443,6 +448,7 @@ int alloc_arena(cvae_handle* h) {
     LayerDev& L = n.L[l];
     L.Wf = h->arena + lo[l].wf + (L.f8 ? sizeof(F8Scale) : 0);  // f8: F8Scale header in front
     L.Wb = h->arena + lo[l].wb;
+    L.Wb8 = L.f8b ? h->arena + lo[l].wb8 : nullptr;
     L.bias = (float*)(h->arena + bias_base) + lo[l].bias;
     L.xT = h->arena + lo[l].xT;
     L.gT = h->arena + lo[l].gT;
@@ -683,7 +689,8 @@ bool wide_layout_matches(const cvae_handle* h) {
     if (L.Kp != A::Kp(l) || L.Np != A::Np(l) || n.bias_off[l] != A::bias_off(l) || (L.f8 != 0) != A::f8(l) ||
         (char*)L.Wf != h->arena + A::wf(l) || (char*)L.Wb != h->arena + A::wb(l) ||
         (char*)L.xT != h->arena + A::act0 + Bp2 * A::xrows(l) ||
-        (char*)L.gT != h->arena + A::act0 + Bp2 * A::grows(l))
+        (char*)L.gT != h->arena + A::act0 + Bp2 * A::grows(l) || (L.f8b != 0) != A::f8b(l) ||
+        (L.f8b && (char*)L.Wb8 != h->arena + A::wb8(l)))
       return false;
     const bool relu = !(l == A::LFC || l == A::LDL || l == A::LCE);
     if (L.relu != (relu ? 1 : 0)) return false;
@@ -753,7 +760,7 @@ bool wide_dw_matches(const cvae_handle* h) {
     const LayerDev F = wchain::wide_layer<A>(l, h->arena, h->net.Bp);
     if (F.K != L.K || F.N != L.N || F.Kp != L.Kp || F.Np != L.Np || F.relu != L.relu || F.nseg != L.nseg ||
         F.seg_rows0 != L.seg_rows0 || F.f8 != L.f8 || F.wt != L.wt || F.has_bias != L.has_bias || F.Wf != L.Wf ||
-        F.Wb != L.Wb || F.bias != L.bias || F.xT != L.xT || F.gT != L.gT)
+        F.Wb != L.Wb || F.bias != L.bias || F.xT != L.xT || F.gT != L.gT || F.f8b != L.f8b || F.Wb8 != L.Wb8)
       return false;
     for (int g = 0; g < 2; ++g)
       if (F.pw[g] != L.pw[g] || F.pb[g] != L.pb[g]) return false;

@@ -34,9 +34,11 @@ struct LayerDev {
   int f8;                // CVAE_FP8: Wf holds OCP e4m3 fragments (pair-chunk order, f8_wf_off), see below
   int wt;                // master weight stored [K][N] (nn.Embedding layout: the class-embedding layer)
   int has_bias;          // 0: no bias parameter (the class-embedding layer); its padded bias stays 0
+  int f8b;               // CVAE_FP8: Wb8 holds e4m3(s·Wᵀ) K-pair fragments for an e4m3 dX GEMM (the wide chain)
   int64_t pw[2], pb[2];  // flat fp32 offsets of weight / bias of each segment
   void* Wf;              // [Np][Kp] T  (f8: [Np][Kp] e4m3, preceded by the F8Scale header)
   void* Wb;              // [Kp][Np] T
+  void* Wb8;             // f8b: [Kp][Np] e4m3, pair-chunk order (f8_wf_off over K = Np); the scale is Wf's
   float* bias;           // [Np] fp32
   void* xT;              // [Kp][Bp] T   input of the layer (feature-major)
   void* gT;              // [Np][Bp] T   gradient w.r.t. pre-activation

@@ -292,6 +292,15 @@ __device__ __forceinline__ void store_operands(const LayerDev& L, int o0, int i0
 #pragma unroll
       for (int e = 0; e < EPL; ++e) val[e] = to_t<T>(wt[(kl + frag_k<T>(q, e)) * LD + nl]);
       op_st<SYS>(L.Wb, ((size_t)(((i0 >> 4) + bt) * (L.Np / KC) + (o0 + kl) / KC) * 64 + ln) * EPL * sizeof(T), val);
+      if constexpr (EPL == 8 && !SYS) {
+        if (L.f8b) {  // the wide chain's e4m3 dX operand: e4m3(s·Wᵀ) in K-pair fragments (K = the outputs)
+          const float sc = f8_header(L.Wf)->s;
+          float f[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] = wt[(kl + frag_k<T>(q, e)) * LD + nl] * sc;
+          gst<long>((long*)((char*)L.Wb8 + f8_wf_off(i0 + bt * 16, (o0 + kl) / 32, L.Np) + (size_t)ln * 16), f8x8(f));
+        }
+      }
     } else if (EPL == 8 && L.f8) {  // CVAE_FP8: e4m3(s·W), 8 B per lane into its K-pair fragment
       const float sc = f8_header(L.Wf)->s;
       float f[8];

@@ -387,7 +387,7 @@ __device__ __forceinline__ void gemm(Ring<P>& ring, const void* img, f32x4 (&acc
   using PL = Plan<A>;
   constexpr StepInfo st = PL::step(S);
   constexpr bool F8 = st.F8;
-  static_assert(st.TS == TS && st.GRP == 0, "accumulator slots");
+  static_assert(st.TS == TS && st.GRP == 0 && st.F8 != 2, "accumulator slots");
   constexpr int G0 = PL::start(S);
   sfor<0, TS>([&](auto t) { acc[decltype(t)::value] = f32x4{0.f, 0.f, 0.f, 0.f}; });
   static_assert(!st.KS || (TS == 1 && !F8), "K split: chunks wave, wave + 8, .. of one n-tile");
@@ -475,6 +475,73 @@ __device__ __forceinline__ void gemm_grouped(Ring<P>& ring, const void* img, con
     });
     if constexpr (F8) sfor<0, GS>([&](auto i) { acc[decltype(i)::value] *= sc; });
     epi(pp, acc);
+  });
+}
+
+// The e4m3 dX GEMM of an f8b layer (StepInfo::F8 == 2; BASELINE cfg5's last decoder layer, decoder
+// L0 and fc): acc[slot] = G·W over the bf16 gradient image G, W streamed as e4m3(s·Wᵀ) K-pair
+// fragments (Wb8), every two K pairs in one block-scaled MFMA.  MX row-block scales: a lane's 32
+// values of the four 32-wide chunks of a K-pair pair are exactly the 32-element block the
+// instruction scales per lane (row r, its K positions), so each lane scales its own block —
+// k = 7 − floor(log2 max|G|) puts the block's largest value in [128, 256) (no saturation, no
+// cross-lane reduction, no step state) — and hands the instruction E8M0 2^−k for A and 1/s for B:
+// the accumulator is the unscaled product.  The gradient rows span ~10^4 in magnitude (the start /
+// time terms of dL/drecon beside the mean-squared ones), which one scale per tensor cannot hold.
+// oracle/cvae_np.py mx_dx restates it.
+__device__ __forceinline__ f32x4 mx2s(l2 x0, l2 x1, bf16x8 w0, bf16x8 w1, f32x4 acc, int sa, int sb) {
+  const l2 w0l = __builtin_bit_cast(l2, w0), w1l = __builtin_bit_cast(l2, w1);
+  typedef long l4 __attribute__((ext_vector_type(4)));
+  const i32x8 a = __builtin_bit_cast(i32x8, l4{x0[0], x0[1], x1[0], x1[1]});
+  const i32x8 b = __builtin_bit_cast(i32x8, l4{w0l[0], w0l[1], w1l[0], w1l[1]});
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, acc, 0, 0, 0, sa, 0, sb);
+}
+// one lane's block of 32 gradient values (4 chunks × 8, frag_k order) → e4m3 bytes of 2^k·g and
+// the block's E8M0 scale byte 127 − k (k = 0 for an all-zero block: padding rows)
+__device__ __forceinline__ int mx_block(const bf16x8 (&c)[4], l2& x0, l2& x1) {
+  float m = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf((float)c[i][e]));
+  const int k = m > 0.f ? min(134 - (int)((__float_as_uint(m) >> 23) & 0xff), 126) : 0;
+  const float sc = __builtin_bit_cast(float, (unsigned)(127 + k) << 23);  // 2^k (k <= 126)
+  long f[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (float)c[i][e] * sc;
+    f[i] = f8x8(v);
+  }
+  x0 = l2{f[0], f[1]};
+  x1 = l2{f[2], f[3]};
+  return 127 - k;
+}
+template <class A, int P, int S, int TS>
+__device__ __forceinline__ void gemm_mxb(Ring<P>& ring, const __bf16* img, f32x4 (&acc)[TS], const char* AR, int wave,
+                                         int lane, int sb) {
+  using PL = Plan<A>;
+  constexpr StepInfo st = PL::step(S);
+  static_assert(st.F8 == 2 && st.TS == TS && st.GRP == 0 && !st.KS, "an MX dX step");
+  constexpr int G0 = PL::start(S), KP = st.KC;  // K pairs (two 32-wide chunks each)
+  sfor<0, TS>([&](auto t) { acc[decltype(t)::value] = f32x4{0.f, 0.f, 0.f, 0.f}; });
+  sfor<0, (KP + 1) / 2>([&](auto gg) {
+    constexpr int g = decltype(gg)::value, p0 = 2 * g, p1 = 2 * g + 1;
+    constexpr bool two = p1 < KP;  // an odd last pair: the second half of the block is zero
+    bf16x8 c[4];
+    c[0] = xfrag(img, 2 * p0);
+    c[1] = xfrag(img, 2 * p0 + 1);
+    c[2] = two ? xfrag(img, 2 * p1) : bf16x8{};
+    c[3] = two ? xfrag(img, 2 * p1 + 1) : bf16x8{};
+    l2 x0, x1;
+    const int sa = mx_block(c, x0, x1);
+    sfor<0, TS>([&](auto t) {
+      constexpr int u = decltype(t)::value, ga = G0 + p0 * TS + u, gb = G0 + (two ? p1 : p0) * TS + u;
+      acc[u] = mx2s(x0, x1, ring.r[ga % P], ring.r[gb % P], acc[u], sa, sb);
+      asm volatile("" : "+v"(acc[u]));  // MFMA before the refills (as gemm)
+      ring_load<A, P, ga + P>(ring, AR, wave, lane);
+      if constexpr (two) ring_load<A, P, gb + P>(ring, AR, wave, lane);
+    });
   });
 }
 
@@ -643,6 +710,16 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   const uint64_t rng_off = a.ctr ? *(const __attribute__((address_space(4))) uint64_t*)a.ctr : a.offset;
 
   Ring<P> ring;
+  // a dX GEMM of step S over the bf16 gradient image: e4m3 with MX scales where the layer is f8b
+  auto dgemm = [&](auto sI, const __bf16* gimg, auto& acc) {
+    constexpr int S_ = decltype(sI)::value;
+    constexpr StepInfo st = PL::step(S_);
+    constexpr int TS_ = st.TS;
+    if constexpr (st.F8 == 2)  // B's E8M0 scale: the exponent byte of 1/s (a power of two)
+      gemm_mxb<A, P, S_, TS_>(ring, gimg, acc, AR, wave, lane, (int)((__float_as_uint(INVS[st.layer]) >> 23) & 0xff));
+    else
+      gemm<A, P, S_, TS_>(ring, gimg, acc, AR, wave, lane);
+  };
   constexpr int PF0 = kPreFill < P ? kPreFill : P;  // ring items issued before the x-tile wait
   float s_recon = 0.f, s_kl = 0.f, s_start = 0.f, s_t0 = 0.f, s_relu = 0.f;
 
@@ -1091,7 +1168,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   static_assert(XR <= ND - 1, "the dL/drecon copy runs over the decoder backward steps");
   {  // last decoder layer ᵀ: dL/d h_D(ND-2) = GL · W_DL, ReLU mask of D(ND-2) → A0
     f32x4 acc[1];
-    gemm<A, P, PL::sDLb>(ring, XIN, acc, AR, wave, lane);
+    dgemm(integral_constant<int, PL::sDLb>{}, XIN, acc);
     img_copy<Ip, 0, 1>(XIN, dst, GT(A::LDL), A::Np(A::LDL), 0, b0);
     img(A0, n, masked(acc[0], integral_constant<int, A::MD(ND - 2)>{}));
   }
@@ -1142,7 +1219,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     if (tid < (A::Np(A::LFC) - 2 * Z) * 4) *(uint64_t*)(GFC + (2 * Z + tid / 4) * 16 + 4 * (tid & 3)) = 0ull;
   } else {
     f32x4 acc[NZT + 1];
-    gemm<A, P, PL::sD0b>(ring, D0IN, acc, AR, wave, lane);
+    dgemm(integral_constant<int, PL::sD0b>{}, D0IN, acc);
     img_copy<H, 0, 1>(D0IN, dst, GT(A::LD0), H, 0, b0);
 #pragma unroll
     for (int k = 0; k < NZT; ++k) {
@@ -1165,7 +1242,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     // CLS: tiles 16, 17 (waves 0, 1, slot 2) are de = fc share + decoder share (no activation) → gT(LCE)
     constexpr int TS = PL::step(PL::sFCb).TS;
     f32x4 acc[TS];
-    gemm<A, P, PL::sFCb>(ring, GFC, acc, AR, wave, lane);
+    dgemm(integral_constant<int, PL::sFCb>{}, GFC, acc);
     sub();
     img_copy<A::Np(A::LFC), 0, (2 * A::Np(A::LFC) + NT - 1) / NT>(GFC, dst, GT(A::LFC), A::Np(A::LFC), 0, b0);
     if constexpr (A::SZ) dhc2 = *(const f32x4*)(DHC2 + n * R + 4 * q);

@@ -93,6 +93,7 @@ __host__ __device__ inline LayerDev wide_layer(int l, char* arena, int Bp) {
   L.Np = (int)P([](int k) { return (int64_t)A::Np(k); });
   L.relu = (l == A::LFC || l == A::LDL) ? 0 : 1;
   L.f8 = (int)P([](int k) { return (int64_t)A::f8(k); });
+  L.f8b = (int)P([](int k) { return (int64_t)A::f8b(k); });
   L.wt = 0;
   L.has_bias = 1;
   const int64_t off = P([](int k) { return wpoff<A>(k); });
@@ -107,6 +108,7 @@ __host__ __device__ inline LayerDev wide_layer(int l, char* arena, int Bp) {
   const int64_t Bp2 = 2 * (int64_t)Bp;
   L.Wf = arena + P([](int k) { return A::wf(k); });
   L.Wb = arena + P([](int k) { return A::wb(k); });
+  L.Wb8 = L.f8b ? arena + P([](int k) { return A::f8b(k) ? A::wb8(k) : (int64_t)0; }) : nullptr;
   L.bias = (float*)(arena + A::bias_base) + P([](int k) { return (int64_t)A::bias_off(k); });
   L.xT = arena + A::act0 + Bp2 * P([](int k) { return A::xrows(k); });
   L.gT = arena + A::act0 + Bp2 * P([](int k) { return A::grows(k); });

@@ -95,6 +95,47 @@ def fp8_layers(p, seq_len, dim, latent_dim, hidden_dim=128, n_enc=4, n_dec=4):
     return out
 
 
+def fp8b_layers(p, seq_len, dim, latent_dim, hidden_dim=128, n_enc=4, n_dec=4):
+    """{layer name: scale} of the layers whose dX GEMM the CVAE_FP8 wide chain runs in e4m3 with MX
+    row-block scales (cvae_capi.hip build_plan LayerDev::f8b, cvae_widechain.h Arch::f8b): an e4m3
+    forward operand (padded K % 64 == 0), the backward K (the padded outputs) a multiple of 64, a dX
+    at all (not condition_encoder.0 / encoder.1) and a padded extent of >= 512 on either side — at
+    BASELINE cfg5 the last decoder layer, decoder.0 and fc.  Only the wide chain runs them (the
+    generic interpreter's fp8 backward stays bf16)."""
+    I, H, Z = seq_len * dim, hidden_dim, latent_dim
+    r32 = lambda v: (v + 31) // 32 * 32  # noqa: E731
+    f8 = fp8_layers(p, seq_len, dim, latent_dim, hidden_dim, n_enc, n_dec)
+    shapes = {"condition_encoder.2": (H, H), "fc_mu": (2 * H, 2 * Z), "fc_logvar": (2 * H, 2 * Z)}
+    for i in range(1, n_enc):
+        shapes[f"encoder.{2 * i + 1}"] = (H, H)
+    for i in range(n_dec):
+        shapes[f"decoder.{2 * i}"] = (Z + H if i == 0 else H, I if i == n_dec - 1 else H)
+    return {n: f8[n] for n, (k, o) in shapes.items()
+            if n in f8 and r32(o) % 64 == 0 and (r32(o) >= 512 or r32(k) >= 512)}
+
+
+def mx_dx(G, W, s):
+    """dX = G·W of an f8b layer as the wide chain computes it (cvae_widechain.h gemm_mxb): G (B, N)
+    the bf16 gradient rows, W (N, K) the layer's weight, s its e4m3 weight scale.  Backward K index
+    k (a padded output of the layer) of row b belongs to the MX block (k // 128, (k % 16) // 4) — the
+    32 values one lane of the block-scaled MFMA holds; each block is scaled by 2^kb with
+    kb = 7 − floor(log2 max|block|) (0 for an all-zero block, at most 126), rounded to e4m3, and
+    unscaled in the product; W enters as e4m3(s·W)/s."""
+    G = np.asarray(G, np.float32)
+    B, N = G.shape
+    Np = (N + 127) // 128 * 128
+    Gp = np.zeros((B, Np), np.float32)
+    Gp[:, :N] = G
+    g6 = Gp.reshape(B, Np // 128, 4, 2, 4, 4)  # (row, 128-group, chunk, half, lane quad, element)
+    amax = np.abs(g6).max(axis=(2, 3, 5), keepdims=True)
+    e = np.frexp(amax)[1]
+    kb = np.where(amax > 0, np.minimum(8 - e, 126), 0).astype(np.float64)
+    sc = np.exp2(kb).astype(np.float32)
+    x8 = (e4m3(g6 * sc) / sc).reshape(B, Np)[:, :N]
+    w8 = e4m3(np.asarray(W, np.float32) * s) / s
+    return (x8.astype(np.float64) @ w8.astype(np.float64)).astype(np.float32)
+
+
 def forward(p, x, eps, n_enc=4, n_dec=4, dt=np.float32, q=None, f8=None):
     """x: (B,S,D) absolute trajectories.  Returns (recon, mu, logvar, h_c, cache).
 
@@ -161,13 +202,16 @@ def dloss_drecon(r, x_rel, w=(0.1, 0.1, 1.0, 1.0), B_norm=None):
     return g
 
 
-def backward(p, c, r, mu, lv, w=(0.1, 0.1, 1.0, 1.0), n_enc=4, n_dec=4, dt=np.float32):
+def backward(p, c, r, mu, lv, w=(0.1, 0.1, 1.0, 1.0), n_enc=4, n_dec=4, dt=np.float32, f8b=None):
     """Gradients of the total loss w.r.t. every parameter (dict keyed like state_dict).
 
     With the cache of ``forward(..., q=bf16)`` every stored gradient G and every GEMM operand
     is rounded as the bf16 kernels round them (dz, the decoder's dh_c share, accumulations and
-    the loss stay fp32).
+    the loss stay fp32).  f8b: {layer name: weight scale} (``fp8b_layers``) — those layers' dX
+    GEMMs run in e4m3 with MX row-block scales (``mx_dx``; the wide chain's CVAE_FP8 form); their
+    dW stays bf16.
     """
+    f8b = f8b or {}
     q = c.get("q", _ident)
     p = {k: v.astype(dt) for k, v in p.items()}
     B, S, D = r.shape
@@ -178,6 +222,8 @@ def backward(p, c, r, mu, lv, w=(0.1, 0.1, 1.0, 1.0), n_enc=4, n_dec=4, dt=np.fl
         G, X = q(G), q(X)
         g[name + ".weight"] = G.T @ X
         g[name + ".bias"] = G.sum(0)
+        if name in f8b:
+            return mx_dx(G, p[name + ".weight"], f8b[name])
         return G @ q(p[name + ".weight"])
 
     G = dloss_drecon(r, c["rel"], w).reshape(B, S * D)

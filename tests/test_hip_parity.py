@@ -972,7 +972,10 @@ def test_fp8_matches_fp8_emulation(cvae, shape):
     loss = eng.forward_backward(x, eps=eps).cpu().numpy()
     want = cvae_np.losses(r, cc["rel"], mu, lv)
     np.testing.assert_allclose(loss, want, rtol=5e-3, atol=1e-6)
-    gw = cvae_np.backward(p, cc, r, mu, lv, n_enc=ne, n_dec=nd)
+    # the cfg5 shape runs the wide chain: its large dX GEMMs are e4m3 with MX row-block scales
+    f8b = cvae_np.fp8b_layers(p, c["S"], c["D"], c["Z"], 128, ne, nd) if eng.train_kernel == "wide" else None
+    assert (shape == "cfg5") == bool(f8b)
+    gw = cvae_np.backward(p, cc, r, mu, lv, n_enc=ne, n_dec=nd, f8b=f8b)
     g = _grads(m, eng)
     errs = {k: rel_l2(g[k], gw[k]) for k in cvae_np.param_keys(ne, nd)}
     print(f"fp8 {shape}: grad rel-L2 vs emulation", {k: round(v, 4) for k, v in errs.items()})
@@ -986,10 +989,12 @@ def test_fp8_matches_fp8_emulation(cvae, shape):
 @pytest.mark.parametrize("B", [37, 200])
 def test_wide_fp8_chain_matches_generic_fp8(cvae, monkeypatch, B):
     """The cfg5 fp8 form of the wide chain (e4m3 activation twins written by the producing
-    epilogues, e4m3 weight pairs in the ring) against the generic interpreter's fp8 path
-    (CVAE_GENERIC=1) — the same rounding points, fp32 summation order aside — and against the CPU
-    emulation (emulation tolerances of test_fp8_matches_fp8_emulation); ragged tile (B=37) and a
-    gathered batch (B=200)."""
+    epilogues, e4m3 weight pairs in the ring; the dX GEMMs of the last decoder layer, decoder L0 and
+    fc in e4m3 with MX row-block scales) against the generic interpreter's fp8 path (CVAE_GENERIC=1:
+    the same forward rounding points, a bf16 backward) — losses tight, gradients within the e4m3
+    backward's rounding (printed) — and against the CPU emulation of exactly its rounding points
+    (cvae_np fp8 forward + mx_dx; emulation tolerances of test_fp8_matches_fp8_emulation); ragged
+    tile (B=37) and a gathered batch (B=200)."""
     ref, m, eng, x, eps = _wide(cvae, "fp8", B)
     monkeypatch.setenv("CVAE_GENERIC", "1")
     m2 = cvae.ConditionalTrajectoryVAE(WIDE["S"], WIDE["D"], WIDE["Z"], 128, WIDE["n_enc"], WIDE["n_dec"])
@@ -1009,16 +1014,23 @@ def test_wide_fp8_chain_matches_generic_fp8(cvae, monkeypatch, B):
     np.testing.assert_allclose(lw, lg, rtol=5e-3, atol=1e-6)
     gw, gg = _grads(m, eng), _grads(m2, e2)
     errs = {k: rel_l2(gw[k], gg[k]) for k in gw}
-    assert max(errs.values()) < 1e-1 and np.median(list(errs.values())) < 2e-2, errs
+    print(f"wide fp8 chain B={B}: grad rel-L2 vs the generic bf16 backward", {k: round(v, 4) for k, v in errs.items()})
+    assert max(errs.values()) < 0.2 and np.median(list(errs.values())) < 0.1, errs
     p = {k: v.numpy() for k, v in ref.state_dict().items()}
     ne, nd = WIDE["n_enc"], WIDE["n_dec"]
     f8 = cvae_np.fp8_layers(p, WIDE["S"], WIDE["D"], WIDE["Z"], 128, ne, nd)
+    f8b = cvae_np.fp8b_layers(p, WIDE["S"], WIDE["D"], WIDE["Z"], 128, ne, nd)
+    assert sorted(f8b) == ["decoder.0", f"decoder.{2 * (nd - 1)}", "fc_logvar", "fc_mu"], sorted(f8b)
     r, mu, lv, hc, cc = cvae_np.forward(p, x.numpy(), eps.numpy(), n_enc=ne, n_dec=nd, q=cvae_np.bf16, f8=f8)
     np.testing.assert_allclose(lw, cvae_np.losses(r, cc["rel"], mu, lv), rtol=5e-3, atol=1e-6)
-    ge = cvae_np.backward(p, cc, r, mu, lv, n_enc=ne, n_dec=nd)
+    ge = cvae_np.backward(p, cc, r, mu, lv, n_enc=ne, n_dec=nd, f8b=f8b)
     errs = {k: rel_l2(gw[k], ge[k]) for k in cvae_np.param_keys(ne, nd)}
     print(f"wide fp8 chain B={B}: grad rel-L2 vs emulation", {k: round(v, 4) for k, v in errs.items()})
     assert max(errs.values()) < 1e-1 and np.median(list(errs.values())) < 2e-2, errs
+    gb = cvae_np.backward(p, cc, r, mu, lv, n_enc=ne, n_dec=nd)  # the same forward, a bf16 backward
+    dev = {k: rel_l2(ge[k], gb[k]) for k in cvae_np.param_keys(ne, nd)}
+    print(f"  emulation: MX e4m3 dX vs bf16 dX, grad rel-L2 median {np.median(list(dev.values())):.4f} "
+          f"max {max(dev.values()):.4f}")
 
 
 def test_fp8_training_full_batch_cfg5(cvae):
