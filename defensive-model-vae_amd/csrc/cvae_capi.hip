@@ -104,6 +104,7 @@ struct cvae_handle {
   int lds_bytes = 0;
   int fast_nki = 0;         // > 0: bf16 training runs fchain::fastchain_kernel<fast_nki>
   int fast_lds = 0;
+  bool fast_buckets = false;  // the two dW buckets run fchain::fastwgrad_bucket_kernel
   bool wide = false;        // bf16 training at BASELINE cfg5's shape runs wchain::widechain_kernel<Cfg5>
   bool wide_dw = false;     // ... and its dW ⊕ Adam runs wchain::widewgrad_kernel (compile-time tile decode)
   int wide_lds = 0;
@@ -650,10 +651,26 @@ bool fast_layout_matches(const cvae_handle* h) {
   return true;
 }
 
+// the bucket kernel's tiles (fastwgrad_bucket_kernel) are the handle's bucket lists, in order
+template <int NKI>
+bool fast_buckets_match(const cvae_handle* h) {
+  using T = fchain::Tiles<NKI>;
+  for (int k = 0; k < 2; ++k) {
+    const int n = T::bucket_count(k);
+    if ((int)h->tiles_part[k].size() != n) return false;
+    for (int b = 0; b < n; ++b) {
+      const TileDesc a = T::decode(T::bucket_first(k) + T::slot(b, n)), &t = h->tiles_part[k][b];
+      if (a.layer != t.layer || a.o0 != t.o0 || a.i0 != t.i0) return false;
+    }
+  }
+  return true;
+}
+
 int plan_fast(cvae_handle* h) {
   const cvae_config& c = h->cfg;
   const NetDev& n = h->net;
   h->fast_nki = 0;
+  h->fast_buckets = false;
   const char* env = std::getenv("CVAE_GENERIC");
   if ((env && env[0] == '1') || c.dtype != CVAE_BF16 || c.n_classes > 0 || c.hidden_dim != fchain::H ||
       c.latent_dim != fchain::Z ||
@@ -666,6 +683,8 @@ int plan_fast(cvae_handle* h) {
     if (nki == 19 && !fast_layout_matches<19>(h)) return CVAE_OK;
     h->fast_nki = nki;
     h->fast_lds = lp.total;
+    const char* gb = std::getenv("CVAE_GENERIC_BUCKETS");  // "1": the buckets on the generic kernel (A/B)
+    h->fast_buckets = nki == 19 && fast_buckets_match<19>(h) && !(gb && gb[0] == '1');
     if (nki == 19) {
       HIPCK(hipFuncSetAttribute((const void*)fchain::fastchain_kernel<19>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lp.total));
@@ -933,6 +952,12 @@ int launch_wgrad(cvae_handle* h, int batch, const AdamArgs& aa, const LossArgs& 
   SplitK sk{splits_of(h, batch), 0, h->splitk_ws, h->splitk_tickets, 0};
   if (dw != (CVAE_PART_DW_DEC | CVAE_PART_DW_REST)) {
     const int k = dw == CVAE_PART_DW_DEC ? 0 : 1;
+    if (h->fast_buckets) {
+      using T = fchain::Tiles<19>;
+      return klaunch(h, fchain::fastwgrad_bucket_kernel<19, MODE>, dim3(T::bucket_count(k) * sk.S + 1),
+                     dim3(WG_THREADS), 0, s, h->arena, aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), h->net.S,
+                     h->net.D, h->net.I, aa, la, sk, T::bucket_first(k), T::bucket_count(k));
+    }
     const int nt = (int)h->tiles_part[k].size();
     if (is16(h))
       return klaunch(h, wgrad_kernel<__bf16, MODE>, dim3(nt * sk.S), dim3(WG_THREADS), 0, s, h->net,
@@ -1244,6 +1269,9 @@ int cvae_adam(cvae_handle* h, float* params, const float* grads, float* m, float
   AdamArgs aa = make_adam(params, (float*)grads, m, v, step, *adam, grad_scale, counters);
   const int nt = (int)h->tiles.size();
   if ((rc = tmark(h, s, "adam"))) return rc;
+  if (h->fast_nki == 19)
+    return klaunch(h, fchain::fastadam_kernel<19>, dim3(fchain::Tiles<19>::total()), dim3(CVAE_THREADS), 0, s,
+                   h->arena, params, m, v, grads, h->net.Bp, h->net.I, aa);
   if (is16(h))
     return klaunch(h, param_kernel<__bf16, PM_ADAM>, dim3(nt), dim3(CVAE_THREADS), 0, s, h->net,
                    (const TileDesc*)h->d_tiles, aa);

@@ -62,11 +62,19 @@ struct Tiles {
     return true;
   }
   static_assert(pow2_inner(), "tile decode assumes power-of-two inner tile counts");
+  // list position of workgroup b in a launch over n consecutive list entries (xcd_order: the n
+  // cut into 8 contiguous chunks, chunk x at blockIdx 8j + x)
+  __host__ __device__ static int slot(int b, int n) {
+    const int q = n >> 3, r = n & 7, x = b & 7, j = b >> 3;
+    return x * q + (x < r ? x : r) + j;
+  }
   // tile of workgroup b (host: the reference decode plan_fast compares with the handle's list)
-  __host__ __device__ static TileDesc at(int b) {
-    constexpr int NTL = total(), q = NTL / 8, r = NTL % 8;
-    const int x = b & 7, j = b >> 3;
-    const int s = x * q + (x < r ? x : r) + j;
+  __host__ __device__ static TileDesc at(int b) { return decode(slot(b, total())); }
+  // the two dW buckets (CVAE_PART_DW_DEC / _REST): the decoder layers are the list's tail
+  __host__ __device__ static constexpr int bucket_first(int k) { return k == 0 ? start(LD0) : 0; }
+  __host__ __device__ static constexpr int bucket_count(int k) { return k == 0 ? total() - start(LD0) : start(LD0); }
+  // tile at list position s
+  __host__ __device__ static TileDesc decode(int s) {
 #ifdef __HIP_DEVICE_COMPILE__
     int l = 0;
 #pragma unroll
@@ -167,6 +175,53 @@ __global__ __launch_bounds__(WG_THREADS) void fastwgrad_kernel(char* arena, floa
     wgrad_body<__bf16, MODE, false, 2>(L, td, Bk, aa, la, false, fn.S, fn.D, Z, sh.red, sh.dbp, sk);
   else
     wgrad_body<__bf16, MODE, false, 1>(L, td, Bk, aa, la, false, fn.S, fn.D, Z, sh.red, sh.dbp, sk);
+}
+
+// One dW bucket of the data-parallel two-bucket step (dist.py buckets=2): the tiles of list
+// positions [first, first + n) — Tiles::bucket_first/count — in the same XCD placement the generic
+// kernel's bucket lists (build_plan tiles_part) have.  grid = n × sk.S + 1; the last block
+// finishes the loss when the call carries it (the decoder bucket, launched with the chain).
+// Split-K tickets and partials are indexed by the list position, so the two buckets never share one.
+template <int NKI, int MODE>
+__global__ __launch_bounds__(WG_THREADS) void fastwgrad_bucket_kernel(char* arena, float* params, float* mst,
+                                                                       float* vst, int Bp, int Bk, int S, int D, int I,
+                                                                       AdamArgs a, LossArgs la, SplitK sk, int first,
+                                                                       int n) {
+  const FastNet fn{arena, Bp, S, D, I};
+  AdamArgs aa = a;
+  aa.params = params;
+  aa.m = mst;
+  aa.v = vst;
+  if ((int)blockIdx.x == n * sk.S) {
+    if (threadIdx.x < 64 && la.partials) finish_loss(la, fn.S, fn.D, Z);
+    return;
+  }
+  static_assert(Tiles<NKI>::ni_max() == 1, "bucket tiles are 32 x 32");
+  __shared__ __attribute__((aligned(16))) WgradLds<1> sh;
+  sk.s = blockIdx.x / n;
+  sk.tile = first + Tiles<NKI>::slot((int)blockIdx.x - sk.s * n, n);
+  const TileDesc td = Tiles<NKI>::decode(sk.tile);
+  const LayerDev L = fast_layer<NKI>(td.layer, fn.arena, fn.Bp, fn.I);
+  wgrad_body<__bf16, MODE, false, 1>(L, td, Bk, aa, la, false, fn.S, fn.D, Z, sh.red, sh.dbp, sk);
+}
+
+// Adam from the all-reduced gradient buffer (the RCCL data-parallel step's last launch,
+// cvae_adam): param_kernel's body over fastwgrad's tiles, the tile and layer record decoded from
+// blockIdx instead of read from the tile list and the NetDev kernel argument (two dependent round
+// trips before the first state load).  grid = Tiles::total(), CVAE_THREADS threads.
+template <int NKI>
+__global__ __launch_bounds__(CVAE_THREADS) void fastadam_kernel(char* arena, float* params, float* mst, float* vst,
+                                                                const float* grads, int Bp, int I, AdamArgs a) {
+  __shared__ __attribute__((aligned(16))) float wt[32 * WT_LD];
+  AdamArgs aa = a;
+  aa.params = params;
+  aa.m = mst;
+  aa.v = vst;
+  aa.grads = const_cast<float*>(grads);
+  TileDesc td;
+  LayerDev L;
+  decode_tile<NKI>(blockIdx.x, arena, Bp, I, td, L);
+  param_body<__bf16, PM_ADAM>(L, td, aa, wt);
 }
 
 // ---------------------------------------------------------------- data parallel: the peer exchange

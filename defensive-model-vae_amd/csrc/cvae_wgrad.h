@@ -681,7 +681,7 @@ __global__ __launch_bounds__(WG_THREADS, 4) void wgrad_kernel(NetDev net, const 
 template <typename T, int MODE>
 __device__ __forceinline__ void param_body(const LayerDev& L, const TileDesc& td, AdamArgs aa, float* wt) {
   const int tid = threadIdx.x;
-  if (MODE == PM_ADAM) adam_resolve(aa, adam_step_load(aa));
+  const adam_f32x2 t_step = MODE == PM_ADAM ? adam_step_load(aa) : adam_f32x2{0.f, 0.f};  // first: in-order vmcnt
   const PreN<4> st = loadn<MODE, 4>(L, td.o0 + (tid >> 3), td.i0 + (tid & 7) * 4, aa);
   PreB sb = {0.f, 0.f, 0.f, -1};
   if (td.i0 == 0 && tid < 32) sb = loadb<MODE>(L, td.o0 + tid, aa);
@@ -695,6 +695,7 @@ __device__ __forceinline__ void param_body(const LayerDev& L, const TileDesc& td
       const int seg = (L.nseg == 2 && ob >= L.seg_rows0) ? 1 : 0;
       db = aa.grads[L.pb[seg] + (seg ? ob - L.seg_rows0 : ob)] * aa.grad_scale;
     }
+    adam_resolve(aa, t_step);  // its first use: after every state load has been issued
   }
   tile_epilogue<T, MODE, CVAE_THREADS, 4>(L, td.o0, td.i0, st, sb, g4, db, aa, wt);
 }
