@@ -480,14 +480,18 @@ __device__ __forceinline__ void gemm_grouped(Ring<P>& ring, const void* img, con
 
 // The e4m3 dX GEMM of an f8b layer (StepInfo::F8 == 2; BASELINE cfg5's last decoder layer, decoder
 // L0 and fc): acc[slot] = G·W over the bf16 gradient image G, W streamed as e4m3(s·Wᵀ) K-pair
-// fragments (Wb8), every two K pairs in one block-scaled MFMA.  MX row-block scales: a lane's 32
-// values of the four 32-wide chunks of a K-pair pair are exactly the 32-element block the
-// instruction scales per lane (row r, its K positions), so each lane scales its own block —
-// k = 7 − floor(log2 max|G|) puts the block's largest value in [128, 256) (no saturation, no
-// cross-lane reduction, no step state) — and hands the instruction E8M0 2^−k for A and 1/s for B:
-// the accumulator is the unscaled product.  The gradient rows span ~10^4 in magnitude (the start /
+// fragments (Wb8), every two K pairs in one block-scaled MFMA.  MX blocks of the instruction
+// (mapped on the GPU by scripts/ubench/mxscale.hip): lane r + 16j holds byte quarters h = 0..3 of
+// row r; block b = 2·(h >> 1) + (j >> 1) — the 16-B half h >> 1 of the lane pair j >> 1 — and its
+// E8M0 byte comes from lane r + 16b.  Quarter h of a lane here is its 8 values of gradient chunk
+// 4g + h, so a block is 16 positions of each of two adjacent chunks of one row (oracle mx_dx).
+// Each lane takes the two exponents of its halves' maxima, one exchange with its pair partner
+// (lane ^ 16) makes them the block maxima, k = 134 − biased exponent = 7 − floor(log2 max|G|) puts
+// a block's largest value in [128, 256) (no saturation, no step state), each half converts with
+// its block's 2^k, and one more exchange fetches the exponent of block j for the scale operand
+// (held by the lane's own pair for j ∈ {0, 3}, by lane ^ 48 for j ∈ {1, 2}); B takes 1/s: the
+// accumulator is the unscaled product.  The gradient rows span ~10^4 in magnitude (the start /
 // time terms of dL/drecon beside the mean-squared ones), which one scale per tensor cannot hold.
-// oracle/cvae_np.py mx_dx restates it.
 __device__ __forceinline__ f32x4 mx2s(l2 x0, l2 x1, bf16x8 w0, bf16x8 w1, f32x4 acc, int sa, int sb) {
   const l2 w0l = __builtin_bit_cast(l2, w0), w1l = __builtin_bit_cast(l2, w1);
   typedef long l4 __attribute__((ext_vector_type(4)));
@@ -495,27 +499,40 @@ __device__ __forceinline__ f32x4 mx2s(l2 x0, l2 x1, bf16x8 w0, bf16x8 w1, f32x4 
   const i32x8 b = __builtin_bit_cast(i32x8, l4{w0l[0], w0l[1], w1l[0], w1l[1]});
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, acc, 0, 0, 0, sa, 0, sb);
 }
-// one lane's block of 32 gradient values (4 chunks × 8, frag_k order) → e4m3 bytes of 2^k·g and
-// the block's E8M0 scale byte 127 − k (k = 0 for an all-zero block: padding rows)
-__device__ __forceinline__ int mx_block(const bf16x8 (&c)[4], l2& x0, l2& x1) {
-  float m = 0.f;
+// the lane's 8 values of four gradient chunks (frag_k order) → e4m3 bytes of 2^k·g (k of the
+// quarter's block), and the E8M0 byte 127 − k of block lane / 16 for the scale operand; k = 0 for an
+// all-zero block (padding rows)
+__device__ __forceinline__ int mx_block(const bf16x8 (&c)[4], l2& x0, l2& x1, int lane) {
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  unsigned eb[2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int hh = 0; hh < 2; ++hh) {
+    float m = 0.f;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf((float)c[i][e]));
-  const int k = m > 0.f ? min(134 - (int)((__float_as_uint(m) >> 23) & 0xff), 126) : 0;
-  const float sc = __builtin_bit_cast(float, (unsigned)(127 + k) << 23);  // 2^k (k <= 126)
+    for (int i = 2 * hh; i < 2 * hh + 2; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf((float)c[i][e]));
+    eb[hh] = (__float_as_uint(m) >> 23) & 0xff;  // biased exponent of the half's max (0: zero)
+  }
+  u16x2 p{(unsigned short)eb[0], (unsigned short)eb[1]};
+  p = __builtin_elementwise_max(p, __builtin_bit_cast(u16x2, __shfl_xor((int)__builtin_bit_cast(unsigned, p), 16)));
   long f[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
+    const int e = p[i >> 1];
+    const int k = e > 0 ? min(134 - e, 126) : 0;
+    const float sc = __builtin_bit_cast(float, (unsigned)(127 + k) << 23);  // 2^k (k <= 126)
     float v[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = (float)c[i][e] * sc;
+    for (int t = 0; t < 8; ++t) v[t] = (float)c[i][t] * sc;
     f[i] = f8x8(v);
   }
   x0 = l2{f[0], f[1]};
   x1 = l2{f[2], f[3]};
-  return 127 - k;
+  const int j = lane >> 4;
+  const u16x2 q = __builtin_bit_cast(u16x2, __shfl((int)__builtin_bit_cast(unsigned, p), (j == 1 || j == 2) ? lane ^ 48 : lane));
+  const int e = (j >> 1) ? q[1] : q[0];
+  return 127 - (e > 0 ? min(134 - e, 126) : 0);
 }
 template <class A, int P, int S, int TS>
 __device__ __forceinline__ void gemm_mxb(Ring<P>& ring, const __bf16* img, f32x4 (&acc)[TS], const char* AR, int wave,
@@ -534,7 +551,7 @@ __device__ __forceinline__ void gemm_mxb(Ring<P>& ring, const __bf16* img, f32x4
     c[2] = two ? xfrag(img, 2 * p1) : bf16x8{};
     c[3] = two ? xfrag(img, 2 * p1 + 1) : bf16x8{};
     l2 x0, x1;
-    const int sa = mx_block(c, x0, x1);
+    const int sa = mx_block(c, x0, x1, lane);
     sfor<0, TS>([&](auto t) {
       constexpr int u = decltype(t)::value, ga = G0 + p0 * TS + u, gb = G0 + (two ? p1 : p0) * TS + u;
       acc[u] = mx2s(x0, x1, ring.r[ga % P], ring.r[gb % P], acc[u], sa, sb);

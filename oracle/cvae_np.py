@@ -115,23 +115,25 @@ def fp8b_layers(p, seq_len, dim, latent_dim, hidden_dim=128, n_enc=4, n_dec=4):
 
 
 def mx_dx(G, W, s):
-    """dX = G·W of an f8b layer as the wide chain computes it (cvae_widechain.h gemm_mxb): G (B, N)
-    the bf16 gradient rows, W (N, K) the layer's weight, s its e4m3 weight scale.  Backward K index
-    k (a padded output of the layer) of row b belongs to the MX block (k // 128, (k % 16) // 4) — the
-    32 values one lane of the block-scaled MFMA holds; each block is scaled by 2^kb with
-    kb = 7 − floor(log2 max|block|) (0 for an all-zero block, at most 126), rounded to e4m3, and
-    unscaled in the product; W enters as e4m3(s·W)/s."""
+    """dX = G·W of an f8b layer as the wide chain computes it (cvae_widechain.h gemm_mxb / mx_block):
+    G (B, N) the bf16 gradient rows, W (N, K) the layer's weight, s its e4m3 weight scale.  The
+    block-scaled MFMA's 32-value MX blocks (their lane / byte mapping measured on the GPU by
+    scripts/ubench/mxscale.hip), in the gradient's feature order: within each 128-feature group,
+    block (half, jj) = positions 16a + 8jj + i (a, i ranging) of the two chunks 2·half, 2·half + 1.
+    Each block is scaled by 2^kb, kb = 134 − (biased fp32 exponent of max|block|) =
+    7 − floor(log2 max|block|) (0 for an all-zero block, at most 126), rounded to e4m3 and unscaled in
+    the product; W enters as e4m3(s·W)/s."""
     G = np.asarray(G, np.float32)
     B, N = G.shape
     Np = (N + 127) // 128 * 128
     Gp = np.zeros((B, Np), np.float32)
     Gp[:, :N] = G
-    g6 = Gp.reshape(B, Np // 128, 4, 2, 4, 4)  # (row, 128-group, chunk, half, lane quad, element)
-    amax = np.abs(g6).max(axis=(2, 3, 5), keepdims=True)
-    e = np.frexp(amax)[1]
-    kb = np.where(amax > 0, np.minimum(8 - e, 126), 0).astype(np.float64)
+    g7 = Gp.reshape(B, Np // 128, 2, 2, 2, 2, 8)  # (row, group, half, chunk, a, jj, i)
+    amax = np.abs(g7).max(axis=(3, 4, 6), keepdims=True)
+    eb = ((amax.view(np.uint32) >> 23) & 0xFF).astype(np.int64)
+    kb = np.where(eb > 0, np.minimum(134 - eb, 126), 0).astype(np.float64)
     sc = np.exp2(kb).astype(np.float32)
-    x8 = (e4m3(g6 * sc) / sc).reshape(B, Np)[:, :N]
+    x8 = (e4m3(g7 * sc) / sc).reshape(B, Np)[:, :N]
     w8 = e4m3(np.asarray(W, np.float32) * s) / s
     return (x8.astype(np.float64) @ w8.astype(np.float64)).astype(np.float32)
 

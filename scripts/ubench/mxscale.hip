@@ -2,9 +2,10 @@
 // A is zero except one 8-byte quarter h of one lane La (e4m3 1.0), B is all 1.0; the output row
 // La % 16 then reads 8.  For every lane Ls the A scale of Ls alone is set to 2^1 (every byte 128,
 // all others 127): the output doubles iff that scale multiplies quarter (La, h).  Prints, for each
-// (La, h), the lanes whose scale multiplies it — the mapping cvae_widechain.h gemm_mxb relies on
-// is "lane La's own scale, every quarter".  Then the same for B (B zero except (Lb, h), A all 1.0),
-// and which byte of the scale VGPR opsel 0 reads.
+// (La, h), the lanes whose scale multiplies it.  Then the same for B (B zero except (Lb, h), A all
+// 1.0), and which byte of the scale VGPR opsel 0 reads.  Measured (gfx950): quarter h of lane
+// r + 16j is scaled by lane r + 16·(2·(h >> 1) + (j >> 1)) for A and B alike — the mapping
+// cvae_widechain.h mx_block relies on; exit status 1 if it differs.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstring>
@@ -65,7 +66,7 @@ int main() {
           run();
           if (total() > 1.5 * base) {
             printf("%s%d", hits ? "," : "", Ls);
-            if (Ls != L) ++bad;
+            if (Ls != L % 16 + 16 * (2 * (h >> 1) + ((L / 16) >> 1))) ++bad;
             ++hits;
           }
         }
@@ -86,6 +87,6 @@ int main() {
     run();
     printf("opsel 0, A scale byte %d of lane 0 = 128: total %s\n", k, total() > base ? "changes" : "unchanged");
   }
-  printf(bad ? "MAPPING DIFFERS from 'own lane' (%d)\n" : "every quarter scaled by its own lane's scale\n", bad);
+  printf(bad ? "MAPPING DIFFERS from r + 16(2(h>>1) + (j>>1)) (%d)\n" : "quarter h of lane r+16j scaled by lane r + 16(2(h>>1) + (j>>1))\n", bad);
   return bad ? 1 : 0;
 }

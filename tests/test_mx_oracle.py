@@ -1,8 +1,10 @@
 """The oracle's restatement of the wide chain's e4m3 dX GEMM with MX row-block scales
 (oracle/cvae_np.py mx_dx ↔ csrc/cvae_widechain.h gemm_mxb / mx_block), checked on CPU against a
-lane-by-lane restatement of the kernel: lane (r, q) of K-pair group g holds the 32 values of
-chunks 4g..4g+3 at chunk positions frag_k(q, e) (cvae_device.h: 4q + e, 16 + 4q + e), takes
-k = 7 − floor(log2 max|block|), converts 2^k·g to e4m3 and multiplies with unit-scaled e4m3(s·W)
+lane-by-lane restatement of the kernel: lane r + 16q of K-pair group g holds, as byte quarter h, the
+8 values of chunk 4g + h at chunk positions frag_k(q, e) (cvae_device.h: 4q + e, 16 + 4q + e); the
+instruction's MX block b of row r is quarters 2(b >> 1), 2(b >> 1) + 1 of the lanes q = 2(b & 1),
+2(b & 1) + 1 (the mapping scripts/ubench/mxscale.hip measured on the GPU), so k = 134 − biased
+exponent of the block max, 2^k·g is converted to e4m3 and multiplied with unit-scaled e4m3(s·W)
 under the E8M0 scales 2^−k and 1/s.  The blocks a reshape forms in mx_dx must be exactly these."""
 import numpy as np
 import pytest
@@ -22,12 +24,16 @@ def _lanewise(G, W, s):
     out = np.zeros((B, K))
     for r in range(B):
         for g in range(groups):
-            for q in range(4):
-                pos = [128 * g + 32 * c + _frag_k(q, e) for c in range(4) for e in range(8)]
+            for b in range(4):
+                pos = [128 * g + 32 * h + _frag_k(q, e) for h in (2 * (b >> 1), 2 * (b >> 1) + 1)
+                       for q in (2 * (b & 1), 2 * (b & 1) + 1) for e in range(8)]
                 pos = [p for p in pos if p < N]
+                if not pos:
+                    continue
                 v = G[r, pos].astype(np.float32)
-                m = float(np.abs(v).max()) if len(pos) else 0.0
-                k = min(7 - int(np.floor(np.log2(m))), 126) if m > 0 else 0
+                m = float(np.abs(v).max())
+                eb = int((np.float32(m).view(np.uint32) >> 23) & 0xFF)
+                k = min(134 - eb, 126) if eb > 0 else 0
                 x8 = cvae_np.e4m3(v * np.float32(2.0 ** k)).astype(np.float64) * 2.0 ** -k
                 out[r] += x8 @ w8[pos]
     return out
