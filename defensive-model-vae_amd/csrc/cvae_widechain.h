@@ -534,24 +534,50 @@ __device__ __forceinline__ int mx_block(const bf16x8 (&c)[4], l2& x0, l2& x1, in
   const int e = (j >> 1) ? q[1] : q[0];
   return 127 - (e > 0 ? min(134 - e, 126) : 0);
 }
+// The MX operand image of step S: wave w converts K-pair groups w, w + 8, .. of the bf16 gradient
+// image (its four chunk fragments, mx_block) into e4m3 operand halves at twin + g·2 KB + h·1 KB +
+// lane·16 and the lane's E8M0 byte at twin + NG·2 KB + (g·64 + lane)·4 — each group converted once
+// per workgroup instead of by all 8 waves (the conversion is ~130 VALU per group and lane; the GEMM
+// itself streams half the bf16 bytes).  The caller joins a barrier before gemm_mxb reads it.
+template <class A, int S>
+__device__ __forceinline__ void mx_convert(const __bf16* img, char* twin, int wave, int lane) {
+  constexpr StepInfo st = Plan<A>::step(S);
+  constexpr int KP = st.KC, NG = (KP + 1) / 2;
+#pragma unroll
+  for (int g0 = 0; g0 < NG; g0 += NW) {
+    const int g = g0 + wave;
+    if (NG % NW != 0 && g >= NG) break;  // wave-uniform
+    const bool two = 2 * g + 1 < KP;      // an odd last pair: the second half of the block is zero
+    bf16x8 c[4];
+    c[0] = xfrag(img, 4 * g);
+    c[1] = xfrag(img, 4 * g + 1);
+    c[2] = two ? xfrag(img, 4 * g + 2) : bf16x8{};
+    c[3] = two ? xfrag(img, 4 * g + 3) : bf16x8{};
+    l2 x0, x1;
+    const int sa = mx_block(c, x0, x1, lane);
+    *(l2*)(twin + g * 2048 + lane * 16) = x0;
+    *(l2*)(twin + g * 2048 + 1024 + lane * 16) = x1;
+    *(int*)(twin + NG * 2048 + (g * 64 + lane) * 4) = sa;
+  }
+}
+template <class A, int S>
+constexpr int mx_twin_bytes() {
+  constexpr int NG = (Plan<A>::step(S).KC + 1) / 2;
+  return NG * (2048 + 256);
+}
 template <class A, int P, int S, int TS>
-__device__ __forceinline__ void gemm_mxb(Ring<P>& ring, const __bf16* img, f32x4 (&acc)[TS], const char* AR, int wave,
+__device__ __forceinline__ void gemm_mxb(Ring<P>& ring, const char* twin, f32x4 (&acc)[TS], const char* AR, int wave,
                                          int lane, int sb) {
   using PL = Plan<A>;
   constexpr StepInfo st = PL::step(S);
   static_assert(st.F8 == 2 && st.TS == TS && st.GRP == 0 && !st.KS, "an MX dX step");
-  constexpr int G0 = PL::start(S), KP = st.KC;  // K pairs (two 32-wide chunks each)
+  constexpr int G0 = PL::start(S), KP = st.KC, NG = (KP + 1) / 2;  // K pairs (two 32-wide chunks each)
   sfor<0, TS>([&](auto t) { acc[decltype(t)::value] = f32x4{0.f, 0.f, 0.f, 0.f}; });
-  sfor<0, (KP + 1) / 2>([&](auto gg) {
+  sfor<0, NG>([&](auto gg) {
     constexpr int g = decltype(gg)::value, p0 = 2 * g, p1 = 2 * g + 1;
-    constexpr bool two = p1 < KP;  // an odd last pair: the second half of the block is zero
-    bf16x8 c[4];
-    c[0] = xfrag(img, 2 * p0);
-    c[1] = xfrag(img, 2 * p0 + 1);
-    c[2] = two ? xfrag(img, 2 * p1) : bf16x8{};
-    c[3] = two ? xfrag(img, 2 * p1 + 1) : bf16x8{};
-    l2 x0, x1;
-    const int sa = mx_block(c, x0, x1, lane);
+    constexpr bool two = p1 < KP;
+    const l2 x0 = *(const l2*)(twin + g * 2048 + lane * 16), x1 = *(const l2*)(twin + g * 2048 + 1024 + lane * 16);
+    const int sa = *(const int*)(twin + NG * 2048 + (g * 64 + lane) * 4);
     sfor<0, TS>([&](auto t) {
       constexpr int u = decltype(t)::value, ga = G0 + p0 * TS + u, gb = G0 + (two ? p1 : p0) * TS + u;
       acc[u] = mx2s(x0, x1, ring.r[ga % P], ring.r[gb % P], acc[u], sa, sb);
@@ -728,13 +754,21 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
 
   Ring<P> ring;
   // a dX GEMM of step S over the bf16 gradient image: e4m3 with MX scales where the layer is f8b
+  // MX operand images: the last decoder layer's in the recon time-channel buffers (dead after the
+  // fix-up step), decoder L0's and fc's in the x_rel / dL/drecon image (dead once its arena copy is out)
   auto dgemm = [&](auto sI, const __bf16* gimg, auto& acc) {
     constexpr int S_ = decltype(sI)::value;
     constexpr StepInfo st = PL::step(S_);
     constexpr int TS_ = st.TS;
-    if constexpr (st.F8 == 2)  // B's E8M0 scale: the exponent byte of 1/s (a power of two)
-      gemm_mxb<A, P, S_, TS_>(ring, gimg, acc, AR, wave, lane, (int)((__float_as_uint(INVS[st.layer]) >> 23) & 0xff));
-    else
+    if constexpr (st.F8 == 2) {  // B's E8M0 scale: the exponent byte of 1/s (a power of two)
+      constexpr int TW = st.layer == A::LDL ? A::L_RCH0 : A::L_XIN;
+      static_assert(st.layer == A::LDL ? mx_twin_bytes<A, S_>() <= 2 * S * R * 4
+                                       : (mx_twin_bytes<A, S_>() <= Ip * 32 && S_ > PL::sDLb),
+                    "MX operand image");
+      mx_convert<A, S_>(gimg, smem + TW, wave, lane);
+      lbar();
+      gemm_mxb<A, P, S_, TS_>(ring, smem + TW, acc, AR, wave, lane, (int)((__float_as_uint(INVS[st.layer]) >> 23) & 0xff));
+    } else
       gemm<A, P, S_, TS_>(ring, gimg, acc, AR, wave, lane);
   };
   constexpr int PF0 = kPreFill < P ? kPreFill : P;  // ring items issued before the x-tile wait

@@ -1,6 +1,5 @@
 set -u
 O=gpurun_out/g1; mkdir -p $O
-timeout -k 5 120 ./scripts/ubench/mxscale > $O/mxscale.txt; echo "mxscale rc=$?"
 timeout -k 10 300 python3 -u -m pytest tests/test_gpu_dp_autograd.py tests/test_train_dp.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/dp_tests.log 2>&1 || { tail -30 $O/dp_tests.log; exit 1; }
 tail -2 $O/dp_tests.log
 B="timeout -k 10 120 python3 bench.py --no-cpu-baseline --steps 200 --warmup 20 --dp"
