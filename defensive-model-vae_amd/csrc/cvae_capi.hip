@@ -1053,11 +1053,8 @@ int fwd_bwd_impl(cvae_handle* h, const CallX& c, float* grads, float* loss_out, 
   AdamArgs aa{};
   aa.grads = grads;
   LossArgs la{};
-  // the loss (and the Philox offset it advances) belongs to the chain's call, or to the decoder
-  // bucket's call when the chain ran alone
-  if ((parts & CVAE_PART_CHAIN) || parts == CVAE_PART_DW_DEC) la = make_loss(h, ra, loss_out, loss_accum);
+  if (parts & CVAE_PART_CHAIN) la = make_loss(h, ra, loss_out, loss_accum);  // the loss belongs to the chain's call
   const int dw = parts & (CVAE_PART_DW_DEC | CVAE_PART_DW_REST);
-  if (!dw) return CVAE_OK;
   if ((rc = tmark(h, s, dw == CVAE_PART_DW_DEC ? "wgrad_dec" : dw == CVAE_PART_DW_REST ? "wgrad_rest" : "wgrad")))
     return rc;
   return launch_wgrad<PM_GRAD>(h, c.batch, aa, la, s, parts);
@@ -1229,9 +1226,8 @@ int cvae_train_fwd_bwd(cvae_handle* h, const void* x, const int64_t* idx, const 
                        float* loss_out, double* loss_accum, uint64_t* counters, const cvae_adam_config* adam,
                        int parts, void* stream) {
   if (!h || !grads || ((parts & CVAE_PART_CHAIN) && !x)) return fail(CVAE_E_INVALID, "null argument");
-  if (parts != CVAE_PART_ALL && parts != (CVAE_PART_CHAIN | CVAE_PART_DW_DEC) && parts != CVAE_PART_CHAIN &&
-      parts != CVAE_PART_DW_DEC && parts != CVAE_PART_DW_REST)
-    return fail(CVAE_E_INVALID, "parts must be CVAE_PART_ALL, CHAIN|DW_DEC, CHAIN, DW_DEC or DW_REST");
+  if (parts != CVAE_PART_ALL && parts != (CVAE_PART_CHAIN | CVAE_PART_DW_DEC) && parts != CVAE_PART_DW_REST)
+    return fail(CVAE_E_INVALID, "parts must be CVAE_PART_ALL, CHAIN|DW_DEC, or DW_REST");
   int rc = check_batch(h, batch);
   if (!rc) rc = check_fault(h);
   if (rc) return rc;

@@ -485,12 +485,13 @@ __device__ __forceinline__ void gemm_grouped(Ring<P>& ring, const void* img, con
 // row r; block b = 2·(h >> 1) + (j >> 1) — the 16-B half h >> 1 of the lane pair j >> 1 — and its
 // E8M0 byte comes from lane r + 16b.  Quarter h of a lane here is its 8 values of gradient chunk
 // 4g + h, so a block is 16 positions of each of two adjacent chunks of one row (oracle mx_dx).
-// Each lane takes the two exponents of its halves' maxima, one exchange with its pair partner
-// (lane ^ 16) makes them the block maxima, k = 134 − biased exponent = 7 − floor(log2 max|G|) puts
-// a block's largest value in [128, 256) (no saturation, no step state), each half converts with
-// its block's 2^k, and one more exchange fetches the exponent of block j for the scale operand
-// (held by the lane's own pair for j ∈ {0, 3}, by lane ^ 48 for j ∈ {1, 2}); B takes 1/s: the
-// accumulator is the unscaled product.  The gradient rows span ~10^4 in magnitude (the start /
+// The operand is converted once per workgroup into LDS (mx_convert, a barrier, then gemm_mxb):
+// each lane takes the exponents of its two halves' maxima, one permlane16 swap with its pair
+// partner (lane ^ 16) makes them the block maxima, k = 134 − biased exponent = 7 − floor(log2
+// max|G|) puts a block's largest value in [128, 256) (no saturation, no step state), and each half
+// converts with its block's 2^k; in the GEMM lane j reads the exponent of block j (stored by the
+// lanes of pair j & 1 of its row) for the scale operand.  B takes 1/s: the accumulator is the
+// unscaled product.  The gradient rows span ~10^4 in magnitude (the start /
 // time terms of dL/drecon beside the mean-squared ones), which one scale per tensor cannot hold.
 __device__ __forceinline__ f32x4 mx2s(l2 x0, l2 x1, bf16x8 w0, bf16x8 w1, f32x4 acc, int sa, int sb) {
   const l2 w0l = __builtin_bit_cast(l2, w0), w1l = __builtin_bit_cast(l2, w1);
@@ -499,65 +500,80 @@ __device__ __forceinline__ f32x4 mx2s(l2 x0, l2 x1, bf16x8 w0, bf16x8 w1, f32x4 
   const i32x8 b = __builtin_bit_cast(i32x8, l4{w0l[0], w0l[1], w1l[0], w1l[1]});
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, acc, 0, 0, 0, sa, 0, sb);
 }
-// the lane's 8 values of four gradient chunks (frag_k order) → e4m3 bytes of 2^k·g (k of the
-// quarter's block), and the E8M0 byte 127 − k of block lane / 16 for the scale operand; k = 0 for an
-// all-zero block (padding rows)
-__device__ __forceinline__ int mx_block(const bf16x8 (&c)[4], l2& x0, l2& x1, int lane) {
+// k of a block whose max has biased exponent e: 2^k puts the max in [128, 256); 0 for an all-zero block
+__device__ __forceinline__ int mx_k(int e) { return e > 0 ? min(134 - e, 126) : 0; }
+// The lane's 8 values of each of four gradient chunks (frag_k order) → e4m3 bytes of 2^k·g, k of the
+// quarter's block; returns the two block exponents of the lane's pair (halves 0, 1 as two u16).  The
+// maxima are taken on the bf16 bit patterns (|x| = bits & 0x7fff orders like the values; the bf16
+// exponent field is fp32's), the pair's in one permlane16 swap (lanes L, L ^ 16), no LDS round trip.
+__device__ __forceinline__ unsigned mx_block(const bf16x8 (&c)[4], l2& x0, l2& x1) {
   typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
   unsigned eb[2];
 #pragma unroll
   for (int hh = 0; hh < 2; ++hh) {
-    float m = 0.f;
+    u16x2 m = {0, 0};
 #pragma unroll
-    for (int i = 2 * hh; i < 2 * hh + 2; ++i)
+    for (int i = 2 * hh; i < 2 * hh + 2; ++i) {
+      const u32x4 w = __builtin_bit_cast(u32x4, c[i]);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf((float)c[i][e]));
-    eb[hh] = (__float_as_uint(m) >> 23) & 0xff;  // biased exponent of the half's max (0: zero)
+      for (int t = 0; t < 4; ++t) m = __builtin_elementwise_max(m, __builtin_bit_cast(u16x2, w[t] & 0x7fff7fffu));
+    }
+    eb[hh] = (unsigned)(m[0] > m[1] ? m[0] : m[1]) >> 7;  // biased exponent of the half's max (0: zero)
   }
-  u16x2 p{(unsigned short)eb[0], (unsigned short)eb[1]};
-  p = __builtin_elementwise_max(p, __builtin_bit_cast(u16x2, __shfl_xor((int)__builtin_bit_cast(unsigned, p), 16)));
+  const unsigned p0 = eb[0] | eb[1] << 16;
+  const auto sw = __builtin_amdgcn_permlane16_swap(p0, p0, false, false);
+  const u16x2 p = __builtin_elementwise_max(__builtin_bit_cast(u16x2, (unsigned)sw[0]),
+                                            __builtin_bit_cast(u16x2, (unsigned)sw[1]));
+  // v_cvt_scalef32_pk_fp8_bf16 divides by its scale and rounds once (scripts/ubench/scalecvt.hip:
+  // bit-equal to RNE(x·2^k) over every bf16 input, e4m3 denormals included), so 2 bf16 → 2 e4m3
+  // per instruction with scale 2^−k; the block max lands in [128, 256): no saturation is needed
+  typedef short i16x2 __attribute__((ext_vector_type(2)));
   long f[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int e = p[i >> 1];
-    const int k = e > 0 ? min(134 - e, 126) : 0;
-    const float sc = __builtin_bit_cast(float, (unsigned)(127 + k) << 23);  // 2^k (k <= 126)
-    float v[8];
-#pragma unroll
-    for (int t = 0; t < 8; ++t) v[t] = (float)c[i][t] * sc;
-    f[i] = f8x8(v);
+    const float sinv = __builtin_bit_cast(float, (unsigned)(127 - mx_k(p[i >> 1])) << 23);  // 2^-k
+    // the operands as shufflevector pairs: a bit_cast of one dword of the vector made the compiler
+    // convert the first dword four times (hipcc of ROCm 7.2)
+    const bf16x8 x = c[i];
+    i16x2 lo = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(i16x2{0, 0}, __builtin_shufflevector(x, x, 0, 1), sinv, false);
+    lo = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(lo, __builtin_shufflevector(x, x, 2, 3), sinv, true);
+    i16x2 hi = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(i16x2{0, 0}, __builtin_shufflevector(x, x, 4, 5), sinv, false);
+    hi = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(hi, __builtin_shufflevector(x, x, 6, 7), sinv, true);
+    f[i] = (long)__builtin_bit_cast(unsigned, lo) | ((long)__builtin_bit_cast(unsigned, hi) << 32);
   }
   x0 = l2{f[0], f[1]};
   x1 = l2{f[2], f[3]};
-  const int j = lane >> 4;
-  const u16x2 q = __builtin_bit_cast(u16x2, __shfl((int)__builtin_bit_cast(unsigned, p), (j == 1 || j == 2) ? lane ^ 48 : lane));
-  const int e = (j >> 1) ? q[1] : q[0];
-  return 127 - (e > 0 ? min(134 - e, 126) : 0);
+  return __builtin_bit_cast(unsigned, p);
 }
 // The MX operand image of step S: wave w converts K-pair groups w, w + 8, .. of the bf16 gradient
 // image (its four chunk fragments, mx_block) into e4m3 operand halves at twin + g·2 KB + h·1 KB +
-// lane·16 and the lane's E8M0 byte at twin + NG·2 KB + (g·64 + lane)·4 — each group converted once
-// per workgroup instead of by all 8 waves (the conversion is ~130 VALU per group and lane; the GEMM
-// itself streams half the bf16 bytes).  The caller joins a barrier before gemm_mxb reads it.
+// lane·16 and the lane pair's two block exponents at twin + NG·2 KB + (g·64 + lane)·4 — each group
+// converted once per workgroup instead of by all 8 waves.  Both rounds' fragments are read before
+// either converts.  The caller joins a barrier before gemm_mxb reads it.
 template <class A, int S>
 __device__ __forceinline__ void mx_convert(const __bf16* img, char* twin, int wave, int lane) {
   constexpr StepInfo st = Plan<A>::step(S);
-  constexpr int KP = st.KC, NG = (KP + 1) / 2;
+  constexpr int KP = st.KC, NG = (KP + 1) / 2, NR = (NG + NW - 1) / NW;
+  bf16x8 c[NR][4];
 #pragma unroll
-  for (int g0 = 0; g0 < NG; g0 += NW) {
-    const int g = g0 + wave;
+  for (int r = 0; r < NR; ++r) {
+    const int g = r * NW + wave;
     if (NG % NW != 0 && g >= NG) break;  // wave-uniform
     const bool two = 2 * g + 1 < KP;      // an odd last pair: the second half of the block is zero
-    bf16x8 c[4];
-    c[0] = xfrag(img, 4 * g);
-    c[1] = xfrag(img, 4 * g + 1);
-    c[2] = two ? xfrag(img, 4 * g + 2) : bf16x8{};
-    c[3] = two ? xfrag(img, 4 * g + 3) : bf16x8{};
+    c[r][0] = xfrag(img, 4 * g);
+    c[r][1] = xfrag(img, 4 * g + 1);
+    c[r][2] = two ? xfrag(img, 4 * g + 2) : bf16x8{};
+    c[r][3] = two ? xfrag(img, 4 * g + 3) : bf16x8{};
+  }
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const int g = r * NW + wave;
+    if (NG % NW != 0 && g >= NG) break;
     l2 x0, x1;
-    const int sa = mx_block(c, x0, x1, lane);
+    const unsigned e = mx_block(c[r], x0, x1);
     *(l2*)(twin + g * 2048 + lane * 16) = x0;
     *(l2*)(twin + g * 2048 + 1024 + lane * 16) = x1;
-    *(int*)(twin + NG * 2048 + (g * 64 + lane) * 4) = sa;
+    *(unsigned*)(twin + NG * 2048 + (g * 64 + lane) * 4) = e;
   }
 }
 template <class A, int S>
@@ -577,7 +593,11 @@ __device__ __forceinline__ void gemm_mxb(Ring<P>& ring, const char* twin, f32x4 
     constexpr int g = decltype(gg)::value, p0 = 2 * g, p1 = 2 * g + 1;
     constexpr bool two = p1 < KP;
     const l2 x0 = *(const l2*)(twin + g * 2048 + lane * 16), x1 = *(const l2*)(twin + g * 2048 + 1024 + lane * 16);
-    const int sa = *(const int*)(twin + NG * 2048 + (g * 64 + lane) * 4);
+    // the scale this lane hands the instruction: block j = lane / 16 = (half j >> 1, lane pair j & 1),
+    // whose exponent the lanes of pair j & 1 of this row stored
+    const int j = lane >> 4;
+    const unsigned ep = *(const unsigned*)(twin + NG * 2048 + (g * 64 + (lane & 15) + 32 * (j & 1)) * 4);
+    const int sa = 127 - mx_k((int)(ep >> (16 * (j >> 1))) & 0xffff);
     sfor<0, TS>([&](auto t) {
       constexpr int u = decltype(t)::value, ga = G0 + p0 * TS + u, gb = G0 + (two ? p1 : p0) * TS + u;
       acc[u] = mx2s(x0, x1, ring.r[ga % P], ring.r[gb % P], acc[u], sa, sb);
@@ -767,6 +787,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
                     "MX operand image");
       mx_convert<A, S_>(gimg, smem + TW, wave, lane);
       lbar();
+      sub();
       gemm_mxb<A, P, S_, TS_>(ring, smem + TW, acc, AR, wave, lane, (int)((__float_as_uint(INVS[st.layer]) >> 23) & 0xff));
     } else
       gemm<A, P, S_, TS_>(ring, gimg, acc, AR, wave, lane);

@@ -31,8 +31,6 @@ The trainer only needs an engine with ``forward_backward / adam_step / grads / l
 """
 from __future__ import annotations
 
-import contextlib
-
 import torch
 import torch.distributed as dist
 
@@ -84,10 +82,6 @@ class DataParallelStep:
         if buckets not in (1, 2):
             raise ValueError("buckets must be 1 or 2")
         self.buckets = buckets
-        # two buckets on a GPU: the rest bucket's dW launch and its all-reduce go to a side stream
-        dev = getattr(engine, "device", None)
-        self._cuda = dev is not None and torch.device(dev).type == "cuda"
-        self._side = torch.cuda.Stream(torch.device(dev)) if self._cuda and buckets == 2 else None
         # exchange: "rccl" = all-reduce of the flat gradient, then Adam; "peer" = the in-kernel
         # exchange over IPC-mapped peer memory (cvae_amd.peer); "auto" = peer where it serves the
         # configuration and its set-up probe passes, else rccl.  self.exchange says which runs.
@@ -143,17 +137,10 @@ class DataParallelStep:
                                **({"classes": classes} if classes is not None else {}))
             return eng.loss
         two = self.buckets == 2  # every rank issues the same collectives, empty shares included
-        main = torch.cuda.current_stream(eng.device) if two and self._cuda else None
         if batch > 0:
-            kw = dict(idx=idx, eps=eps, batch=batch, weights=weights, row0=row0,
-                      **({"classes": classes} if classes is not None else {}))
-            if two:  # the row chain, then the two dW buckets on two streams (both wait for the chain only)
-                eng.forward_backward(x, parts=1, **kw)  # CVAE_PART_CHAIN
-                if main is not None:
-                    self._side.wait_stream(main)
-                eng.forward_backward(x, parts=2, **kw)  # CVAE_PART_DW_DEC (+ the loss)
-            else:
-                eng.forward_backward(x, parts=7, **kw)  # CVAE_PART_ALL
+            parts = 3 if two else 7  # CVAE_PART_CHAIN | DW_DEC, or CVAE_PART_ALL
+            eng.forward_backward(x, idx=idx, eps=eps, batch=batch, weights=weights, row0=row0, parts=parts,
+                                 **({"classes": classes} if classes is not None else {}))
             ragged = batch * self.world_size != global_batch
             scale = 1.0 if ragged else 1.0 / self.world_size
         else:  # an empty share of a ragged last batch still joins the collectives, and its device
@@ -166,17 +153,13 @@ class DataParallelStep:
             if ragged:
                 dec.mul_(batch / global_batch)
             w1 = dist.all_reduce(dec, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-            if batch == 0 and main is not None:
-                self._side.wait_stream(main)
-            side = torch.cuda.stream(self._side) if main is not None else contextlib.nullcontext()
-            with side:  # beside the decoder bucket and its all-reduce
-                if batch > 0:
-                    eng.wgrad_rest(batch)
-                if ragged:
-                    rest.mul_(batch / global_batch)
-                w2 = dist.all_reduce(rest, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            if batch > 0:
+                eng.wgrad_rest(batch)  # beside the decoder bucket's all-reduce
+            if ragged:
+                rest.mul_(batch / global_batch)
+            w2 = dist.all_reduce(rest, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
             w1.wait()
-            w2.wait()  # the current (main) stream waits for both collectives
+            w2.wait()
         else:
             if ragged and batch > 0:
                 g.mul_(batch / global_batch)

@@ -362,9 +362,7 @@ class CVAEEngine:
         """fwd + loss + bwd into ``self.grads`` (means over this batch) — the DP half-step.
 
         ``parts``: CVAE_PART_ALL, or CHAIN|DW_DEC then (separately) ``wgrad_rest()`` — the two-bucket
-        split that lets the decoder bucket's all-reduce run beside the rest of the dW GEMMs — or
-        CHAIN, then DW_DEC (same arguments: it finishes the loss) and ``wgrad_rest()``, the two dW
-        launches free to run on two streams.  The host step mirror advances with the chain."""
+        split that lets the decoder bucket's all-reduce run beside the rest of the dW GEMMs."""
         x, idx, B = self._prep(x, idx, batch)
         e = self._eps(eps, B)
         cl = self._classes(classes, x.shape[0])
@@ -375,9 +373,8 @@ class CVAEEngine:
             self._h, ptr(x), ptr(idx), ptr(cl), B, self._xflags(x), ptr(e), self.seed, 0, int(row0), C.byref(w),
             ptr(self.grads), ptr(self.loss), ptr(self.loss_accum) if accumulate else None, ptr(self.counters),
             C.byref(a), int(parts), self._stream()), "cvae_train_fwd_bwd")
-        if parts & CVAE_PART_CHAIN:
-            self._ctr[0] += 1
-            self._ctr[1] += 1
+        self._ctr[0] += 1
+        self._ctr[1] += 1
         self._last_batch = B
         return self.loss
 

@@ -195,10 +195,7 @@ int cvae_decode(cvae_handle* h, const float* z, const float* start, const float*
  * Means are over this call's batch, so a data-parallel caller all-reduces
  * `grads` and passes grad_scale = 1/world to cvae_adam.
  * parts: CVAE_PART_ALL, or CVAE_PART_CHAIN|CVAE_PART_DW_DEC followed by a CVAE_PART_DW_REST call
- * on the same batch (the two-bucket overlap; loss and counters advance in the first call), or the
- * three calls CVAE_PART_CHAIN, CVAE_PART_DW_DEC (finishes the loss and advances the Philox
- * offset: pass the same arguments as to the chain call), CVAE_PART_DW_REST — the two dW calls
- * then only need the chain's call before them, and may run concurrently on two streams.
+ * on the same batch (the two-bucket overlap; loss and counters advance in the first call).
  * counters + adam (nullable): the step this call begins, with its Adam scalars precomputed for the
  * cvae_adam(counters) that completes it — a data-parallel step is capturable as one graph. */
 int cvae_train_fwd_bwd(cvae_handle* h, const void* x, const int64_t* idx, const int32_t* classes, int batch,

@@ -55,6 +55,11 @@ if WIDE:
                  + [f"E{i}" for i in range(2, 8)] + ["FC", "D0"] + [f"D{i}" for i in range(1, 7)]
                  + ["D7+loss", "fixup", "D7b"] + [f"D{i}b" for i in range(6, 0, -1)]
                  + ["D0b", "FCb gemm", "FCb epi"] + [f"E{i}b" for i in range(7, 1, -1)] + ["E1b|C1b", "partials"])
+        if os.environ.get("DT") == "fp8":  # the MX dX steps stamp the end of their operand conversion
+            for n, m in (("D7b", ["D7b mx cvt", "D7b"]), ("D0b", ["D0b mx cvt", "D0b"]),
+                         ("FCb gemm", ["FCb mx cvt", "FCb gemm"])):
+                i = names.index(n)
+                names = names[:i] + m + names[i + 1:]
 if os.environ.get("RING") == "1":  # the reference architecture on the ring chain (CVAE_KERNEL_RING)
     names = (["prologue", "C0|E0", "C1|E1", "E2", "E3", "FC", "reparam", "D0", "D1", "D2", "D3+loss", "fixup",
               "D3b", "D2b", "D1b", "D0b", "FCb", "E3b", "E2b", "E1b|C1b", "partials"])

@@ -41,4 +41,8 @@ echo driver trace ok
 cd $GRAFT_REPO_ROOT
 TAG=${T}_cfg2 PASSES=${PASSES:-sq1,sq2,ta,tcc,fetch,write} STEPS=100 bash scripts/profile.sh || exit 1
 python3 scripts/pmc_traffic.py gpurun_out/prof ${T}_cfg2 gpurun_out/prof/${T}_traffic.json 1024 bf16 > /dev/null &&
-python3 scripts/pmc_summary.py gpurun_out/prof ${T}_cfg2 > gpurun_out/prof/${T}_cfg2_pmc_summary.txt && echo pmc ok
+python3 scripts/pmc_summary.py gpurun_out/prof ${T}_cfg2 > gpurun_out/prof/${T}_cfg2_pmc_summary.txt && echo pmc ok &&
+# BASELINE cfg5 in e4m3: instruction mix, L2 hit/miss and HBM traffic of the wide chain and its dW
+TAG=${T}_wfp8 PASSES=sq2,tcc,fetch,write STEPS=50 BENCH_EXTRA="--workload wide --dtype fp8" bash scripts/profile.sh &&
+python3 scripts/pmc_traffic.py gpurun_out/prof ${T}_wfp8 gpurun_out/prof/${T}_wfp8_traffic.json 1024 fp8 > /dev/null &&
+python3 scripts/pmc_summary.py gpurun_out/prof ${T}_wfp8 > gpurun_out/prof/${T}_wfp8_pmc_summary.txt && echo pmc wfp8 ok

@@ -17,8 +17,6 @@ from collections import defaultdict
 def short(name):
     if "rowchain_kernel" in name or "fastchain_kernel" in name or "widechain_kernel" in name:
         return "rowchain"
-    if "fused_step_kernel" in name:
-        return "fused_step"
     if "wgrad_kernel" in name:  # wgrad_kernel and fastwgrad_kernel
         return "wgrad_adam"
     if "param_kernel" in name:

@@ -54,14 +54,10 @@ class OracleEngine:
     def forward_backward(self, x, idx=None, eps=None, batch=None, weights=None, accumulate=True, row0=0, parts=7,
                          classes=None):
         # the device-counter path: the launch that begins a step advances steps-begun and the offset;
-        # adam_step then takes its step number from that counter (CVAEEngine / include/cvae.h).
-        # parts = CVAE_PART_DW_DEC alone follows a CVAE_PART_CHAIN call on the same batch: everything
-        # was computed there (the oracle has no separate dW launch)
-        self.calls.append(("fb", None if idx is None else idx.clone(), batch, row0, parts))
-        if not parts & 1:
-            return self.loss
+        # adam_step then takes its step number from that counter (CVAEEngine / include/cvae.h)
         self.step_count += 1
         self.rng_offset += 1
+        self.calls.append(("fb", None if idx is None else idx.clone(), batch, row0, parts))
         rows = x[idx] if idx is not None else x[:batch]
         cls = None if classes is None else (classes[idx] if idx is not None else classes[:batch]).long()
         rel, start = relative(rows)
