@@ -268,8 +268,11 @@ struct Ring {
 //  * an L2 warm-up of E0's fragments in the prologue measured +0.7-1.0 us (profiles/r03g/warm_ab.txt)
 //    and is not built.
 constexpr int kPreFill = 4;
+#ifndef CVAE_DIAG_EPS_PRO_F8
+#define CVAE_DIAG_EPS_PRO_F8 2  // diagnostic builds only: the e4m3 form's prologue draws (A/B)
+#endif
 template <class A>
-constexpr int kEpsProWide = A::F8 ? 2 : 0;
+constexpr int kEpsProWide = A::F8 ? CVAE_DIAG_EPS_PRO_F8 : 0;
 // one 16-B piece of fragment item at byte offset `off` from the arena base.  bf16: a
 // buffer load — lane·16 is a loop-invariant voffset, the item's offset a scalar soffset (2-3 SALU
 // per item); the 64-bit global address cost 3 VALU (one a 64-bit shift-add) + ~7 SALU per item
