@@ -11,7 +11,6 @@
 #include <cstdlib>
 #include <type_traits>
 #include <string>
-#include <deque>
 #include <vector>
 
 #include "../../include/cvae.h"
@@ -93,11 +92,6 @@ struct cvae_handle {
   // the reference architecture's training step as ONE launch (cvae_fusedring.h: ring chain + dW
   // tiles + loss block); its self-resetting hand-off words
   bool fring = false;
-  // CVAE_FUSE_RING=2 / 3: the one-launch step with the decoder tiles gated on the decoder rows
-  // (fused_ring2_kernel), its per-batch block plans (fused2_plan) for 1..kFused2MaxChain chain blocks
-  int fring_mode = 0;
-  int2* d_fplan = nullptr;
-  std::vector<int> fplan_grid;
   unsigned* d_rsync = nullptr;
   int64_t arena_bytes = 0;
   float* d_partials = nullptr;
@@ -728,45 +722,6 @@ bool wide_layout_matches(const cvae_handle* h) {
 // register prefetch: the per-CU L2 stream stays busy across step barriers.  The default for this
 // shape (row chain 17.8 vs 18.35 us at B = 1024); CVAE_RING=0 at creation keeps
 // fastchain_kernel.
-// fused_ring2_kernel's block plan for nchain chain blocks (mode 2: a decoder-tile block takes an
-// encoder tile after its decoder tile; mode 3: the remaining encoder tiles take blocks of their own).
-// Block b runs on XCD b mod 8; XCD x takes chunk x of the decoder list positions and chunk x of the
-// others (xcd_order's chunks), so each XCD's L2 reads few layers' rows.  Chain blocks take an encoder
-// tile after the chain.  Entry b = (first, second) list position, -1 = none.
-constexpr int kFused2MaxChain = 64, kFused2MaxGrid = 512;
-std::vector<int2> fused2_plan(int nchain, int mode) {
-  using T = fchain::Tiles<19>;
-  constexpr int NTL = T::total(), DEC0 = T::bucket_first(0);
-  std::deque<int> D[8], E[8];
-  auto chunks = [](std::deque<int>* q, int first, int n) {
-    const int per = n / 8, rem = n % 8;
-    int s = first;
-    for (int x = 0; x < 8; ++x)
-      for (int j = 0; j < per + (x < rem ? 1 : 0); ++j) q[x].push_back(s++);
-  };
-  chunks(D, DEC0, NTL - DEC0);
-  chunks(E, 0, DEC0);
-  std::vector<int2> pl(nchain, int2{-1, -1});
-  auto pop = [](std::deque<int>& q) { const int v = q.front(); q.pop_front(); return v; };
-  auto any = [](std::deque<int>* q) { for (int x = 0; x < 8; ++x) if (!q[x].empty()) return true; return false; };
-  const int dec0 = (int)pl.size();
-  while (any(D)) {  // decoder-tile blocks
-    const int x = (int)pl.size() % 8;
-    pl.push_back(int2{D[x].empty() ? -1 : pop(D[x]), -1});
-  }
-  const int dec1 = (int)pl.size();
-  for (int b = 0; b < nchain; ++b)
-    if (!E[b % 8].empty()) pl[b].x = pop(E[b % 8]);
-  if (mode == 2)
-    for (int b = dec0; b < dec1; ++b)
-      if (!E[b % 8].empty()) pl[b].y = pop(E[b % 8]);
-  while (any(E)) {
-    const int x = (int)pl.size() % 8;
-    pl.push_back(int2{E[x].empty() ? -1 : pop(E[x]), -1});
-  }
-  return pl;
-}
-
 int plan_ring(cvae_handle* h) {
   using A = wchain::Cfg2;
   const cvae_config& c = h->cfg;
@@ -784,20 +739,7 @@ int plan_ring(cvae_handle* h) {
   HIPCK(hipFuncSetAttribute((const void*)wchain::fused_ring_kernel<A>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             A::L_TOTAL));
   const char* fr = std::getenv("CVAE_FUSE_RING");
-  h->fring = fr && (fr[0] == '1' || fr[0] == '2' || fr[0] == '3');
-  h->fring_mode = h->fring ? fr[0] - '0' : 0;
-  if (h->fring_mode >= 2) {
-    HIPCK(hipFuncSetAttribute((const void*)wchain::fused_ring2_kernel<A>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              A::L_TOTAL));
-    HIPCK(hipMalloc(&h->d_fplan, (size_t)kFused2MaxChain * kFused2MaxGrid * sizeof(int2)));
-    h->fplan_grid.assign(kFused2MaxChain + 1, 0);
-    for (int nc = 1; nc <= kFused2MaxChain; ++nc) {
-      const std::vector<int2> pl = fused2_plan(nc, h->fring_mode);
-      h->fplan_grid[nc] = (int)pl.size() + 1;  // + the loss block
-      HIPCK(hipMemcpy(h->d_fplan + (size_t)(nc - 1) * kFused2MaxGrid, pl.data(), pl.size() * sizeof(int2),
-                      hipMemcpyHostToDevice));
-    }
-  }
+  h->fring = fr && fr[0] == '1';
   return CVAE_OK;
 }
 
@@ -1071,9 +1013,8 @@ __global__ void step_skip_kernel(uint64_t* c, double lr, double b1, double b2) {
 
 // one training step as ONE launch: ring chain + every dW tile + the loss block (cvae_fusedring.h)
 bool use_fused_ring(const cvae_handle* h, const RowArgs& ra) {  // its chain blocks also take tiles
-  const int nchain = rup_i(ra.batch, 32) / wchain::R;
-  return h->fring && ring_ok(h, ra) && ra.batch >= 1 && nchain <= fchain::Tiles<19>::total() &&
-         (h->fring_mode < 2 || nchain <= kFused2MaxChain);
+  return h->fring && ring_ok(h, ra) && ra.batch >= 1 &&
+         rup_i(ra.batch, 32) / wchain::R <= fchain::Tiles<19>::total();
 }
 int launch_fused_ring(cvae_handle* h, RowArgs ra, const AdamArgs& aa, float* loss_out, double* loss_accum,
                       hipStream_t s) {
@@ -1090,11 +1031,6 @@ int launch_fused_ring(cvae_handle* h, RowArgs ra, const AdamArgs& aa, float* los
   const int nt = fchain::Tiles<19>::total();
   int rc = tmark(h, s, "fused_step");
   if (rc) return rc;
-  if (h->fring_mode >= 2) {
-    f.plan = h->d_fplan + (size_t)(f.nchain - 1) * kFused2MaxGrid;
-    return klaunch(h, wchain::fused_ring2_kernel<A>, dim3(h->fplan_grid[f.nchain]), dim3(wchain::NT), h->ring_lds, s,
-                   h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra.ctr, ra, f);
-  }
   return klaunch(h, wchain::fused_ring_kernel<A>, dim3(nt + 1), dim3(wchain::NT), h->ring_lds, s,
                  h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra.ctr, ra, f);
 }
@@ -1174,7 +1110,6 @@ int cvae_destroy(cvae_handle* h) {
   if (!h) return CVAE_OK;
   for (auto e : h->pool) (void)hipEventDestroy(e);
   if (h->arena) (void)hipFree(h->arena);
-  if (h->d_fplan) (void)hipFree(h->d_fplan);
   if (h->fault_host) (void)hipHostFree(h->fault_host);
   cvae_px_close(h);
   delete h;
@@ -1749,7 +1684,7 @@ int cvae_ring_sync_words(cvae_handle* h, unsigned* out) {
   HIPCK(hipDeviceSynchronize());
   unsigned w[wchain::RF_WORDS];
   HIPCK(hipMemcpy(w, h->d_rsync, sizeof(w), hipMemcpyDeviceToHost));
-  for (int r = 0; r < 8; ++r) out[r] = w[wchain::RF_READY + 32 * r] + w[wchain::RF_DEC + 32 * r];
+  for (int r = 0; r < 8; ++r) out[r] = w[wchain::RF_READY + 32 * r];
   out[8] = w[wchain::RF_DONE];
   out[9] = w[wchain::RF_FLAG];
   return CVAE_OK;

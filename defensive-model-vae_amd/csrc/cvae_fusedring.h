@@ -25,10 +25,9 @@
 
 namespace wchain {
 
-// the launch's hand-off words (cvae_capi.hip alloc_arena: 4 KB, zero between launches):
-// [32 r] ready replica r (r < 8), [256] done counter, [288] sticky time-out flag, [512 + 32 r]
-// decoder-ready replica r (fused_ring2_kernel)
-constexpr int RF_READY = 0, RF_DONE = 256, RF_FLAG = 288, RF_DEC = 512, RF_WORDS = 1024;
+// the launch's hand-off words (cvae_capi.hip alloc_arena: 2 KB, zero between launches):
+// [32 r] ready replica r (r < 8), [256] done counter, [288] sticky time-out flag
+constexpr int RF_READY = 0, RF_DONE = 256, RF_FLAG = 288, RF_WORDS = 512;
 
 struct RingFuseArgs {
   AdamArgs aa;
@@ -38,7 +37,6 @@ struct RingFuseArgs {
   uint64_t timeout; // bound of a wait, s_memrealtime ticks (100 MHz)
   int Bk;           // batch rows rounded to the dW K chunk
   int nchain;       // row-chain blocks
-  const int2* plan; // fused_ring2_kernel: per block, the list positions of its (up to) two tiles
 };
 
 // one lane of a block: wait until the block's replica counts f.nchain (sc1 loads, s_sleep between
@@ -70,9 +68,6 @@ struct ReadyGate {
 
 #ifndef CVAE_FRING_P
 #define CVAE_FRING_P 11  // 12 (the two-launch chain's depth) spills at 128 VGPRs
-#endif
-#ifndef CVAE_FRING2_P
-#define CVAE_FRING2_P 10  // fused_ring2_kernel: 11 spills 16 B at 128 VGPRs
 #endif
 
 // grid = NTL + 1 blocks: block b < nchain runs row tile b of the chain, then (after the wait) dW
@@ -121,98 +116,6 @@ __global__ __launch_bounds__(NT, 4) void fused_ring_kernel(char* arena, const vo
       for (int r = 0; r < 8; ++r) __hip_atomic_store(f.sync + RF_READY + 32 * r, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(f.sync + RF_DONE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-  }
-}
-
-// ReadyGate by value (fused_ring2_kernel): rep = the replica family this tile waits on
-struct ReadyGate2 {
-  static constexpr bool gated = true;
-  unsigned* sync;
-  unsigned* fault;
-  uint64_t timeout;
-  unsigned target;
-  int family;  // RF_READY or RF_DEC
-  int* word;   // LDS
-  __device__ bool operator()() const {
-    if (threadIdx.x == 0) {
-      const unsigned* rep = sync + family + 32 * (blockIdx.x & 7);
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      int ok = 1;
-      while (__hip_atomic_load(rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-        __builtin_amdgcn_s_sleep(4);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
-          __hip_atomic_store(sync + RF_FLAG, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (fault) __hip_atomic_store(fault, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          ok = 0;
-          break;
-        }
-      }
-      *word = ok;
-    }
-    __syncthreads();
-    return *word != 0;
-  }
-};
-
-// The one-launch step with the decoder's dW overlapping the encoder backward (CVAE_FUSE_RING=2, 3):
-// each chain block publishes twice — after the decoder-L0 backward (every decoder arena row written:
-// the RF_DEC replicas) and at its end (RF_READY).  A decoder tile (list positions from
-// Tiles::bucket_first(0)) waits for RF_DEC only, so the 128 decoder tiles run while the chain's
-// fc / encoder backward does; the 152 others wait for RF_READY.  plan (host, cvae_capi.hip
-// fused2_plan): per block up to two list positions, XCD-aware (block b runs on XCD b mod 8, and
-// each XCD takes a contiguous chunk of the decoder list and of the rest): chain blocks take one
-// encoder tile after the chain, decoder-tile blocks one decoder tile and (mode 2) one encoder tile
-// after it, or (mode 3) the remaining encoder tiles take blocks of their own.  The last block
-// finishes the loss.  Done counting and the counters' reset as fused_ring_kernel (every tile + the
-// loss block).
-template <class A>
-__global__ __launch_bounds__(NT, 4) void fused_ring2_kernel(char* arena, const void* x, const int64_t* idx, int Bp,
-                                                           int batch, uint64_t* ctr, RowArgs a, RingFuseArgs f) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  using TL = fchain::Tiles<19>;
-  constexpr int NTL = TL::total(), DEC0 = TL::bucket_first(0);
-  static_assert(sizeof(WgradLds<1>) + 16 <= A::L_TOTAL, "the tiles' reduction image fits the chain's LDS");
-  WgradLds<1>* const sh = (WgradLds<1>*)smem;
-  int* const word = (int*)(smem + sizeof(WgradLds<1>));
-  auto done = [&]() {
-    if (threadIdx.x == 0) {
-      const unsigned old = __hip_atomic_fetch_add(f.sync + RF_DONE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (old == (unsigned)NTL) {  // NTL tiles + the loss block: every add and poll of this launch precede it
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          __hip_atomic_store(f.sync + RF_READY + 32 * r, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(f.sync + RF_DEC + 32 * r, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __hip_atomic_store(f.sync + RF_DONE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  };
-  if ((int)blockIdx.x == (int)gridDim.x - 1) {  // the loss block
-    const ReadyGate2 gate{f.sync, f.fault, f.timeout, (unsigned)f.nchain, RF_READY, word};
-    if (gate() && threadIdx.x < 64 && f.la.partials) finish_loss<true>(f.la, A::S, A::D, A::Z);
-    done();
-    return;
-  }
-  if ((int)blockIdx.x < f.nchain) {
-    RowArgs ra = a;
-    ra.x = x;
-    ra.idx = idx;
-    ra.batch = batch;
-    ra.ctr = ctr;
-    wide_body<A, CVAE_FRING2_P>(arena, Bp, ra, smem, blockIdx.x, f.sync + RF_READY, f.sync + RF_DEC);
-  }
-  const int2 pl = f.plan[blockIdx.x];
-#pragma nounroll
-  for (int k = 0; k < 2; ++k) {
-    const int s = k ? pl.y : pl.x;
-    if (s < 0) continue;  // block-uniform
-    __syncthreads();      // the chain's LDS / the previous tile's image becomes this tile's
-    const ReadyGate2 gate{f.sync, f.fault, f.timeout, (unsigned)f.nchain, s >= DEC0 ? RF_DEC : RF_READY, word};
-    const TileDesc td = TL::decode(s);
-    const LayerDev L = fchain::fast_layer<19>(td.layer, arena, Bp, A::I);
-    wgrad_body<__bf16, PM_ADAM, true, 1>(L, td, f.Bk, f.aa, f.la, false, A::S, A::D, A::Z, sh->red, sh->dbp,
-                                         SplitK{1, 0, nullptr, nullptr, s, 0}, nullptr, gate);
-    done();
   }
 }
 

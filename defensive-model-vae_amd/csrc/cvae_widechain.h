@@ -668,7 +668,7 @@ __device__ __forceinline__ void img_copy(const __bf16* img, const ArenaDst& dst,
 // (batch, Z)) — to a.recon_out / a.mu_out / a.lv_out: the training step's own rounding points
 template <class A, int P, bool TAP = false>
 __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const RowArgs& a, char* smem, int blk,
-                                          unsigned* pub = nullptr, unsigned* pub_dec = nullptr) {
+                                          unsigned* pub = nullptr) {
   using PL = Plan<A>;
   constexpr int Ip = A::Ip, S = A::S, D = A::D, I = A::I, Z = A::Z, NE = A::NE, ND = A::ND;
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
@@ -1312,11 +1312,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     }
     dhc2 = acc[NZT];  // feature n of dh_c: the lane that masks it in the fc backward
   }
-  // pub_dec (fused_ring2_kernel): every decoder arena row (xT in the forward, gT up to gT(D0) just
-  // above) is stored: drain them, and after the barrier one add per replica of the decoder counter
-  if (pub_dec) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   bar();
-  if (pub_dec && tid < 8) __hip_atomic_fetch_add(pub_dec + 32 * tid, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   {  // fcᵀ: dh = G_fc · W_fc → h_traj gradient (mask E(NE-1)) and h_c gradient (+ decoder share, mask C1)
     // CLS: tiles 16, 17 (waves 0, 1, slot 2) are de = fc share + decoder share (no activation) → gT(LCE)
     constexpr int TS = PL::step(PL::sFCb).TS;

@@ -287,9 +287,8 @@ int cvae_bench_kernels(cvae_handle* h, const void* x, const int64_t* idx, int ba
 int cvae_step_launches(const cvae_handle* h, int* launches);
 
 /* Its ten self-resetting hand-off words, copied to `out` (host, 10 entries): the 8 replicas of the
- * ready counter (each summed with the same replica of the decoder-ready counter of
- * CVAE_FUSE_RING=2/3), the done counter, the sticky time-out flag.  Between launches the first nine
- * are zero.  Synchronises the device. */
+ * ready counter, the done counter, the sticky time-out flag.  Between launches the first nine are
+ * zero.  Synchronises the device. */
 int cvae_ring_sync_words(cvae_handle* h, unsigned* out);
 
 /* The handle's sticky fault word.  A kernel that waits on a hand-off (the fused launch's tiles, the

@@ -1,5 +1,5 @@
 #!/bin/bash
-# The one-launch ring step with the decoder tiles gated on the decoder rows (CVAE_FUSE_RING=2, 3)
+# Round 4 (commit dc3e266, the kernel removed since): the one-launch ring step with the decoder tiles gated on the decoder rows (CVAE_FUSE_RING=2, 3)
 # against the two-launch step (0) and the round-3 one-launch form (1): parity tests, then the
 # bench alternating the four (200 steps, twice), and the per-step stamps of mode 2.
 set -u
