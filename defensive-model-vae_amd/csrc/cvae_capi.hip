@@ -21,7 +21,6 @@
 #include "cvae_fastwgrad.h"
 #include "cvae_widechain.h"
 #include "cvae_widewgrad.h"
-#include "cvae_fusedring.h"
 #include "cvae_extract.h"
 #include "cvae_mpc.h"
 
@@ -89,10 +88,6 @@ struct cvae_handle {
   int px_grid = 0;             // tile blocks of px_wgrad_kernel (the residency precondition, cvae_peer.h)
   // one-shot outputs of the next training row chain (cvae_tap_outputs): recon, mu, logvar
   float* tap[3] = {nullptr, nullptr, nullptr};
-  // the reference architecture's training step as ONE launch (cvae_fusedring.h: ring chain + dW
-  // tiles + loss block); its self-resetting hand-off words
-  bool fring = false;
-  unsigned* d_rsync = nullptr;
   int64_t arena_bytes = 0;
   float* d_partials = nullptr;
   int max_row_tiles = 0;
@@ -424,7 +419,6 @@ int alloc_arena(cvae_handle* h) {
   for (int l = 0; l < n.n_layers; ++l) maxnp = std::max(maxnp, std::max(n.L[l].Np, n.L[l].Kp));
   const int64_t zb_off = take((int64_t)maxnp * 4);
   const int64_t part_off = take((int64_t)h->max_row_tiles * 8 * 4);
-  const int64_t rsync_off = take(wchain::RF_WORDS * 4);  // fused ring step: zero between launches
   // split-K for batches of >= 8192 rows: up to 16 splits of >= 2048 rows (cvae_wgrad.h SplitK)
   h->splitk_max = std::max(1, std::min(16, rup_i(h->cfg.max_batch, 32) / 2048));
   if (rup_i(h->cfg.max_batch, 32) < 8192) h->splitk_max = 1;
@@ -457,7 +451,6 @@ int alloc_arena(cvae_handle* h) {
   n.zbias = (const float*)(h->arena + zb_off);
   n.bias_all = (const float*)(h->arena + bias_base);
   h->d_partials = (float*)(h->arena + part_off);
-  h->d_rsync = (unsigned*)(h->arena + rsync_off);
   if (h->splitk_max > 1) {  // tickets start at zero (the arena memset) and return to zero after every launch
     h->splitk_ws = (float*)(h->arena + skw_off);
     h->splitk_tickets = (unsigned*)(h->arena + skt_off);
@@ -735,11 +728,6 @@ int plan_ring(cvae_handle* h) {
                             hipFuncAttributeMaxDynamicSharedMemorySize, A::L_TOTAL));
   h->ring = true;
   h->ring_lds = A::L_TOTAL;
-  // the one-launch step (cvae_fusedring.h): CVAE_FUSE_RING=0 at creation keeps two launches
-  HIPCK(hipFuncSetAttribute((const void*)wchain::fused_ring_kernel<A>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            A::L_TOTAL));
-  const char* fr = std::getenv("CVAE_FUSE_RING");
-  h->fring = fr && fr[0] == '1';
   return CVAE_OK;
 }
 
@@ -1011,30 +999,6 @@ __global__ void step_skip_kernel(uint64_t* c, double lr, double b1, double b2) {
   c[0] = c[0] + 1;
 }
 
-// one training step as ONE launch: ring chain + every dW tile + the loss block (cvae_fusedring.h)
-bool use_fused_ring(const cvae_handle* h, const RowArgs& ra) {  // its chain blocks also take tiles
-  return h->fring && ring_ok(h, ra) && ra.batch >= 1 &&
-         rup_i(ra.batch, 32) / wchain::R <= fchain::Tiles<19>::total();
-}
-int launch_fused_ring(cvae_handle* h, RowArgs ra, const AdamArgs& aa, float* loss_out, double* loss_accum,
-                      hipStream_t s) {
-  using A = wchain::Cfg2;
-  ra.stamps = h->d_stamps;
-  wchain::RingFuseArgs f{};
-  f.aa = aa;
-  f.la = make_loss(h, ra, loss_out, loss_accum);
-  f.sync = h->d_rsync;
-  f.fault = h->fault_dev;
-  f.timeout = 200000000ull;  // 2 s of s_memrealtime (100 MHz); the chain takes ~20 us
-  f.Bk = bk_of(h, ra.batch);
-  f.nchain = rup_i(ra.batch, 32) / wchain::R;
-  const int nt = fchain::Tiles<19>::total();
-  int rc = tmark(h, s, "fused_step");
-  if (rc) return rc;
-  return klaunch(h, wchain::fused_ring_kernel<A>, dim3(nt + 1), dim3(wchain::NT), h->ring_lds, s,
-                 h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra.ctr, ra, f);
-}
-
 int check_adam(const cvae_adam_config* adam) {
   if (!adam) return fail(CVAE_E_INVALID, "null adam config");
   if (!(adam->beta1 >= 0.0 && adam->beta1 < 1.0 && adam->beta2 >= 0.0 && adam->beta2 < 1.0))
@@ -1067,7 +1031,6 @@ int train_step_impl(cvae_handle* h, const CallX& c, float* params, float* m, flo
   CallX ca = c;
   ca.adam = adam;
   const RowArgs ra = row_args(h, ca);
-  if (use_fused_ring(h, ra)) return launch_fused_ring(h, ra, aa, loss_out, loss_accum, s);
   int rc = is16(h) ? launch_train_chain<__bf16>(h, ra, s) : launch_train_chain<float>(h, ra, s);
   if (rc) return rc;
   const LossArgs la = make_loss(h, ra, loss_out, loss_accum);
@@ -1669,24 +1632,6 @@ int cvae_fault(const cvae_handle* h, unsigned* word) {
 int cvae_clear_fault(cvae_handle* h) {
   if (!h) return fail(CVAE_E_INVALID, "null argument");
   if (h->fault_host) __atomic_store_n(h->fault_host, 0u, __ATOMIC_RELEASE);
-  if (h->d_rsync) HIPCK(hipMemset(h->d_rsync, 0, wchain::RF_WORDS * 4));  // a timed-out launch left counts
-  return CVAE_OK;
-}
-
-int cvae_step_launches(const cvae_handle* h, int* launches) {
-  if (!h || !launches) return fail(CVAE_E_INVALID, "null argument");
-  *launches = h->fring ? 1 : 2;
-  return CVAE_OK;
-}
-
-int cvae_ring_sync_words(cvae_handle* h, unsigned* out) {
-  if (!h || !out) return fail(CVAE_E_INVALID, "null argument");
-  HIPCK(hipDeviceSynchronize());
-  unsigned w[wchain::RF_WORDS];
-  HIPCK(hipMemcpy(w, h->d_rsync, sizeof(w), hipMemcpyDeviceToHost));
-  for (int r = 0; r < 8; ++r) out[r] = w[wchain::RF_READY + 32 * r];
-  out[8] = w[wchain::RF_DONE];
-  out[9] = w[wchain::RF_FLAG];
   return CVAE_OK;
 }
 

@@ -172,9 +172,9 @@ __global__ __launch_bounds__(WG_THREADS) void fastwgrad_kernel(char* arena, floa
   LayerDev L;
   decode_tile<NKI>(sk.tile, fn.arena, fn.Bp, fn.I, td, L);
   if (Tiles<NKI>::ni(td.layer) == 2)  // block-uniform
-    wgrad_body<__bf16, MODE, false, 2>(L, td, Bk, aa, la, false, fn.S, fn.D, Z, sh.red, sh.dbp, sk);
+    wgrad_body<__bf16, MODE, 2>(L, td, Bk, aa, la, false, fn.S, fn.D, Z, sh.red, sh.dbp, sk);
   else
-    wgrad_body<__bf16, MODE, false, 1>(L, td, Bk, aa, la, false, fn.S, fn.D, Z, sh.red, sh.dbp, sk);
+    wgrad_body<__bf16, MODE, 1>(L, td, Bk, aa, la, false, fn.S, fn.D, Z, sh.red, sh.dbp, sk);
 }
 
 // One dW bucket of the data-parallel two-bucket step (dist.py buckets=2): the tiles of list
@@ -202,7 +202,7 @@ __global__ __launch_bounds__(WG_THREADS) void fastwgrad_bucket_kernel(char* aren
   sk.tile = first + Tiles<NKI>::slot((int)blockIdx.x - sk.s * n, n);
   const TileDesc td = Tiles<NKI>::decode(sk.tile);
   const LayerDev L = fast_layer<NKI>(td.layer, fn.arena, fn.Bp, fn.I);
-  wgrad_body<__bf16, MODE, false, 1>(L, td, Bk, aa, la, false, fn.S, fn.D, Z, sh.red, sh.dbp, sk);
+  wgrad_body<__bf16, MODE, 1>(L, td, Bk, aa, la, false, fn.S, fn.D, Z, sh.red, sh.dbp, sk);
 }
 
 // Adam from the all-reduced gradient buffer (the RCCL data-parallel step's last launch,
@@ -264,9 +264,9 @@ __global__ __launch_bounds__(WG_THREADS, 4) void px_wgrad_kernel(char* arena, fl
     LayerDev L;
     decode_tile<NKI>(t, fn.arena, fn.Bp, fn.I, td, L);
     if (owned)
-      wgrad_body<__bf16, PM_ADAM, false, 1>(L, td, Bk, aa, la, false, fn.S, fn.D, Z, sh.red, sh.dbp, sk, &px);
+      wgrad_body<__bf16, PM_ADAM, 1>(L, td, Bk, aa, la, false, fn.S, fn.D, Z, sh.red, sh.dbp, sk, &px);
     else
-      wgrad_body<__bf16, PM_GRAD, false, 1>(L, td, Bk, aa, la, false, fn.S, fn.D, Z, sh.red, sh.dbp, sk, &px);
+      wgrad_body<__bf16, PM_GRAD, 1>(L, td, Bk, aa, la, false, fn.S, fn.D, Z, sh.red, sh.dbp, sk, &px);
   };
   if constexpr (!SHARED) {
     tile(blockIdx.x, px_owner(blockIdx.x, px.world) == px.rank);  // block-uniform

@@ -381,16 +381,11 @@ __device__ __forceinline__ void px_broadcast(const PeerArgs& p, const LayerDev& 
 }
 
 // called by one whole wave: lane-strided partial sums, then a fixed-order butterfly (deterministic).
-// SC1: the partials were handed over inside the launch (sc1 loads, fused_step_kernel).
-template <bool SC1 = false>
 __device__ void finish_loss(const LossArgs& l, int S, int D, int Z) {
   const int lane = threadIdx.x & 63;
   float s[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   for (int t = lane; t < l.ntiles; t += 64)
-    for (int k = 0; k < 5; ++k)
-      s[k] += SC1 ? __builtin_bit_cast(float, __hip_atomic_load((const unsigned*)(l.partials + t * 8 + k),
-                                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                  : l.partials[t * 8 + k];
+    for (int k = 0; k < 5; ++k) s[k] += l.partials[t * 8 + k];
   for (int k = 0; k < 5; ++k) s[k] = wave_sum(s[k]);
   if (lane != 0) return;
   const float B = (float)l.batch;
@@ -432,24 +427,13 @@ struct SplitK {
   int pw;             // floats per partial (0: 32·TW + 32 of the tile)
 };
 
-// A wait inside the launch before the arena rows are read (cvae_fusedring.h): gate() returns false
-// on a time-out (the block then skips its update).  NoGate: the rows are final at launch.
-struct NoGate {
-  static constexpr bool gated = false;
-  __device__ bool operator()() const { return true; }
-};
-
 // One workgroup = tile td of layer L: 32 outputs × 32·NI inputs (NI = 2: two 32-wide input tiles
 // sharing the G rows).  loss_block: this workgroup also finishes the loss (S, D, Z: its shape).
-// SC1: the arena rows were handed over inside the launch (fused_step_kernel): every load of them
-// is an sc1 buffer load.  gate (gated): called after the master-state loads are issued, before
-// any operand load; the step's Adam scalars are then read after it (sc1), not first.
-template <typename T, int MODE, bool SC1 = false, int NI = 1, class Gate = NoGate>
+template <typename T, int MODE, int NI = 1>
 __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td, int Bk, AdamArgs aa,
                                            const LossArgs& la, bool loss_block, int S, int D, int Z,
                                            float* red, float* dbp, SplitK sk = SplitK{1, 0, nullptr, nullptr, 0},
-                                           const PeerArgs* px = nullptr, Gate&& gate = Gate{}) {
-  constexpr bool GATED = std::remove_reference_t<Gate>::gated;
+                                           const PeerArgs* px = nullptr) {
   using V = typename Op<T>::V;
   constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC;
   constexpr int NX = 2 * NI, TW = 32 * NI, LD = TW + 4;  // X fragments per chunk, tile width, image stride
@@ -464,8 +448,8 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
   using VE = typename VecF<EPT>::T;
   const int o = tid / TPR, iv = (tid % TPR) * EPT;
 
-  if (!GATED) WSTAMP(0);  // gated: the stamp marks the end of the wait
-  adam_f32x2 t_step = MODE == PM_ADAM && !GATED ? adam_step_load(aa) : adam_f32x2{0.f, 0.f};
+  WSTAMP(0);
+  const adam_f32x2 t_step = MODE == PM_ADAM ? adam_step_load(aa) : adam_f32x2{0.f, 0.f};
   f32x4 acc[2][NX];
 #pragma unroll
   for (int m = 0; m < 2; ++m)
@@ -490,28 +474,12 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
   // otherwise take the kernel past 128 VGPRs (one workgroup per CU instead of two)
   constexpr int PF = NI == 2 ? 2 : 4;
   V ga[PF][2], xb[PF][NX];
-  __amdgpu_buffer_rsrc_t rg, rx;
-  if (SC1) {
-    rg = __builtin_amdgcn_make_buffer_rsrc((void*)G, (short)0, 0x7fffffff, 0x00020000);
-    rx = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, 0x7fffffff, 0x00020000);
-  }
   auto load = [&](int u, int j) {  // unconditional, clamped to this wave's last chunk
     const size_t ct = (size_t)(c0 + wave + WG_NW * min(j, nmine > 0 ? nmine - 1 : 0)) * (KC / 16) * 16;
-    if (SC1) {
 #pragma unroll
-      for (int m = 0; m < 2; ++m)
-        ga[u][m] = __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(
-                                             rg, (int)((gp[m] + ct * Kg - G) * sizeof(T)), 0, 16));
+    for (int m = 0; m < 2; ++m) ga[u][m] = gld<V>(gp[m] + ct * Kg);
 #pragma unroll
-      for (int n = 0; n < NX; ++n)
-        xb[u][n] = __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(
-                                             rx, (int)((xp[n] + ct * Kx - X) * sizeof(T)), 0, 16));
-    } else {
-#pragma unroll
-      for (int m = 0; m < 2; ++m) ga[u][m] = gld<V>(gp[m] + ct * Kg);
-#pragma unroll
-      for (int n = 0; n < NX; ++n) xb[u][n] = gld<V>(xp[n] + ct * Kx);
-    }
+    for (int n = 0; n < NX; ++n) xb[u][n] = gld<V>(xp[n] + ct * Kx);
   };
   // the master state the epilogue updates (independent of the gradient), issued FIRST: the
   // compiler's waits inside loadn's paths then cover nothing but these loads, never the operands
@@ -519,18 +487,11 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
   if (tid < 32 * TPR) st = loadn<MODE, EPT>(L, td.o0 + o, td.i0 + iv, aa);
   PreB sb = {0.f, 0.f, 0.f, -1};
   if (bias_tile && tid < 32) sb = loadb<MODE>(L, td.o0 + tid, aa);
-  if constexpr (GATED) {
-    if (!gate()) return;  // block-uniform
-    WSTAMP(0);
-    if (MODE == PM_ADAM && aa.ctr)
-      t_step = __builtin_bit_cast(adam_f32x2, __hip_atomic_load((const uint64_t*)(aa.ctr + 2), __ATOMIC_RELAXED,
-                                                                __HIP_MEMORY_SCOPE_AGENT));
-  }
 #pragma unroll
   for (int u = 0; u < PF; ++u) load(u, u);
   // device-counter path: this step's Adam scalars (double pow), computed while the operands load
   if (MODE == PM_ADAM) adam_resolve(aa, t_step);
-  if (loss_block && wave == WG_NW - 1 && la.partials) finish_loss<SC1>(la, S, D, Z);
+  if (loss_block && wave == WG_NW - 1 && la.partials) finish_loss(la, S, D, Z);
   for (int j0 = 0; j0 < nmine; j0 += PF) {
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
@@ -669,7 +630,7 @@ __global__ __launch_bounds__(WG_THREADS, 4) void wgrad_kernel(NetDev net, const 
   const TileDesc td = tiles[sk.tile];
   if constexpr (NI2) {
     if (td.ni == 2) {  // block-uniform
-      wgrad_body<T, MODE, false, 2>(net.L[td.layer], td, Bk, aa, la, blockIdx.x == 0, net.S, net.D, net.Z, sh.red,
+      wgrad_body<T, MODE, 2>(net.L[td.layer], td, Bk, aa, la, blockIdx.x == 0, net.S, net.D, net.Z, sh.red,
                                     sh.dbp, sk);
       return;
     }

@@ -661,14 +661,11 @@ __device__ __forceinline__ void img_copy(const __bf16* img, const ArenaDst& dst,
   }
 }
 
-// pub (the fused step, cvae_fusedring.h): after its last arena store the block drains every store
-// (all sc1) and adds 1 to each of the 8 replicas of the ready counter (pub[32 r], a line each)
 // TAP (parity tests only, cvae_tap_outputs): the chain also writes what its epilogues computed —
 // recon (the last decoder layer's output before the loss, fp32 (batch, S, D)), mu and logvar (fp32
 // (batch, Z)) — to a.recon_out / a.mu_out / a.lv_out: the training step's own rounding points
 template <class A, int P, bool TAP = false>
-__device__ __forceinline__ void wide_body(char* const AR, const int Bp, const RowArgs& a, char* smem, int blk,
-                                          unsigned* pub = nullptr) {
+__device__ __forceinline__ void wide_body(char* const AR, const int Bp, const RowArgs& a, char* smem, int blk) {
   using PL = Plan<A>;
   constexpr int Ip = A::Ip, S = A::S, D = A::D, I = A::I, Z = A::Z, NE = A::NE, ND = A::ND;
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
@@ -917,7 +914,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
       const uint64_t t = *(const __attribute__((address_space(4))) uint64_t*)(a.ctr + 1) + 1;
       float s0 = 0.f, s1 = 0.f;
       if (a.adam_pre && !CVAE_DIAG_NOADAMPRE) adam_scalars(a.lr, a.beta1, a.beta2, (double)t, s0, s1);
-      if (lane == 0) {  // write-through (sc1): the fused step's dW tiles on other XCDs read them
+      if (lane == 0) {  // agent-scope stores: the lines leave this CU's cache at once
         __hip_atomic_store(a.ctr + 1, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (a.adam_pre)
           __hip_atomic_store(a.ctr + 2, __builtin_bit_cast(uint64_t, adam_f32x2{s0, s1}), __ATOMIC_RELAXED,
@@ -1378,14 +1375,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     float s = 0.f;
     for (int w = 0; w < NW; ++w) s += PART[w * 8 + tid];
     __hip_atomic_store((unsigned*)(a.partials + blk * 8 + tid), __builtin_bit_cast(unsigned, s), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);  // sc1: the fused step's loss block reads it
-  }
-  if (pub) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lbar();
-    if (CVAE_DIAG_STAMPS && tid == 0 && stamp_i < 64) STAMPS[stamp_i] = __builtin_amdgcn_s_memrealtime();
-    if (CVAE_DIAG_STAMPS) ++stamp_i;
-    if (tid < 8) __hip_atomic_fetch_add(pub + 32 * tid, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                       __HIP_MEMORY_SCOPE_AGENT);  // (a plain store here took the cfg4 chain to 130 VGPRs)
   }
   if (CVAE_DIAG_STAMPS && a.stamps && tid < 64)
     gst<unsigned long long>(a.stamps + blk * 64 + tid, tid < stamp_i ? STAMPS[tid] : 0ull);

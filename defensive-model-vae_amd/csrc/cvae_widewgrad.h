@@ -135,9 +135,9 @@ __global__ __launch_bounds__(WG_THREADS, 4) void widewgrad_kernel(char* arena, f
   const TileDesc td = WTiles<A>::at(sk.tile);
   const LayerDev L = wide_layer<A>(td.layer, arena, Bp);
   if (td.ni == 2)  // block-uniform
-    wgrad_body<__bf16, MODE, false, 2>(L, td, Bk, aa, la, false, A::S, A::D, A::Z, sh.red, sh.dbp, sk);
+    wgrad_body<__bf16, MODE, 2>(L, td, Bk, aa, la, false, A::S, A::D, A::Z, sh.red, sh.dbp, sk);
   else
-    wgrad_body<__bf16, MODE, false, 1>(L, td, Bk, aa, la, false, A::S, A::D, A::Z, sh.red, sh.dbp, sk);
+    wgrad_body<__bf16, MODE, 1>(L, td, Bk, aa, la, false, A::S, A::D, A::Z, sh.red, sh.dbp, sk);
 }
 
 }  // namespace wchain

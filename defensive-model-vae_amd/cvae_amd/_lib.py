@@ -70,8 +70,6 @@ _SIGS = {
     "cvae_train_steps": (_i, [_v, _v, _v, _v, _i, _i, _i, _v, _u64, _u64, _i64, _W, _v, _v, _v, _i64, _A, _v, _v,
                               _v, _v]),
     "cvae_bench_kernels": (_i, [_v, _v, _v, _i, _i, _v, _v, _v, _i64, C.POINTER(_f), _v]),
-    "cvae_step_launches": (_i, [_v, C.POINTER(C.c_int)]),
-    "cvae_ring_sync_words": (_i, [_v, C.POINTER(C.c_uint)]),
     "cvae_fault": (_i, [_v, C.POINTER(C.c_uint)]),
     "cvae_clear_fault": (_i, [_v]),
     "cvae_step_skip": (_i, [_v, _v, _A, _v]),  # h, counters, adam, stream

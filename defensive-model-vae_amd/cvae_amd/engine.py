@@ -537,21 +537,6 @@ class CVAEEngine:
         self.step_count = self.step_count + 2 * int(reps)
         return {"rowchain": ms[0], "wgrad_adam": ms[1], "step": ms[2]}
 
-    def ring_sync_words(self):
-        """The one-launch step's hand-off words (cvae_ring_sync_words): 8 ready-counter replicas,
-        the done counter, the sticky time-out flag; the first nine are zero between launches."""
-        out = (C.c_uint * 10)()
-        check(lib().cvae_ring_sync_words(self._h, out), "cvae_ring_sync_words")
-        return list(out)
-
-    @property
-    def step_launches(self):
-        """Kernels per training step on this engine: 1 (the one-launch step, cvae_fusedring.h) or 2
-        (row chain, then dW ⊕ Adam) — cvae_step_launches."""
-        n = C.c_int()
-        check(lib().cvae_step_launches(self._h, C.byref(n)))
-        return n.value
-
     @property
     def train_kernel(self):
         """'generic', 'fast' / 'ring' (reference architecture, bf16; 'ring' = the single weight-stream

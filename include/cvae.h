@@ -280,20 +280,8 @@ int cvae_kernel_times(cvae_handle* h, char* names, int names_len, float* ms, int
 int cvae_bench_kernels(cvae_handle* h, const void* x, const int64_t* idx, int batch, int reps,
                        float* params, float* m, float* v, int64_t step0, float* ms, void* stream);
 
-/* The one-launch training step of the reference architecture at S = 100 (the ring chain, every
- * dW ⊕ Adam tile and the loss block in ONE kernel; replaces the chain + dW pair of
- * cvae_train_step when enabled — CVAE_FUSE_RING at handle creation):
- * *launches = the kernels one cvae_train_step launches on this handle (1 or 2). */
-int cvae_step_launches(const cvae_handle* h, int* launches);
-
-/* Its ten self-resetting hand-off words, copied to `out` (host, 10 entries): the 8 replicas of the
- * ready counter, the done counter, the sticky time-out flag.  Between launches the first nine are
- * zero.  Synchronises the device. */
-int cvae_ring_sync_words(cvae_handle* h, unsigned* out);
-
-/* The handle's sticky fault word.  A kernel that waits on a hand-off (the fused launch's tiles, the
- * peer exchange) waits a bounded time; on a time-out it skips its update and sets this word in
- * pinned host memory.  Every later training call (cvae_train_step[s], cvae_train_fwd_bwd, cvae_adam)
+/* The handle's sticky fault word.  A kernel that waits on a hand-off (the peer exchange) waits a
+ * bounded time; on a time-out it skips its update and sets this word in pinned host memory.  Every later training call (cvae_train_step[s], cvae_train_fwd_bwd, cvae_adam)
  * then returns CVAE_E_TIMEOUT without launching; the check reads host memory and does not
  * synchronise, so it sees a time-out once the faulting launch has run.  cvae_fault reads the word,
  * cvae_clear_fault resets it (after the caller restored consistent parameters). */

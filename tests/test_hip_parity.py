@@ -422,66 +422,6 @@ def test_train_steps_equals_repeated_train_step(cvae):
         assert torch.equal(e1.loss, e2.loss) and torch.equal(e1.loss_accum, e2.loss_accum), dtype
 
 
-def _fring_pair(cvae, monkeypatch, max_batch=1024):
-    """Two engines of the reference architecture on the ring chain from the same weights: e1 with
-    the two-launch step, e2 with the one-launch step (CVAE_FUSE_RING at creation)."""
-    torch.manual_seed(0)
-    ref = OracleCVAE(100, 6, 8)
-    engines = []
-    for v in ("0", "1"):
-        monkeypatch.setenv("CVAE_FUSE_RING", v)
-        engines.append(_model(cvae, 100, 6, 8, sd=ref.state_dict(), dtype="bf16", max_batch=max_batch)[1])
-    monkeypatch.delenv("CVAE_FUSE_RING")
-    e1, e2 = engines
-    assert e1.train_kernel == e2.train_kernel == "ring"
-    assert (e1.step_launches, e2.step_launches) == (2, 1)
-    return e1, e2
-
-
-def _same_state(e1, e2, what):
-    assert torch.equal(e1.params, e2.params), what
-    assert torch.equal(e1.m, e2.m) and torch.equal(e1.v, e2.v), what
-    assert torch.equal(e1.loss, e2.loss) and torch.equal(e1.loss_accum, e2.loss_accum), what
-    assert torch.equal(e1.counters, e2.counters), what
-
-
-def test_fused_ring_step_equals_two_launch_ring_step(cvae, monkeypatch):
-    """The one-launch step (cvae_fusedring.h: ring chain + every dW ⊕ Adam tile + the loss block,
-    hand-off through a replicated ready counter inside the launch) == the two-launch ring step
-    (widechain_kernel, then fastwgrad_kernel), bit for bit after every step: params, moments, the
-    loss and its fp64 accumulator, the device counters (Philox offset, Adam step) — full and ragged
-    batches (1024, 77, 16 rows), Philox and host eps, bf16 operand rows and fp32 rows (CVAE_X_F32);
-    the self-resetting hand-off words are zero after every launch and the time-out flag clear."""
-    e1, e2 = _fring_pair(cvae, monkeypatch)
-    data = torch.randn(2048, 100, 6).cuda() * 3.0
-    x16 = e1.as_input(data)
-    cases = [(1024, None, x16), (1024, "host", x16), (77, None, x16), (16, "host", x16), (1000, None, data),
-             (160, "host", data)]
-    for i, (B, eps_kind, x) in enumerate(cases):
-        idx = torch.randint(0, 2048, (B,), generator=torch.Generator().manual_seed(i)).cuda()
-        eps = torch.randn(B, 8, generator=torch.Generator().manual_seed(50 + i)).cuda() if eps_kind else None
-        for e in (e1, e2):
-            e.keep_f32 = x.dtype == torch.float32
-            e.train_step(x, idx=idx, eps=eps)
-        torch.cuda.synchronize()
-        _same_state(e1, e2, (i, B))
-        assert e2.ring_sync_words() == [0] * 10, (i, B)
-        assert torch.isfinite(e2.loss).all()
-
-
-def test_fused_ring_train_steps_prepared_equal_two_launch(cvae, monkeypatch):
-    """K one-launch steps issued by one cvae_train_steps call (the bench's prepared call) == the same
-    K two-launch steps, bit for bit; back-to-back launches reuse the self-reset counters."""
-    e1, e2 = _fring_pair(cvae, monkeypatch)
-    x = e1.as_input(torch.randn(1024, 100, 6))
-    runs = [e.prepare_steps(x, batch=1024) for e in (e1, e2)]
-    for r in runs:
-        r(25)
-    torch.cuda.synchronize()
-    _same_state(e1, e2, "prepared x25")
-    assert e2.ring_sync_words() == [0] * 10
-
-
 def _bf16_run(cvae, sd, x, idx_list, monkeypatch=None, env=None):
     if monkeypatch is not None:
         if env:

@@ -48,7 +48,7 @@ def test_ring_chain_fits_128_vgprs_without_scratch(res):
 
 
 def test_two_blocks_per_cu_kernels_fit(res):
-    for name in ("px_wgrad_kernel", "fused_ring_kernel"):
+    for name in ("px_wgrad_kernel",):
         ks = _pick(res, name)
         assert ks, name
         for k in ks:
