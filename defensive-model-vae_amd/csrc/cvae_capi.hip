@@ -987,7 +987,8 @@ int check_fault(const cvae_handle* h) {
   if (h->fault_host && __atomic_load_n(h->fault_host, __ATOMIC_ACQUIRE))
     return fail(CVAE_E_TIMEOUT, "an earlier training launch timed out waiting for a hand-off and skipped its "
                                 "update (fault word set); the parameters are incomplete — cvae_clear_fault after "
-                                "restoring them");
+                                "restoring them (with the peer exchange open: cvae_px_reset on every rank, which "
+                                "also re-arms its mailbox)");
   return CVAE_OK;
 }
 
