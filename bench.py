@@ -446,7 +446,10 @@ def main():
         nbytes["px_wgrad"] = bt["wgrad"] * rows_launch + ADAM_BYTES_PER_PARAM * n_par // max(world, 1)
         dom = max((k for k in kt if k in flop and flop[k] > 0), key=lambda k: kt[k][0])
         std = (S, D, Z, H, NE, ND) == (100, 6, 8, 128, 4, 4)
-        traffic = measured_traffic(args.traffic_file, dom, B, dtype) if std else None
+        # BASELINE cfg5's shape: its own committed pass (gpu_round.sh, profiles/traffic_wide_<dtype>.json)
+        tfile = args.traffic_file if std else (os.path.join(ROOT, "profiles", f"traffic_wide_{dtype}.json")
+                                              if (S, D, Z, H, NE, ND) == (200, 6, 512, 128, 8, 8) else None)
+        traffic = measured_traffic(tfile, dom, B, dtype) if tfile else None
         roof = roofline(dom, kt[dom][0], flop[dom], nbytes[dom], dtype, traffic)
         if "rowchain" in kt and wl != "cfg1":
             wsb = weight_stream_bytes(S, D, Z, H, dtype, n_enc=NE, n_dec=ND)
