@@ -115,8 +115,10 @@ def _reference(sizes, steps):
 # then had 281 blocks per rank, 1,124 against the GPU's 512 workgroup slots; the exchange is now
 # sized to the residency precondition (cvae_peer.h: k ranks on one GPU share its slots, 127 tile
 # blocks each at k = 4, every block pushing its tiles before it waits on any it owns).
-@pytest.mark.parametrize("sizes", [(64, 64), (96, 32), (40, 24, 0), (64, 64, 64, 64)],
-                         ids=["w2", "ragged", "empty-share", "w4"])
+# world 8: the driver's N = 8 ownership (tile t -> rank t mod 8) and flag epochs, 8 ranks on one GPU
+# (63 tile blocks each).
+@pytest.mark.parametrize("sizes", [(64, 64), (96, 32), (40, 24, 0), (64, 64, 64, 64), (32,) * 8],
+                         ids=["w2", "ragged", "empty-share", "w4", "w8"])
 def test_peer_exchange_equals_split_step(sizes, tmp_path):
     """world ranks on one GPU through the in-kernel exchange == the split data-parallel step of
     the same partial gradients in one process, bit for bit, after 3 steps."""
