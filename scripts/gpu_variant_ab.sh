@@ -2,7 +2,7 @@
 # GPU box: bench A/B of the current library against diagnostic builds (names in $VARIANTS),
 # alternating, cfg2 (default) and optionally the wide shape ($WIDE=1).
 set -u
-O=gpurun_out/vab; mkdir -p $O
+O=${O:-gpurun_out/vab}; mkdir -p $O
 EX=""; [ "${WIDE:-0}" = 1 ] && EX="--workload wide --dtype ${DT:-bf16} --steps 100 --warmup 10"
 B="timeout -k 10 120 python -u bench.py --no-cpu-baseline --steps 400 $EX"
 for i in 1 2; do

@@ -1037,3 +1037,4 @@ def test_rccl_allreduce_split_step_equals_fused(cvae):
         assert torch.equal(acc1, acc2) and float(e2.loss_accum.abs().sum()) == 0.0
     finally:
         tdist.destroy_process_group()
+
