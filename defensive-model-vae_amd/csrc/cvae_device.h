@@ -235,9 +235,12 @@ __device__ __forceinline__ void adam_precompute(uint64_t* ctr, double lr, double
 }
 
 // ------------------------------------------------------------------ Philox4x32-10
+#ifndef CVAE_DIAG_PHILOX_ROUNDS
+#define CVAE_DIAG_PHILOX_ROUNDS 10  // diagnostic builds only (A/B of the draw's cost)
+#endif
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
 #pragma unroll
-  for (int i = 0; i < 10; ++i) {
+  for (int i = 0; i < CVAE_DIAG_PHILOX_ROUNDS; ++i) {
     // one 32 x 32 -> 64-bit product per word (v_mad_u64_u32) instead of separate lo and hi multiplies
     const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
     const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
