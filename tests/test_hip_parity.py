@@ -1038,3 +1038,33 @@ def test_rccl_allreduce_split_step_equals_fused(cvae):
     finally:
         tdist.destroy_process_group()
 
+
+
+@pytest.mark.parametrize("B", [1024, 8192])
+def test_dw_buckets_equal_whole_launch(cvae, monkeypatch, B):
+    """The two dW buckets of the RCCL data-parallel step (fchain::fastwgrad_bucket_kernel: the
+    decoder tail of the tile list with the chain, then the rest) give the whole dW launch's gradient
+    bit for bit — also with split-K (B = 8192) — and so do the generic tile-list buckets
+    (CVAE_GENERIC_BUCKETS=1).  Host eps: every call draws the same noise."""
+    torch.manual_seed(0)
+    ref = cvae.ConditionalTrajectoryVAE(100, 6, 8)
+    engines = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("CVAE_GENERIC_BUCKETS", v)
+        m = cvae.ConditionalTrajectoryVAE(100, 6, 8)
+        m.load_state_dict(ref.state_dict())
+        engines.append(m.attach(dtype="bf16", max_batch=B, device="cuda:0"))
+    monkeypatch.delenv("CVAE_GENERIC_BUCKETS")
+    x = engines[0].as_input(torch.randn(B, 100, 6, generator=torch.Generator().manual_seed(5)))
+    eps = torch.randn(B, 8, generator=torch.Generator().manual_seed(6)).cuda()
+    e = engines[0]
+    e.forward_backward(x, eps=eps)  # CVAE_PART_ALL: one dW launch
+    torch.cuda.synchronize()
+    g_all, l_all = e.grads.clone(), e.loss.clone()
+    for eng in engines:
+        eng.grads.fill_(float("nan"))
+        eng.forward_backward(x, eps=eps, parts=3)  # chain + decoder bucket
+        eng.wgrad_rest(B)
+        torch.cuda.synchronize()
+        assert torch.equal(eng.grads, g_all)
+        assert torch.equal(eng.loss, l_all)
