@@ -1588,6 +1588,9 @@ int cvae_px_reset(cvae_handle* h, uint64_t base) {
 
 int cvae_tap_outputs(cvae_handle* h, float* recon, float* mu, float* logvar) {
   if (!h) return fail(CVAE_E_INVALID, "null handle");
+  if ((recon || mu || logvar) && !h->ring)
+    return fail(CVAE_E_INVALID, "cvae_tap_outputs: the outputs are tapped from the ring chain only "
+                                "(the reference architecture at S=100, D=6, bf16)");
   h->tap[0] = recon;
   h->tap[1] = mu;
   h->tap[2] = logvar;
