@@ -1234,7 +1234,7 @@ int cvae_adam(cvae_handle* h, float* params, const float* grads, float* m, float
   const int nt = (int)h->tiles.size();
   if ((rc = tmark(h, s, "adam"))) return rc;
   if (h->fast_nki == 19)
-    return klaunch(h, fchain::fastadam_kernel<19>, dim3(fchain::Tiles<19>::total()), dim3(WG_THREADS), 0, s,
+    return klaunch(h, fchain::fastadam_kernel<19>, dim3(fchain::Tiles<19>::total()), dim3(CVAE_THREADS), 0, s,
                    h->arena, params, m, v, grads, h->net.Bp, h->net.I, aa);
   if (is16(h))
     return klaunch(h, param_kernel<__bf16, PM_ADAM>, dim3(nt), dim3(CVAE_THREADS), 0, s, h->net,

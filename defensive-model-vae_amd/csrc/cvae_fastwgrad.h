@@ -208,10 +208,10 @@ __global__ __launch_bounds__(WG_THREADS) void fastwgrad_bucket_kernel(char* aren
 // Adam from the all-reduced gradient buffer (the RCCL data-parallel step's last launch,
 // cvae_adam): param_kernel's body over fastwgrad's tiles, the tile and layer record decoded from
 // blockIdx instead of read from the tile list and the NetDev kernel argument (two dependent round
-// trips before the first state load).  grid = Tiles::total(), WG_THREADS threads (2 weights each).
+// trips before the first state load).  grid = Tiles::total(), CVAE_THREADS threads.
 template <int NKI>
-__global__ __launch_bounds__(WG_THREADS) void fastadam_kernel(char* arena, float* params, float* mst, float* vst,
-                                                              const float* grads, int Bp, int I, AdamArgs a) {
+__global__ __launch_bounds__(CVAE_THREADS) void fastadam_kernel(char* arena, float* params, float* mst, float* vst,
+                                                                const float* grads, int Bp, int I, AdamArgs a) {
   __shared__ __attribute__((aligned(16))) float wt[32 * WT_LD];
   AdamArgs aa = a;
   aa.params = params;
@@ -221,7 +221,7 @@ __global__ __launch_bounds__(WG_THREADS) void fastadam_kernel(char* arena, float
   TileDesc td;
   LayerDev L;
   decode_tile<NKI>(blockIdx.x, arena, Bp, I, td, L);
-  param_body_n<__bf16, PM_ADAM, WG_THREADS>(L, td, aa, wt);
+  param_body<__bf16, PM_ADAM>(L, td, aa, wt);
 }
 
 // ---------------------------------------------------------------- data parallel: the peer exchange

@@ -661,33 +661,6 @@ __device__ __forceinline__ void param_body(const LayerDev& L, const TileDesc& td
   tile_epilogue<T, MODE, CVAE_THREADS, 4>(L, td.o0, td.i0, st, sb, g4, db, aa, wt);
 }
 
-// param_body over NTHR threads with EPT = 32·32 / NTHR weights each (the decoded Adam kernel runs
-// 512 threads, 2 weights each: half the epilogue arithmetic per thread, twice the loads in flight)
-template <typename T, int MODE, int NTHR>
-__device__ __forceinline__ void param_body_n(const LayerDev& L, const TileDesc& td, AdamArgs aa, float* wt) {
-  constexpr int EPT = 32 * 32 / NTHR, TPR = 32 / EPT;
-  static_assert(EPT == 2 || EPT == 4, "2 or 4 weights per thread");
-  using V = typename VecF<EPT>::T;
-  const int tid = threadIdx.x;
-  const adam_f32x2 t_step = MODE == PM_ADAM ? adam_step_load(aa) : adam_f32x2{0.f, 0.f};  // first: in-order vmcnt
-  const PreN<EPT> st = loadn<MODE, EPT>(L, td.o0 + tid / TPR, td.i0 + (tid % TPR) * EPT, aa);
-  PreB sb = {0.f, 0.f, 0.f, -1};
-  if (td.i0 == 0 && tid < 32) sb = loadb<MODE>(L, td.o0 + tid, aa);
-  V g = {};
-  float db = 0.f;
-  if (MODE == PM_ADAM) {
-#pragma unroll
-    for (int c = 0; c < EPT; ++c) g[c] = c < st.nv ? aa.grads[st.base + c * st.stride] * aa.grad_scale : 0.f;
-    const int ob = td.o0 + tid;
-    if (td.i0 == 0 && tid < 32 && ob < L.N && L.has_bias) {
-      const int seg = (L.nseg == 2 && ob >= L.seg_rows0) ? 1 : 0;
-      db = aa.grads[L.pb[seg] + (seg ? ob - L.seg_rows0 : ob)] * aa.grad_scale;
-    }
-    adam_resolve(aa, t_step);  // its first use: after every state load has been issued
-  }
-  tile_epilogue<T, MODE, NTHR, EPT>(L, td.o0, td.i0, st, sb, g, db, aa, wt);
-}
-
 template <typename T, int MODE>
 __global__ __launch_bounds__(CVAE_THREADS) void param_kernel(NetDev net, const TileDesc* __restrict__ tiles,
                                                              AdamArgs aa) {
