@@ -67,8 +67,6 @@ if os.environ.get("RING") == "1":  # the reference architecture on the ring chai
         names = (["pro:issue", "pro:transform", "pro:bar", "C0+copies", "E0 gemm", "E0 epi", "C1|E1", "E2", "E3",
                   "FC", "reparam", "D0", "D1", "D2", "D3+loss", "fixup", "D3b", "D2b", "D1b", "D0b", "FCb gemm",
                   "FCb epi", "E3b", "E2b", "E1b|C1b", "partials"])
-    if os.environ.get("CVAE_FUSE_RING", "0") != "0":  # the one-launch step: E1b|C1b ends at the drain stamp
-        names = names[:-2] + ["E1b|C1b+drain"]
 for i in range(k - 1):
     print(f"{names[i]:>14s} {i:2d}: median {np.median(d[:, i]) / 1000:7.3f} us   max {d[:, i].max() / 1000:7.3f} us"
           f"   block0 {d[0, i] / 1000:7.3f} us")
@@ -76,12 +74,20 @@ ends = (st[:, k - 1] - t0) * 10 / 1000
 starts = (st[:, 0] - t0) * 10 / 1000
 print(f"block ends (us after the first start): block0 {ends[0]:.2f}  median {np.median(ends):.2f}  max {ends.max():.2f}"
       f" (block {int(ends.argmax())});  block0 start {starts[0]:.2f}")
+# dispatch order: each block's start, in block order (8 per line: blockIdx % 8 is the XCD), and how
+# much of each block's end its start explains
+print("block starts (us):")
+for i in range(0, nb, 8):
+    print("  " + " ".join(f"{v:5.2f}" for v in starts[i:i + 8]))
+dur = ends - starts
+print(f"block durations: median {np.median(dur):.2f} max {dur.max():.2f} us; corr(start, end) "
+      f"{np.corrcoef(starts, ends)[0, 1]:.2f}")
 
 w = wbuf.view(NT, 8).cpu().numpy().astype(np.int64)
 wid = np.nonzero(w[:, 0] > 0)[0]  # fused launch: tile blocks follow the row-chain blocks
 w = w[wid]
 nw = len(wid)
-if len(wid) and (wid[0] > 0 or os.environ.get("CVAE_FUSE_RING", "0") != "0"):
+if len(wid) and wid[0] > 0:
     rel = lambda v: (v - t0) * 10 / 1000  # noqa: E731
     print(f"fused: chain blocks end {rel(st[:, k - 1].min()):.2f}..{rel(st[:, k - 1].max()):.2f} us after the first"
           f" chain stamp; tile work starts (pctl 0/25/50/75/100) "
