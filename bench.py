@@ -207,14 +207,118 @@ def cpu_baseline(B, S, D, Z, H, seconds, n_enc=4, n_dec=4, data=None, min_steps=
                       f"{sum(times) / len(times) * 1e3:.3f} mean, {threads} threads"}
 
 
+def launch_plan(gpus, env, device_count):
+    """What ``bench.py --gpus N`` does with the process it runs in (decided before any GPU call:
+    ``torch.cuda.device_count()`` does not initialise the GPU on this image).
+
+    Returns ("run", world) to measure in this process, ("spawn", N) to start N rank processes as
+    children of this one (``--gpus N`` without a launcher), or ("error", message).
+    - Under a launcher (``WORLD_SIZE`` set, e.g. ``torch.distributed.run --nproc-per-node N``) the
+      launcher's world is the world; ``--gpus`` must agree with it when given.
+    - Without one, N > 1 spawns N ranks (one per GPU), which needs N visible GPUs unless the ranks
+      rehearse on one GPU (``CVAE_BENCH_SHARE_GPU=1``)."""
+    share = env.get("CVAE_BENCH_SHARE_GPU") == "1"
+    if "WORLD_SIZE" in env:
+        try:
+            world = int(env["WORLD_SIZE"])
+        except ValueError:
+            return "error", f"WORLD_SIZE={env['WORLD_SIZE']!r} is not an integer"
+        if gpus is not None and gpus != world:
+            return "error", (f"--gpus {gpus} but the launcher started WORLD_SIZE={world} ranks: the line would "
+                             f"report n_gpus={world}; run with --gpus {world}, or without a launcher")
+        return "run", world
+    n = 1 if gpus is None else gpus
+    if n < 1:
+        return "error", f"--gpus {n}: need at least one GPU"
+    if n > 1 and not share and device_count < n:
+        return "error", (f"--gpus {n} but only {device_count} GPU(s) are visible (CVAE_BENCH_SHARE_GPU=1 runs the "
+                         f"ranks on GPU 0 as a rehearsal, not a scaling measurement)")
+    return ("spawn", n) if n > 1 else ("run", 1)
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_envs(n, env, port):
+    """The environment of each of the n rank processes: torch.distributed.run's variables for one
+    node (rendezvous on 127.0.0.1), everything else inherited (HSA_ENABLE_IPC_MODE_LEGACY=0 too)."""
+    out = []
+    for r in range(n):
+        e = dict(env)
+        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+                  "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+        out.append(e)
+    return out
+
+
+def run_ranks(cmd, envs, out, grace_s=60.0, poll_s=0.05):
+    """Start one child per environment running ``cmd``, forward rank 0's result line to ``out``, and
+    return the worst exit status (the first non-zero one in rank order among the ranks that ended by
+    themselves, else 0).  Rank 0's stdout is
+    read through a pipe (its other output and every other rank's stdout go to this process's
+    stderr); the line forwarded is the last one that parses as a JSON object with a "metric" key.
+    When a rank fails, the others get ``grace_s`` to finish (they may be blocked in a collective
+    with it) and are then killed — by their own PIDs."""
+    import subprocess
+    import threading
+    procs, lines = [], []
+    for r, e in enumerate(envs):
+        procs.append(subprocess.Popen(cmd, env=e, stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno()))
+
+    def pump():
+        for raw in procs[0].stdout:
+            s = raw.decode(errors="replace").rstrip("\n")
+            try:
+                d = json.loads(s)
+            except ValueError:
+                d = None
+            if isinstance(d, dict) and "metric" in d:
+                lines.append(s)
+            else:
+                print(s, file=sys.stderr, flush=True)
+    th = threading.Thread(target=pump, daemon=True)
+    th.start()
+    deadline, killed = None, set()
+    while None in [p.poll() for p in procs]:  # a list: every child polled each round
+        if deadline is None and any(p.returncode not in (None, 0) for p in procs):
+            deadline = time.monotonic() + grace_s
+        if deadline is not None and time.monotonic() > deadline:
+            for r, p in enumerate(procs):
+                if p.poll() is None:
+                    p.kill()
+                    killed.add(r)
+        time.sleep(poll_s)
+    th.join()
+    codes = [p.wait() for p in procs]
+    if lines:
+        print(lines[-1], file=out, flush=True)
+    # the ranks that failed by themselves first; the ones killed here only if nothing else failed
+    bad = [c for r, c in enumerate(codes) if c != 0 and r not in killed] or [c for c in codes if c != 0]
+    if not bad:
+        return 0
+    return bad[0] if bad[0] > 0 else 128 - bad[0]  # killed by signal s: the shell's 128 + s
+
+
+def spawn_main(n, argv):
+    """``bench.py --gpus N`` without a launcher: N rank processes, this one a plain parent that never
+    touches the GPU (no exec — the ranks are children).  The ranks run this same script with the
+    same arguments under torch.distributed.run's environment."""
+    cmd = [sys.executable, "-u", os.path.abspath(__file__)] + list(argv)
+    envs = rank_envs(n, os.environ, int(os.environ.get("MASTER_PORT") or _free_port()))
+    print(f"bench.py: starting {n} rank processes (master 127.0.0.1:{envs[0]['MASTER_PORT']})", file=sys.stderr,
+          flush=True)
+    return run_ranks(cmd, envs, sys.stdout)
+
+
 def main():
-    # ONE JSON line on stdout: native libraries (RCCL's version banner) write to fd 1 directly, so
-    # fd 1 becomes stderr for the whole run and the result goes to a duplicate of the original stdout
-    out = os.fdopen(os.dup(1), "w")
-    sys.stdout.flush()
-    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (one rank each); without a launcher N > 1 starts the N ranks as child processes; "
+                         "under torch.distributed.run it must equal WORLD_SIZE (default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (cfg2/wide: 1024, cfg1: 32)")
@@ -246,8 +350,19 @@ def main():
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="per-launch HBM traffic from rocprofv3 --pmc passes (scripts/pmc_traffic.py)")
     args = ap.parse_args()
+    what, arg = launch_plan(args.gpus, os.environ, torch.cuda.device_count())
+    if what == "error":
+        print(f"bench.py: {arg}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if what == "spawn":
+        sys.exit(spawn_main(arg, sys.argv[1:]))
+    # ONE JSON line on stdout: native libraries (RCCL's version banner) write to fd 1 directly, so
+    # fd 1 becomes stderr for the whole run and the result goes to a duplicate of the original stdout
+    out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = arg
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal of the N>1 path on a one-GPU box: every rank on GPU 0, gloo for the host-side

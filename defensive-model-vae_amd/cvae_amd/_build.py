@@ -5,6 +5,7 @@ to this file so it travels to the GPU box with the repo snapshot.
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -25,27 +26,57 @@ def _inputs():
     return files
 
 
+def _command(out):
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wno-unused-result", "-Wno-pass-failed", "-mllvm", "-amdgpu-mfma-vgpr-form",
+           "-mllvm", "-amdgpu-kernarg-preload-count=16", "-o", out]
+    cmd += os.environ.get("CVAE_EXTRA_FLAGS", "").split()  # diagnostic builds only (with CVAE_LIB)
+    return cmd + [os.path.join(CSRC, s) for s in SOURCES]
+
+
+def source_digest() -> str:
+    """sha256 over every input's bytes and the compile flags: what the library was built from.
+    Kept beside the library (``<lib>.sha256``) so a library is rebuilt when its sources differ,
+    whatever the files' timestamps say."""
+    h = hashlib.sha256()
+    for f in _inputs():
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    h.update(" ".join(_command("")[1:]).encode())
+    return h.hexdigest()
+
+
+def _stamp():
+    return LIB + ".sha256"
+
+
 def needs_build() -> bool:
-    if not os.path.exists(LIB):
+    if not os.path.exists(LIB) or not os.path.exists(_stamp()):
         return True
-    t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(f) > t for f in _inputs())
+    with open(_stamp()) as f:
+        return f.read().strip() != source_digest()
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile when the library is missing or was built from other sources (content digest);
+    with ``verbose`` say which (the hipcc command, or "up to date")."""
+    digest = source_digest()
     if not force and not needs_build():
+        if verbose:
+            print(f"cvae_amd: {LIB} up to date (sources sha256 {digest[:16]})", file=sys.stderr)
         return LIB
-    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     tmp = LIB + ".tmp"
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wno-unused-result", "-Wno-pass-failed", "-mllvm", "-amdgpu-mfma-vgpr-form",
-           "-mllvm", "-amdgpu-kernarg-preload-count=16", "-o", tmp]
-    cmd += os.environ.get("CVAE_EXTRA_FLAGS", "").split()  # diagnostic builds only (with CVAE_LIB)
-    cmd += [os.path.join(CSRC, s) for s in SOURCES]
+    cmd = _command(tmp)
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True, cwd=CSRC)
     os.replace(tmp, LIB)
+    with open(_stamp(), "w") as f:
+        f.write(digest + "\n")
+    if verbose:
+        print(f"cvae_amd: built {LIB} (sources sha256 {digest[:16]})", file=sys.stderr)
     return LIB
 
 

@@ -116,16 +116,19 @@ class DataParallelStep:
     def step(self, x, idx=None, eps=None, batch=None, global_batch=None, weights=None, row0=None, classes=None,
              sizes=None):
         """One data-parallel training step; ``batch`` = this rank's rows, ``global_batch`` = Σ over
-        ranks, ``row0`` = this rank's first row in the global batch (default: rank · batch);
-        ``sizes`` = every rank's rows (peer exchange; default: ``split_rows`` shares)."""
+        ranks, ``row0`` = this rank's first row in the global batch (default: the sum of the lower
+        ranks' ``sizes``, else this rank's ``split_rows`` share of ``global_batch`` — rank · batch
+        for equal shares); ``sizes`` = every rank's rows (peer exchange; default: ``split_rows``
+        shares)."""
         eng = self.engine
         if batch is None:
             batch = idx.numel() if idx is not None else x.shape[0]
         batch = int(batch)
         if global_batch is None:
             global_batch = batch * self.world_size
-        if row0 is None:
-            row0 = self.rank * batch if sizes is None else sum(sizes[:self.rank])
+        if row0 is None:  # ADVICE r04: rank · batch is wrong for ragged shares (7 rows over 2 ranks)
+            row0 = (split_rows(global_batch, self.world_size, self.rank)[0] if sizes is None
+                    else sum(sizes[:self.rank]))
         if self.px is not None:
             if classes is not None:
                 raise ValueError("the peer exchange serves the reference model (no class embedding)")

@@ -8,7 +8,6 @@ Tolerances: fp32 path vs oracle/goldens as test_hip_parity (losses rel <= 2e-5, 
 bit; device Adam scalars vs torch's Python doubles: bit for bit.
 """
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -174,10 +173,7 @@ def test_philox_training_step_keyed_by_global_row(cvae):
 
 
 # ---------------------------------------------------------------- data-parallel split step
-def _port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+from conftest import free_port as _port  # noqa: E402
 
 
 def test_dp_split_buckets_graph_rccl_equal_fused(cvae):

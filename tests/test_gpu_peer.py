@@ -12,7 +12,6 @@ produce.  Params, moments and device counters must equal it BIT FOR BIT; the los
 batch, and an empty share (world 3, a rank with no rows); the train loop over the exchange.
 """
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -23,21 +22,18 @@ pytestmark = pytest.mark.gpu
 S, D, Z = 100, 6, 8
 
 
-def _port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+from conftest import free_port as _port  # noqa: E402
 
 
 def _data(n):
     return torch.randn(n, S, D, generator=torch.Generator().manual_seed(21))
 
 
-def _model():
+def _model(max_batch=256):
     import cvae_amd
     torch.manual_seed(0)
     m = cvae_amd.ConditionalTrajectoryVAE(S, D, Z)
-    return m, m.attach(dtype="bf16", max_batch=256, device="cuda:0", seed=4321)
+    return m, m.attach(dtype="bf16", max_batch=max_batch, device="cuda:0", seed=4321)
 
 
 def _worker(rank, world, port, sizes, steps, out):
@@ -45,13 +41,13 @@ def _worker(rank, world, port, sizes, steps, out):
     from cvae_amd.dist import DataParallelStep
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     # ranks sharing one GPU are scheduled by the GPU's process scheduler, which can hold one
-    # rank's queue off the GPU for milliseconds to seconds: a longer bound than the 2 s default
-    # (one rank per GPU); a protocol deadlock still fails the test
+    # rank's queue off the GPU for milliseconds to seconds: a longer bound than the 10 s default
+    # (one rank per GPU, cvae_capi.hip px_timeout_ticks); a protocol deadlock still fails the test
     os.environ["CVAE_PX_TIMEOUT_MS"] = "30000"
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
-        m, eng = _model()
+        m, eng = _model(max(256, max(sizes)))
         gb = sum(sizes)
         lo = sum(sizes[:rank])
         x = eng.as_input(_data(gb)[lo:lo + max(sizes[rank], 1)])
@@ -71,7 +67,7 @@ def _worker(rank, world, port, sizes, steps, out):
         if rank == 0:
             torch.save({"params": eng.params.cpu(), "m": eng.m.cpu(), "v": eng.v.cpu(),
                         "counters": eng.counters.cpu(), "acc": acc.cpu(), "fault": fault, "verified": verified,
-                        "layout": layout}, out)
+                        "layout": layout, "waits": dp.px.stats()}, out)
         dp.close()
     finally:
         dist.destroy_process_group()
@@ -80,7 +76,7 @@ def _worker(rank, world, port, sizes, steps, out):
 def _reference(sizes, steps):
     """One process: per step, every rank's forward_backward at the step's Philox offset, partial
     gradients weighted (ragged) and summed in rank order, then Adam."""
-    m, eng = _model()
+    m, eng = _model(max(256, max(sizes)))
     gb = sum(sizes)
     world = len(sizes)
     xs = _data(gb)
@@ -117,8 +113,12 @@ def _reference(sizes, steps):
 # blocks each at k = 4, every block pushing its tiles before it waits on any it owns).
 # world 8: the driver's N = 8 ownership (tile t -> rank t mod 8) and flag epochs, 8 ranks on one GPU
 # (63 tile blocks each).
-@pytest.mark.parametrize("sizes", [(64, 64), (96, 32), (40, 24, 0), (64, 64, 64, 64), (32,) * 8],
-                         ids=["w2", "ragged", "empty-share", "w4", "w8"])
+# cfg3: BASELINE configs[2]'s workload, B_local = 1024 per rank (global 8192 at world 8; 2048 at
+# world 2): every rank's 64-block row chain plus its share of the exchange's tile blocks
+# (2 * CUs / 8 - 1 = 63, and the end block) fill the GPU's 512 workgroup slots exactly.
+@pytest.mark.parametrize("sizes", [(64, 64), (96, 32), (40, 24, 0), (64, 64, 64, 64), (32,) * 8,
+                                   (1024,) * 2, (1024,) * 8],
+                         ids=["w2", "ragged", "empty-share", "w4", "w8", "cfg3-w2", "cfg3-w8"])
 def test_peer_exchange_equals_split_step(sizes, tmp_path):
     """world ranks on one GPU through the in-kernel exchange == the split data-parallel step of
     the same partial gradients in one process, bit for bit, after 3 steps."""
@@ -137,6 +137,7 @@ def test_peer_exchange_equals_split_step(sizes, tmp_path):
             p.kill()
     assert codes == [0] * len(sizes), codes
     got = torch.load(out, weights_only=True)
+    print(f"sizes {sizes}: rank 0 owner waits {got['waits']}, layout {got['layout']}")
     assert got["fault"] == 0
     assert got["verified"] is True, got["verified"]
     k = len(sizes)  # every rank on this box's one GPU: 2 slots per CU shared by k ranks

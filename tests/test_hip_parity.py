@@ -997,12 +997,6 @@ def test_fp8_training_full_batch_cfg5(cvae):
 
 
 
-def _port(socket):
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 def test_rccl_allreduce_split_step_equals_fused(cvae):
     """The DP step's exchange on the real backend: fwd/bwd → RCCL all_reduce (the "nccl" backend,
     a world-1 group on this one-GPU box) → Adam, plus the epoch loss all_reduce, equals the fused
@@ -1010,10 +1004,10 @@ def test_rccl_allreduce_split_step_equals_fused(cvae):
     import os
     import torch.distributed as tdist
     from cvae_amd import dist as dp
-    import socket
+    from conftest import free_port
     assert not tdist.is_initialized()
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    tdist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_port(socket)}", rank=0,
+    tdist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{free_port()}", rank=0,
                              world_size=1, device_id=torch.device("cuda", 0))
     try:
         torch.manual_seed(0)
