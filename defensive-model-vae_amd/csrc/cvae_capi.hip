@@ -860,11 +860,16 @@ int chain_rows(const cvae_handle* h, const RowArgs& ra) {
 }
 
 // the training row chain (forward + loss + every dX): the specialised bf16 chain where it applies
+// tap_ok: the caller is cvae_train_fwd_bwd, the one entry point that consumes an armed parity tap
+// (cvae_tap_outputs); every other training call fails while one is armed, so a tap whose buffers a
+// caller freed is never written by a later step or by a captured graph
 template <typename T>
-int launch_train_chain(cvae_handle* h, RowArgs ra, hipStream_t s) {
+int launch_train_chain(cvae_handle* h, RowArgs ra, hipStream_t s, bool tap_ok = false) {
+  const bool tap = h->tap[0] || h->tap[1] || h->tap[2];
+  if (tap && !tap_ok)
+    return fail(CVAE_E_INVALID, "cvae_tap_outputs is armed: only cvae_train_fwd_bwd consumes it (disarm with NULLs)");
   int rc = tmark(h, s, "rowchain");
   if (rc) return rc;
-  const bool tap = h->tap[0] || h->tap[1] || h->tap[2];
   if (tap) {  // one-shot (cvae_tap_outputs): this launch only
     ra.recon_out = h->tap[0];
     ra.mu_out = h->tap[1];
@@ -1013,7 +1018,7 @@ int fwd_bwd_impl(cvae_handle* h, const CallX& c, float* grads, float* loss_out, 
   const RowArgs ra = row_args(h, c);
   int rc = CVAE_OK;
   if (parts & CVAE_PART_CHAIN)
-    rc = is16(h) ? launch_train_chain<__bf16>(h, ra, s) : launch_train_chain<float>(h, ra, s);
+    rc = is16(h) ? launch_train_chain<__bf16>(h, ra, s, true) : launch_train_chain<float>(h, ra, s, true);
   if (rc) return rc;
   AdamArgs aa{};
   aa.grads = grads;

@@ -299,8 +299,10 @@ int cvae_operand_checksum(cvae_handle* h, uint64_t* out, void* stream);
 /* Parity taps (tests): the NEXT training call's row chain also writes what its epilogues computed
  * at the training step's own rounding points — recon fp32 (batch,S,D) (the last decoder layer's
  * output, Training_VAE.py:215, before the loss), mu and logvar fp32 (batch,Z) (:195-196); any may be
- * NULL.  One-shot.  Served by the ring chain (CVAE_KERNEL_RING) only: on another handle this call
- * fails (CVAE_E_INVALID) unless every pointer is NULL. */
+ * NULL.  One-shot, and consumed by cvae_train_fwd_bwd only: while a tap is armed every other
+ * training call (cvae_train_step(s), the peer step, cvae_bench_kernels) fails with CVAE_E_INVALID
+ * and launches nothing; disarm it by passing NULLs.  Served by the ring chain (CVAE_KERNEL_RING)
+ * only: on another handle this call fails (CVAE_E_INVALID) unless every pointer is NULL. */
 int cvae_tap_outputs(cvae_handle* h, float* recon, float* mu, float* logvar);
 
 /* ---- Data parallelism over xGMI without a collective library (Training_VAE.py:362-363

@@ -15,6 +15,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef short i16x4 __attribute__((ext_vector_type(4)));
 typedef short i16x8 __attribute__((ext_vector_type(8)));
 #define G __attribute__((address_space(1)))
@@ -231,6 +232,99 @@ __global__ __launch_bounds__(64 * (8 + L)) void kC(const __bf16* W, __bf16* out,
   }
 }
 
+// ---- D<K>: the N-split chain (VERDICT r04 Next #6).  K co-XCD workgroups share one 16-row tile:
+// member m computes outputs [m·128/K, (m+1)·128/K) of every step with 8/K waves, so each streams 1/K
+// of the step's 32 KB of fragments, and the members exchange their activation slices through the
+// XCD's L2 after every step: sc1 (write-through) stores of the slice, every storing wave's
+// vmcnt(0), a barrier, one lane's agent-scope add to the tile's counter (MI355X_MICROARCH.md hand-off
+// table, first row), one lane's sc1 poll until all K members have added, a barrier, then sc1 loads
+// of the other members' slices into the LDS image.  Blocks 8·(K·(t/8) + m) + t%8 are tile t's
+// members: all on XCD t % 8.  MODE bit1: no arena stores (the chain's 4-KB store per step);
+// bit2: no exchange (the members run unsynchronised: the stream-only part of the price).
+// Every spin is bounded (err[0] counts give-ups), so every wave reaches the end.
+__device__ __forceinline__ bool spin_sc1(const unsigned* c, unsigned target, unsigned* err) {
+  for (unsigned it = 0; __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++it) {
+    __builtin_amdgcn_s_sleep(1);
+    if (it > (1u << 22)) {
+      atomicAdd(err, 1u);
+      return false;
+    }
+  }
+  return true;
+}
+template <int K, int MODE>
+__global__ __launch_bounds__(512) void kD(const __bf16* W, __bf16* out, int nstep, unsigned* ctr, __bf16* xch,
+                                          unsigned* err) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  auto img = [&](int i) { return (__bf16*)(smem + (i & 1) * 4096); };
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, n16 = lane & 15, q = lane >> 4;
+  const int b = blockIdx.x, x = b % 8, j = b / 8, m = j % K, t = (j / K) * 8 + x;
+  constexpr int WPM = 8 / K;           // computing waves per member
+  constexpr int SL = 128 / K;          // features per member slice
+  const bool comp = wave < WPM;
+  const int n = m * SL + wave * 16 + n16;  // this lane's output feature (computing waves)
+  if (tid < 512) ((u32x4*)smem)[tid] = u32x4{0, 0, 0, 0};
+  bf16x8 w[3][4];
+  auto wl = [&](bf16x8* wr, int s) {
+    const __bf16* p = W + (size_t)(s % NWSTEPS) * (WSTEP / 2) + ((size_t)(m * WPM + wave) * 4 * 64 + lane) * 8;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) wr[c] = *(const G bf16x8*)(p + c * 512);
+  };
+  if (comp) {
+    wl(w[0], 0);
+    wl(w[1], 1);
+  }
+  lbar();
+  unsigned* my = ctr + t * 64;  // one counter per tile, on a line of its own
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(xch, (short)0, 0x7fffffff, 0x00020000);
+  for (int s0 = 0; s0 < nstep; s0 += 3) {
+#pragma unroll
+    for (int bb = 0; bb < 3; ++bb) {
+      const int s = s0 + bb;
+      if (s >= nstep) break;
+      const __bf16* in = img(s);
+      __bf16* o = img(s + 1);
+      if (comp) {
+        bf16x8 xf[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) xf[c] = xfrag(in, c);
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[c], w[bb][c], acc, 0, 0, 0);
+        bf16x4 h;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) h[i] = (__bf16)fmaxf(acc[i] * 0.01f, 0.f);
+        *(bf16x4*)(o + n * 16 + 4 * q) = h;
+        if (!(MODE & 4))  // the slice to the other members: 8 B per lane, write-through (sc1 = aux 16)
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, h), xr,
+                                                (int)((((size_t)t * 2 + (s & 1)) * 2048 + n * 16 + 4 * q) * 2), 0, 16);
+        if (!(MODE & 2))  // the chain's arena copy of the step (its share of it)
+          *(G bf16x4*)(out + ((size_t)t * nstep + s) * 2048 + n * 16 + 4 * q) = h;
+        wl(w[(bb + 2) % 3], s + 2);
+        if (!(MODE & 4)) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // the slice stores (the 4 loads stay)
+      }
+      if (!(MODE & 4)) {
+        __syncthreads();
+        if (tid == 0) {
+          __hip_atomic_fetch_add(my, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          spin_sc1(my, (unsigned)K * (s + 1), err);
+        }
+        __syncthreads();
+        // the other members' slices: 16 rows × (128 − SL) features, 16-B sc1 loads into the image
+        const int pieces = (128 - SL) * 16 * 2 / 16;  // 16-B pieces
+        for (int e = tid; e < pieces; e += 512) {
+          const int fo = e / 2, half = e & 1;           // feature among the others, row half
+          const int f = fo < m * SL ? fo : fo + SL;     // skip this member's own slice
+          const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
+              xr, (int)((((size_t)t * 2 + (s & 1)) * 2048 + f * 16 + half * 8) * 2), 0, 16);  // sc1 load
+          *(u32x4*)((char*)o + (f * 16 + half * 8) * 2) = v;
+        }
+      }
+      lbar();
+    }
+  }
+}
+
 template <typename F>
 float timeit(F launch) {
   hipEvent_t a, b;
@@ -247,7 +341,8 @@ float timeit(F launch) {
   return ms * 1e6f / reps;  // ns per launch
 }
 
-int main() {
+int main(int argc, char** argv) {
+  const bool only_d = argc > 1 && argv[1][0] == 'D';
   __bf16 *W, *out;
   hipMalloc(&W, (size_t)WSTEP * NWSTEPS);
   hipMalloc(&out, (size_t)64 * 96 * 4096);
@@ -276,6 +371,32 @@ int main() {
   hipFuncSetAttribute((const void*)kC<3, 0, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 8192 + 3 * WSTEP + 64);
   hipFuncSetAttribute((const void*)kC<3, 0, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 8192 + 3 * WSTEP + 64);
   hipFuncSetAttribute((const void*)kC<3, 2, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 8192 + 3 * WSTEP + 64);
+  if (only_d) {
+    unsigned* ctr;
+    __bf16* xch;
+    hipMalloc(&ctr, 64 * 64 * 4);
+    hipMalloc(&xch, (size_t)64 * 2 * 4096);
+    auto d = [&](auto kern, int K) {
+      return [=](int s) {
+        hipMemsetAsync(ctr, 0, 64 * 64 * 4, 0);
+        hipLaunchKernelGGL(kern, dim3(64 * K), dim3(512), 8192, 0, W, out, s, ctr, xch, err);
+      };
+    };
+    per_step("A LA=2 (the chain's form)", [&](int s) { hipMemsetAsync(ctr, 0, 64 * 64 * 4, 0);
+                                              hipLaunchKernelGGL((kA<0, 3>), dim3(64), dim3(512), 8192, 0, W, out, s); });
+    per_step("D K=1 exchange", d(kD<1, 0>, 1));
+    per_step("D K=2 exchange", d(kD<2, 0>, 2));
+    per_step("D K=4 exchange", d(kD<4, 0>, 4));
+    per_step("D K=2 exchange no st", d(kD<2, 2>, 2));
+    per_step("D K=4 exchange no st", d(kD<4, 2>, 4));
+    per_step("D K=2 no exchange", d(kD<2, 4>, 2));
+    per_step("D K=4 no exchange", d(kD<4, 4>, 4));
+    per_step("D K=1 no exchange", d(kD<1, 4>, 1));
+    unsigned herr = 0;
+    hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost);
+    printf("spin time-outs: %u\n", herr);
+    return 0;
+  }
   for (int c = 0; c < 1; ++c) {
     cold = c == 1;
     per_step("C ring NS=2", [&](int s) { hipLaunchKernelGGL((kC<2, 0>), dim3(64), dim3(576), 8192 + 2 * WSTEP + 64, 0, W, out, s, err); });

@@ -291,6 +291,28 @@ def test_ring_chain_reconstruction_bf16_vs_oracle(cvae, B):
     np.testing.assert_allclose(loss, cvae_np.losses(re, c["rel"], mue, lve), rtol=2e-3, atol=1e-7)
 
 
+def test_armed_tap_is_consumed_by_fwd_bwd_only(cvae):
+    """cvae_tap_outputs: while a tap is armed, a training call other than
+    cvae_train_fwd_bwd fails and launches nothing (no write into buffers the caller may have freed);
+    disarming with NULLs restores training, and the weights did not move in between."""
+    import ctypes as C
+    from cvae_amd._lib import lib
+    ref, m, eng, x, eps = _cfg2(cvae, "bf16", 64)
+    assert eng.train_kernel == "ring"
+    x = x.to(torch.bfloat16).float()
+    buf = torch.empty(64, 8, device="cuda:0")
+    assert lib().cvae_tap_outputs(eng._h, None, C.c_void_p(buf.data_ptr()), None) == 0
+    p0 = eng.params.clone()
+    with pytest.raises(RuntimeError, match="armed"):
+        eng.train_step(x, eps=eps)
+    torch.cuda.synchronize()
+    assert torch.equal(eng.params, p0)
+    assert lib().cvae_tap_outputs(eng._h, None, None, None) == 0
+    eng.train_step(x, eps=eps)
+    torch.cuda.synchronize()
+    assert not torch.equal(eng.params, p0)
+
+
 def test_bf16_training_decreases_loss_full_size(cvae):
     """Size-independent property at the bench shape (B=1024, S=100, D=6): finite, decreasing ELBO."""
     torch.manual_seed(0)
