@@ -102,6 +102,7 @@ struct cvae_handle {
   bool fast_buckets = false;  // the two dW buckets run fchain::fastwgrad_bucket_kernel
   bool wide = false;        // bf16 training at BASELINE cfg5's shape runs wchain::widechain_kernel<Cfg5>
   bool wide_dw = false;     // ... and its dW ⊕ Adam runs wchain::widewgrad_kernel (compile-time tile decode)
+  bool wide_mx = false;     // CVAE_FP8 at that shape: the large dX GEMMs e4m3 + MX scales (Cfg5F8), else bf16 (Cfg5F8B)
   int wide_lds = 0;
   bool ring = false;        // the fast configuration's training chain runs wchain::widechain_kernel<Cfg2>
   bool ring_cls = false;    // cfg4 (class embedding) at cfg2's shape: widechain_kernel<Cfg4>, generic dW
@@ -121,6 +122,18 @@ namespace {
 int rup_i(int v, int a) { return (v + a - 1) / a * a; }
 // 16-bit activation/arena types: bf16, and CVAE_FP8 (bf16 activations, e4m3 forward operands)
 inline bool is16(const cvae_handle* h) { return h->cfg.dtype != CVAE_F32; }
+
+// The wide chain's e4m3 dX GEMMs (wchain::Cfg5F8): CVAE_FP8 at exactly BASELINE cfg5's shape, the
+// specialised kernels allowed, and not CVAE_FP8_DX=bf16 (the bf16-dX fallback, wchain::Cfg5F8B).
+// Only such a handle reserves and writes the e4m3 Wᵀ copies (LayerDev::f8b) — ADVICE r04.
+bool wide_fp8_mx(const cvae_config& c) {
+  using A = wchain::Cfg5F8;
+  const char* gen = std::getenv("CVAE_GENERIC");
+  const char* dx = std::getenv("CVAE_FP8_DX");
+  return c.dtype == CVAE_FP8 && !(gen && gen[0] == '1') && !(dx && std::strcmp(dx, "bf16") == 0) &&
+         c.n_classes == 0 && c.hidden_dim == wchain::H && c.seq_len == A::S && c.dim == A::D &&
+         c.latent_dim == A::Z && c.n_enc == A::NE && c.n_dec == A::ND;
+}
 
 int build_plan(cvae_handle* h) {
   const cvae_config& c = h->cfg;
@@ -170,7 +183,8 @@ int build_plan(cvae_handle* h) {
     L.f8 = c.dtype == CVAE_FP8 && L.Kp % 64 == 0;  // fp8 forward GEMM where K pairs up (cvae_device.h)
     // e4m3 copy of Wᵀ for the wide chain's MX dX GEMMs (wchain::Arch::f8b): the backward K pairs up,
     // the layer has a dX, and it is one of the large ones
-    L.f8b = L.f8 && L.Np % 64 == 0 && l != lC0(n) && l != lE(n, 0) && (L.Np >= 512 || L.Kp >= 512) ? 1 : 0;
+    L.f8b = wide_fp8_mx(c) && L.f8 && L.Np % 64 == 0 && l != lC0(n) && l != lE(n, 0) && (L.Np >= 512 || L.Kp >= 512)
+                ? 1 : 0;
     L.has_bias = 1;
     L.wt = 0;
     if (n.n_cls && l == lCE(n)) {  // nn.Embedding(n_classes, class_dim).weight: [K][N], no bias
@@ -788,7 +802,8 @@ int plan_wide_as(cvae_handle* h) {
   return CVAE_OK;
 }
 
-// bf16 runs wchain::Cfg5, CVAE_FP8 wchain::Cfg5F8 (e4m3 forward GEMMs)
+// bf16 runs wchain::Cfg5, CVAE_FP8 wchain::Cfg5F8 (e4m3 forward GEMMs and MX dX GEMMs) or, with
+// CVAE_FP8_DX=bf16, wchain::Cfg5F8B (e4m3 forward, bf16 dX)
 int plan_wide(cvae_handle* h) {
   using A = wchain::Cfg5;
   const cvae_config& c = h->cfg;
@@ -798,7 +813,9 @@ int plan_wide(cvae_handle* h) {
       c.hidden_dim != wchain::H || c.seq_len != A::S || c.dim != A::D || c.latent_dim != A::Z || c.n_enc != A::NE ||
       c.n_dec != A::ND)
     return CVAE_OK;
-  return c.dtype == CVAE_FP8 ? plan_wide_as<wchain::Cfg5F8>(h) : plan_wide_as<A>(h);
+  if (c.dtype != CVAE_FP8) return plan_wide_as<A>(h);
+  h->wide_mx = wide_fp8_mx(c);
+  return h->wide_mx ? plan_wide_as<wchain::Cfg5F8>(h) : plan_wide_as<wchain::Cfg5F8B>(h);
 }
 
 // What every training / inference call hands the row chain.
@@ -905,8 +922,11 @@ int launch_train_chain(cvae_handle* h, RowArgs ra, hipStream_t s, bool tap_ok = 
   if (std::is_same<T, __bf16>::value && wide_ok(h, ra)) {
     ra.stamps = h->d_stamps;
     const int grid = rup_i(ra.batch, 32) / wchain::R;
-    if (h->cfg.dtype == CVAE_FP8)
+    if (h->cfg.dtype == CVAE_FP8 && h->wide_mx)
       return klaunch(h, wchain::widechain_kernel<wchain::Cfg5F8>, dim3(grid), dim3(wchain::NT), h->wide_lds, s,
+                     h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra.ctr, ra);
+    if (h->cfg.dtype == CVAE_FP8)
+      return klaunch(h, wchain::widechain_kernel<wchain::Cfg5F8B>, dim3(grid), dim3(wchain::NT), h->wide_lds, s,
                      h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra.ctr, ra);
     return klaunch(h, wchain::widechain_kernel<wchain::Cfg5>, dim3(grid), dim3(wchain::NT), h->wide_lds, s,
                    h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra.ctr, ra);
@@ -963,8 +983,11 @@ int launch_wgrad(cvae_handle* h, int batch, const AdamArgs& aa, const LossArgs& 
     sk.pw = 32 * 64 + 32;
     const int g = wchain::WTiles<wchain::Cfg5>::total() * sk.S + 1;
     static_assert(wchain::WTiles<wchain::Cfg5>::total() == wchain::WTiles<wchain::Cfg5F8>::total(), "tile lists");
-    if (h->cfg.dtype == CVAE_FP8)
+    if (h->cfg.dtype == CVAE_FP8 && h->wide_mx)
       return klaunch(h, wchain::widewgrad_kernel<wchain::Cfg5F8, MODE>, dim3(g), dim3(WG_THREADS), 0, s, h->arena,
+                     aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), aa, la, sk);
+    if (h->cfg.dtype == CVAE_FP8)
+      return klaunch(h, wchain::widewgrad_kernel<wchain::Cfg5F8B, MODE>, dim3(g), dim3(WG_THREADS), 0, s, h->arena,
                      aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), aa, la, sk);
     return klaunch(h, wchain::widewgrad_kernel<wchain::Cfg5, MODE>, dim3(g), dim3(WG_THREADS), 0, s, h->arena,
                    aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), aa, la, sk);
@@ -1416,6 +1439,21 @@ int cvae_px_export(cvae_handle* h, int world, int rank, void* blob) {
   return CVAE_OK;
 }
 
+// Workgroups of the exchange's launches one CU holds at once, from the compiled kernels' resources
+// (the residency precondition of cvae_peer.h was a constant): the minimum of what the
+// occupancy calculator gives the row chain (its dynamic LDS) and both px_wgrad forms, capped at
+// PX_SLOTS_PER_CU.  Falls below 2 only if a kernel's VGPRs or LDS grow past the two-per-CU budget.
+int px_slots_per_cu(const cvae_handle* h, int* out) {
+  int a = 0, b = 0, c = 0;
+  HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, (const void*)wchain::widechain_kernel<wchain::Cfg2>,
+                                                     wchain::NT, h->ring_lds));
+  HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, (const void*)fchain::px_wgrad_kernel<19, true>,
+                                                     WG_THREADS, 0));
+  HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&c, (const void*)fchain::px_wgrad_kernel<19>, WG_THREADS, 0));
+  *out = std::min(PX_SLOTS_PER_CU, std::min(a, std::min(b, c)));
+  return CVAE_OK;
+}
+
 int cvae_px_import(cvae_handle* h, const void* blobs, uint64_t base) {
   if (!h || !blobs || !h->px_mbox) return fail(CVAE_E_INVALID, "peer exchange: export first");
   const PxBlob* b = (const PxBlob*)blobs;
@@ -1430,8 +1468,15 @@ int cvae_px_import(cvae_handle* h, const void* blobs, uint64_t base) {
   int share = 0;
   for (int r = 0; r < h->px_world; ++r)
     share += b[r].pci_domain == me.pci_domain && b[r].pci_bus == me.pci_bus && b[r].pci_device == me.pci_device;
-  const int slots = PX_SLOTS_PER_CU * me.cus / std::max(share, 1);
+  int per_cu = 0;
+  if (int rc = px_slots_per_cu(h, &per_cu)) return rc;
   const int nt = px_tiles(h);
+  // one rank per GPU: the launch's nt tile blocks + the end block must all be resident at once
+  if (per_cu * me.cus < nt + 1)
+    return fail(CVAE_E_INVALID, "peer exchange: the kernels fit " + std::to_string(per_cu) +
+                                    " workgroup(s) per CU, the exchange launch needs " + std::to_string(nt + 1) +
+                                    " resident workgroups on " + std::to_string(me.cus) + " CUs");
+  const int slots = per_cu * me.cus / std::max(share, 1);
   if (share > 1 && me.chain_blocks > slots)
     return fail(CVAE_E_INVALID, "peer exchange: " + std::to_string(share) + " ranks share one GPU; each may hold " +
                                     std::to_string(slots) + " resident workgroups, its row chain needs " +

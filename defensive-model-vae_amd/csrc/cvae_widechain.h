@@ -58,10 +58,12 @@ __device__ __forceinline__ void sfor(F&& f) {
 // concatenations, [h_traj ‖ h_c ‖ e] and [z ‖ h_c ‖ e]; the table is the last layer (LCE, one-hot
 // input, no bias, no activation).  Its padded dims do not depend on class_dim within that bound, so
 // one instantiation serves every class_dim the host accepts (plan_ring_cls).
-template <int S_, int D_, int Z_, int NE_, int ND_, bool F8_ = false, bool CLS_ = false>
+// MXB_ (with F8_): the large dX GEMMs in e4m3 with MX block scales (f8b below); false keeps every
+// backward GEMM bf16 — the creation-time fallback CVAE_FP8_DX=bf16 (cvae_capi.hip build_plan).
+template <int S_, int D_, int Z_, int NE_, int ND_, bool F8_ = false, bool CLS_ = false, bool MXB_ = F8_>
 struct Arch {
   static constexpr int S = S_, D = D_, Z = Z_, NE = NE_, ND = ND_, I = S_ * D_;
-  static constexpr bool F8 = F8_, CLS = CLS_;
+  static constexpr bool F8 = F8_, CLS = CLS_, MXB = MXB_ && F8_;
   static constexpr int CLS_EMAX = 24, CLS_NMAX = 32;
   static constexpr int NKI = (I + 31) / 32, Ip = 32 * NKI;
   static constexpr int NL = 3 + NE + ND + (CLS_ ? 1 : 0), ZH = Z + H;
@@ -96,7 +98,7 @@ struct Arch {
   // e4m3 forward operand, backward K (= Np) pairing up, a dX at all (not C0 / E0), and large enough
   // for the halved stream to matter — at cfg5 the last decoder layer, decoder L0 and fc
   static constexpr bool f8b(int l) {
-    return f8(l) && Np(l) % 64 == 0 && l != LC0 && l != LE0 && (Np(l) >= 512 || Kp(l) >= 512);
+    return MXB && f8(l) && Np(l) % 64 == 0 && l != LC0 && l != LE0 && (Np(l) >= 512 || Kp(l) >= 512);
   }
   // the arena as alloc_arena (cvae_capi.hip) lays it out, bf16 operands: byte offsets from its base;
   // an e4m3 layer's Wf region starts with its 256-B F8Scale header
@@ -1385,8 +1387,10 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
 using Cfg5 = Arch<200, 6, 512, 8, 8>;
 // BASELINE cfg2 / the reference architecture: S=100, D=6, latent 8, 4 + 4 layers
 using Cfg2 = Arch<100, 6, 8, 4, 4>;
-// BASELINE cfg5 in the CVAE_FP8 form (e4m3 forward GEMMs)
+// BASELINE cfg5 in the CVAE_FP8 form (e4m3 forward GEMMs; the large dX GEMMs e4m3 with MX scales)
 using Cfg5F8 = Arch<200, 6, 512, 8, 8, true>;
+// ... with every dX GEMM bf16 (CVAE_FP8_DX=bf16 at creation: the accuracy fallback and its A/B)
+using Cfg5F8B = Arch<200, 6, 512, 8, 8, true, false, false>;
 // BASELINE cfg4: the reference architecture at cfg2's shape with the scenario-class embedding
 using Cfg4 = Arch<100, 6, 8, 4, 4, false, true>;
 #ifndef CVAE_WIDE_RING

@@ -911,6 +911,27 @@ def test_bf16_200_step_loss_curve_vs_fp32_oracle(cvae):
 # the distance to the fp32 reference is printed (a measured deviation, not a parity claim).
 FP8_SHAPES = {"cfg2": dict(S=100, D=6, Z=8, n_enc=4, n_dec=4), "cfg5": WIDE}
 
+# Gradient rel-L2 bounds of the fp8 paths against the CPU emulation of their rounding points,
+# (max over tensors, median over tensors, max over every tensor but decoder.0.weight): about 2x the
+# maxima measured on the MI355X (round 4, profiles/r04y; printed by every run).  An emulation of
+# e4m3 rounding points is not bit-exact — the kernels accumulate in another order, and an element
+# whose pre-rounding value lands on the other side of a rounding boundary moves by one e4m3 ulp
+# (6 %) — so these bounds sit above bf16's 3e-2 where the flips compound:
+#   cfg2 (generic fp8 interpreter, bf16 backward): max 0.009, median 0.0022;
+#   cfg5 wide chain (MX dX): max 0.0512-0.0564 — decoder.0.weight every time, the end of the longest
+#   chain of e4m3 rounding points (16 e4m3 forward layers, the MX D7ᵀ, six bf16 dX, the MX D0ᵀ
+#   input) — every other tensor <= 0.0148, median 0.0019-0.0041.
+FP8_EMU_BOUNDS = {"cfg2": (2e-2, 5e-3, 2e-2), "cfg5": (1e-1, 1e-2, 3e-2)}
+
+
+def _fp8_bounds(errs, what, bounds):
+    mx, med, rest = bounds
+    vals = list(errs.values())
+    others = [v for k, v in errs.items() if k != "decoder.0.weight"]
+    print(f"{what}: max {max(vals):.4f} ({max(errs, key=errs.get)}), median {np.median(vals):.4f}, "
+          f"max without decoder.0.weight {max(others):.4f}")
+    assert max(vals) < mx and np.median(vals) < med and max(others) < rest, errs
+
 
 @pytest.mark.parametrize("shape", ["cfg2", "cfg5"])
 def test_fp8_matches_fp8_emulation(cvae, shape):
@@ -941,7 +962,7 @@ def test_fp8_matches_fp8_emulation(cvae, shape):
     g = _grads(m, eng)
     errs = {k: rel_l2(g[k], gw[k]) for k in cvae_np.param_keys(ne, nd)}
     print(f"fp8 {shape}: grad rel-L2 vs emulation", {k: round(v, 4) for k, v in errs.items()})
-    assert max(errs.values()) < 1e-1 and np.median(list(errs.values())) < 2e-2, errs
+    _fp8_bounds(errs, f"fp8 {shape} vs emulation", FP8_EMU_BOUNDS[shape])
     want32, _ = _oracle_grads(ref, x, eps)
     dev = np.abs(loss - want32) / np.abs(want32)
     print(f"fp8 {shape}: loss rel deviation from the fp32 reference {dev}")
@@ -977,7 +998,9 @@ def test_wide_fp8_chain_matches_generic_fp8(cvae, monkeypatch, B):
     gw, gg = _grads(m, eng), _grads(m2, e2)
     errs = {k: rel_l2(gw[k], gg[k]) for k in gw}
     print(f"wide fp8 chain B={B}: grad rel-L2 vs the generic bf16 backward", {k: round(v, 4) for k, v in errs.items()})
-    assert max(errs.values()) < 0.2 and np.median(list(errs.values())) < 0.1, errs
+    # the MX dX GEMMs against a bf16 backward: measured max 0.0424-0.0466 (decoder.0.bias), median 0.020
+    print(f"  max {max(errs.values()):.4f}, median {np.median(list(errs.values())):.4f}")
+    assert max(errs.values()) < 0.1 and np.median(list(errs.values())) < 0.04, errs
     p = {k: v.numpy() for k, v in ref.state_dict().items()}
     ne, nd = WIDE["n_enc"], WIDE["n_dec"]
     f8 = cvae_np.fp8_layers(p, WIDE["S"], WIDE["D"], WIDE["Z"], 128, ne, nd)
@@ -988,11 +1011,75 @@ def test_wide_fp8_chain_matches_generic_fp8(cvae, monkeypatch, B):
     ge = cvae_np.backward(p, cc, r, mu, lv, n_enc=ne, n_dec=nd, f8b=f8b)
     errs = {k: rel_l2(gw[k], ge[k]) for k in cvae_np.param_keys(ne, nd)}
     print(f"wide fp8 chain B={B}: grad rel-L2 vs emulation", {k: round(v, 4) for k, v in errs.items()})
-    assert max(errs.values()) < 1e-1 and np.median(list(errs.values())) < 2e-2, errs
+    _fp8_bounds(errs, f"wide fp8 chain B={B} vs emulation", FP8_EMU_BOUNDS["cfg5"])
     gb = cvae_np.backward(p, cc, r, mu, lv, n_enc=ne, n_dec=nd)  # the same forward, a bf16 backward
     dev = {k: rel_l2(ge[k], gb[k]) for k in cvae_np.param_keys(ne, nd)}
     print(f"  emulation: MX e4m3 dX vs bf16 dX, grad rel-L2 median {np.median(list(dev.values())):.4f} "
           f"max {max(dev.values()):.4f}")
+    # what the MX dX GEMMs cost in accuracy, on the CPU: measured median 0.0196-0.0199,
+    # max 0.0423-0.0470 (profiles/r04y)
+    assert max(dev.values()) < 0.1 and np.median(list(dev.values())) < 0.04, dev
+
+
+@pytest.mark.parametrize("B", [37, 200])
+def test_wide_fp8_bf16_dx_fallback(cvae, monkeypatch, B):
+    """CVAE_FP8_DX=bf16 at creation: the wide chain keeps its e4m3 forward GEMMs and
+    runs every dX GEMM in bf16 (wchain::Cfg5F8B, no e4m3 Wᵀ copies) — the rounding points of the
+    generic interpreter's fp8 path.  Against it: losses rtol 5e-3, gradients rel-L2 < 3e-2 (the
+    bf16 wide chain's bound against its emulation); against the CPU emulation without MX dX, the
+    bounds of the fp8 emulation tests."""
+    monkeypatch.setenv("CVAE_FP8_DX", "bf16")
+    ref, m, eng, x, eps = _wide(cvae, "fp8", B)
+    monkeypatch.setenv("CVAE_GENERIC", "1")
+    m2 = cvae.ConditionalTrajectoryVAE(WIDE["S"], WIDE["D"], WIDE["Z"], 128, WIDE["n_enc"], WIDE["n_dec"])
+    m2.load_state_dict(ref.state_dict())
+    e2 = m2.attach(dtype="fp8", max_batch=max(B, 32), device="cuda:0")
+    monkeypatch.delenv("CVAE_GENERIC")
+    monkeypatch.delenv("CVAE_FP8_DX")
+    assert eng.train_kernel == "wide" and e2.train_kernel == "generic"
+    x = x.to(torch.bfloat16).float()
+    lw = eng.forward_backward(x, eps=eps).cpu().numpy()
+    lg = e2.forward_backward(x, eps=eps).cpu().numpy()
+    np.testing.assert_allclose(lw, lg, rtol=5e-3, atol=1e-6)
+    gw, gg = _grads(m, eng), _grads(m2, e2)
+    errs = {k: rel_l2(gw[k], gg[k]) for k in gw}
+    print(f"wide fp8 chain, bf16 dX, B={B}: grad rel-L2 vs the generic fp8 path: max {max(errs.values()):.4f} "
+          f"({max(errs, key=errs.get)}), median {np.median(list(errs.values())):.4f}")
+    assert max(errs.values()) < 3e-2, errs
+    p = {k: v.numpy() for k, v in ref.state_dict().items()}
+    ne, nd = WIDE["n_enc"], WIDE["n_dec"]
+    f8 = cvae_np.fp8_layers(p, WIDE["S"], WIDE["D"], WIDE["Z"], 128, ne, nd)
+    r, mu, lv, hc, cc = cvae_np.forward(p, x.numpy(), eps.numpy(), n_enc=ne, n_dec=nd, q=cvae_np.bf16, f8=f8)
+    ge = cvae_np.backward(p, cc, r, mu, lv, n_enc=ne, n_dec=nd)
+    errs = {k: rel_l2(gw[k], ge[k]) for k in cvae_np.param_keys(ne, nd)}
+    _fp8_bounds(errs, f"wide fp8 chain, bf16 dX, B={B} vs emulation", FP8_EMU_BOUNDS["cfg5"])
+
+
+def test_fp8_mx_dx_loss_trajectory_vs_bf16_dx(cvae, monkeypatch):
+    """What the MX e4m3 dX GEMMs cost a training run: 40 steps of the cfg5 fp8 step
+    (B=256, Philox eps, one seeded batch pool) with MX dX against the same run with bf16 dX
+    (CVAE_FP8_DX=bf16), same init and batches: the loss curves (10-step means of the total ELBO)
+    within 2 %, every step within 5 %; both runs train.  Deviations printed."""
+    B, pool = 256, 1024
+    xs = torch.randn(pool, WIDE["S"], WIDE["D"], generator=torch.Generator().manual_seed(5)).cuda()
+    gen = torch.Generator().manual_seed(6)
+    idxs = [torch.randint(0, pool, (B,), generator=gen).cuda() for _ in range(40)]
+    curves = {}
+    for form in ("mx", "bf16"):
+        if form == "bf16":
+            monkeypatch.setenv("CVAE_FP8_DX", "bf16")
+        ref, m, eng, _, _ = _wide(cvae, "fp8", B)
+        monkeypatch.delenv("CVAE_FP8_DX", raising=False)
+        xin = eng.as_input(xs)
+        curves[form] = np.array([eng.train_step(xin, idx=i).cpu().numpy()[0] for i in idxs])
+    a, b = curves["mx"], curves["bf16"]
+    sm = lambda v: v.reshape(4, 10).mean(1)  # noqa: E731
+    print(f"cfg5 fp8 40 steps: MX dX {a[0]:.5f} -> {a[-1]:.5f}, bf16 dX {b[0]:.5f} -> {b[-1]:.5f}; "
+          f"max step rel dev {np.max(np.abs(a - b) / np.abs(b)):.4f}, "
+          f"10-step means rel dev {np.max(np.abs(sm(a) - sm(b)) / np.abs(sm(b))):.4f}")
+    assert np.isfinite(a).all() and a[-10:].mean() < a[:10].mean() and b[-10:].mean() < b[:10].mean()
+    np.testing.assert_allclose(sm(a), sm(b), rtol=2e-2)
+    np.testing.assert_allclose(a, b, rtol=5e-2)
 
 
 def test_fp8_training_full_batch_cfg5(cvae):
