@@ -103,6 +103,7 @@ struct cvae_handle {
   bool wide = false;        // bf16 training at BASELINE cfg5's shape runs wchain::widechain_kernel<Cfg5>
   bool wide_dw = false;     // ... and its dW ⊕ Adam runs wchain::widewgrad_kernel (compile-time tile decode)
   bool wide_mx = false;     // CVAE_FP8 at that shape: the large dX GEMMs e4m3 + MX scales (Cfg5F8), else bf16 (Cfg5F8B)
+  bool wide_mxw = false;    // ... and (CVAE_FP8_DW=mx) its dW GEMMs e4m3 + MX scales along the batch
   int wide_lds = 0;
   bool ring = false;        // the fast configuration's training chain runs wchain::widechain_kernel<Cfg2>
   bool ring_cls = false;    // cfg4 (class embedding) at cfg2's shape: widechain_kernel<Cfg4>, generic dW
@@ -799,6 +800,9 @@ int plan_wide_as(cvae_handle* h) {
   h->wide_lds = A::L_TOTAL;
   const char* g = std::getenv("CVAE_GENERIC_DW");  // "1": the generic tile-list dW kernel (A/B)
   h->wide_dw = !(g && g[0] == '1') && wide_dw_matches<A>(h);
+  // the MX dW (measured slower than the bf16 dW at B = 1024, DESIGN §4.5: an option, not the default)
+  const char* mw = std::getenv("CVAE_FP8_DW");
+  h->wide_mxw = std::is_same<A, wchain::Cfg5F8>::value && h->wide_dw && mw && std::strcmp(mw, "mx") == 0;
   return CVAE_OK;
 }
 
@@ -983,6 +987,9 @@ int launch_wgrad(cvae_handle* h, int batch, const AdamArgs& aa, const LossArgs& 
     sk.pw = 32 * 64 + 32;
     const int g = wchain::WTiles<wchain::Cfg5>::total() * sk.S + 1;
     static_assert(wchain::WTiles<wchain::Cfg5>::total() == wchain::WTiles<wchain::Cfg5F8>::total(), "tile lists");
+    if (h->cfg.dtype == CVAE_FP8 && h->wide_mxw && batch % 128 == 0)  // the MX dW: 128-row chunks
+      return klaunch(h, wchain::widewgrad_kernel<wchain::Cfg5F8, MODE, true>, dim3(g), dim3(WG_THREADS), 0, s,
+                     h->arena, aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), aa, la, sk);
     if (h->cfg.dtype == CVAE_FP8 && h->wide_mx)
       return klaunch(h, wchain::widewgrad_kernel<wchain::Cfg5F8, MODE>, dim3(g), dim3(WG_THREADS), 0, s, h->arena,
                      aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), aa, la, sk);

@@ -144,10 +144,20 @@ __host__ __device__ inline size_t f8_wf_off(int n, int kc, int Kp) {  // byte of
 __device__ __forceinline__ const F8Scale* f8_header(const void* Wf) {
   return (const F8Scale*)((const char*)Wf - sizeof(F8Scale));
 }
+// ---- MX (block-scaled e4m3) operands of v_mfma_scale_f32_16x16x128_f8f6f4 (the wide chain's dX
+// GEMMs, cvae_widechain.h gemm_mxb; the MX dW, cvae_wgrad.h mx_dw_chunk).  A lane's 32 bytes are
+// four 8-byte quarters h; the instruction's MX block b of row r is quarters 2(b >> 1), 2(b >> 1) + 1
+// of the lanes r + 16j with j >> 1 == b & 1 (mapped on the GPU: scripts/ubench/mxscale.hip), and its
+// E8M0 scale comes from lane r + 16b.
+typedef long l2 __attribute__((ext_vector_type(2)));
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+// saturation to ±448 before an e4m3 conversion: one v_med3_f32 (fminf(fmaxf(..)) compiled to a
+// canonicalizing v_max_f32 plus the same med3: two VALU per value; equal for every non-NaN input)
+__device__ __forceinline__ float f8_sat(float x) { return __builtin_amdgcn_fmed3f(x, -F8_MAX, F8_MAX); }
 // 8 values → 8 e4m3 bytes (RNE, saturated to ±448), element e in byte e
 __device__ __forceinline__ long f8x8(const float (&v)[8]) {
   int w0 = 0, w1 = 0;
-  auto c = [](float x) { return fminf(fmaxf(x, -F8_MAX), F8_MAX); };
+  auto c = [](float x) { return f8_sat(x); };
   w0 = __builtin_amdgcn_cvt_pk_fp8_f32(c(v[0]), c(v[1]), w0, false);
   w0 = __builtin_amdgcn_cvt_pk_fp8_f32(c(v[2]), c(v[3]), w0, true);
   w1 = __builtin_amdgcn_cvt_pk_fp8_f32(c(v[4]), c(v[5]), w1, false);
@@ -316,3 +326,56 @@ __device__ __forceinline__ float wave_sum(float v) {
   return (rd(v, 0) + rd(v, 16)) + (rd(v, 32) + rd(v, 48));
 }
 #undef CVAE_DPP_ADD
+
+// k of a block whose max has biased exponent e: 2^k puts the max in [128, 256); 0 for an all-zero block
+__device__ __forceinline__ int mx_k(int e) { return e > 0 ? min(134 - e, 126) : 0; }
+// The lane's four quarters of 8 values (the wide chain's dX: gradient chunks in frag_k order; the MX
+// dW: 8 batch rows of one feature) → e4m3 bytes of 2^k·g, k of the quarter's block; returns the two block exponents of the lane's pair (halves 0, 1 as two u16).  The
+// maxima are taken on the bf16 bit patterns (|x| = bits & 0x7fff orders like the values; the bf16
+// exponent field is fp32's), the pair's in one permlane16 swap (lanes L, L ^ 16), no LDS round trip.
+__device__ __forceinline__ unsigned mx_block(const bf16x8 (&c)[4], l2& x0, l2& x1) {
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  unsigned eb[2];
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    u16x2 m = {0, 0};
+#pragma unroll
+    for (int i = 2 * hh; i < 2 * hh + 2; ++i) {
+      const u32x4 w = __builtin_bit_cast(u32x4, c[i]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) m = __builtin_elementwise_max(m, __builtin_bit_cast(u16x2, w[t] & 0x7fff7fffu));
+    }
+    eb[hh] = (unsigned)(m[0] > m[1] ? m[0] : m[1]) >> 7;  // biased exponent of the half's max (0: zero)
+  }
+  const unsigned p0 = eb[0] | eb[1] << 16;
+  const auto sw = __builtin_amdgcn_permlane16_swap(p0, p0, false, false);
+  const u16x2 p = __builtin_elementwise_max(__builtin_bit_cast(u16x2, (unsigned)sw[0]),
+                                            __builtin_bit_cast(u16x2, (unsigned)sw[1]));
+  // v_cvt_scalef32_pk_fp8_bf16 divides by its scale and rounds once (scripts/ubench/scalecvt.hip:
+  // bit-equal to RNE(x·2^k) over every bf16 input, e4m3 denormals included), so 2 bf16 → 2 e4m3
+  // per instruction with scale 2^−k; the block max lands in [128, 256): no saturation is needed
+  typedef short i16x2 __attribute__((ext_vector_type(2)));
+  long f[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float sinv = __builtin_bit_cast(float, (unsigned)(127 - mx_k(p[i >> 1])) << 23);  // 2^-k
+    // the operands as shufflevector pairs: a bit_cast of one dword of the vector made the compiler
+    // convert the first dword four times (hipcc of ROCm 7.2)
+    const bf16x8 x = c[i];
+    i16x2 lo = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(i16x2{0, 0}, __builtin_shufflevector(x, x, 0, 1), sinv, false);
+    lo = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(lo, __builtin_shufflevector(x, x, 2, 3), sinv, true);
+    i16x2 hi = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(i16x2{0, 0}, __builtin_shufflevector(x, x, 4, 5), sinv, false);
+    hi = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(hi, __builtin_shufflevector(x, x, 6, 7), sinv, true);
+    f[i] = (long)__builtin_bit_cast(unsigned, lo) | ((long)__builtin_bit_cast(unsigned, hi) << 32);
+  }
+  x0 = l2{f[0], f[1]};
+  x1 = l2{f[2], f[3]};
+  return __builtin_bit_cast(unsigned, p);
+}
+// one block-scaled MFMA over two 16-B e4m3 halves per operand; sa, sb: this lane's E8M0 scales
+__device__ __forceinline__ f32x4 mx_mfma(l2 a0, l2 a1, l2 b0, l2 b1, f32x4 acc, int sa, int sb) {
+  typedef long l4 __attribute__((ext_vector_type(4)));
+  const i32x8 a = __builtin_bit_cast(i32x8, l4{a0[0], a0[1], a1[0], a1[1]});
+  const i32x8 b = __builtin_bit_cast(i32x8, l4{b0[0], b0[1], b1[0], b1[1]});
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, acc, 0, 0, 0, sa, 0, sb);
+}

@@ -427,13 +427,83 @@ struct SplitK {
   int pw;             // floats per partial (0: 32·TW + 32 of the tile)
 };
 
+// ---- MX dW (CVAE_FP8_DW=mx: the wide fp8 form's 32 × 64 tiles, batch a multiple of 128).  One
+// 128-row chunk of the batch (K) per block-scaled MFMA; every 32 consecutive rows of one feature are
+// one MX block, converted by the consumer — the chain's 16-row workgroups cannot form them (DESIGN
+// §4.5).  Lane r + 16j loads, as quarter h, the 8 rows 32·(2(h >> 1) + (j >> 1)) + 8·(2(h & 1) + (j & 1))
+// of its feature, so the instruction's block b (quarters 2(b >> 1), +1 of the lanes j = 2(b & 1), +1)
+// is rows 32b..32b+31 (oracle/cvae_np.py mx_dw; tests/test_mx_oracle.py checks the two agree).
+// mx_block converts a lane's quarters and returns its lane pair's two block exponents; the scale
+// lane r + 16j hands the instruction (block j: half j >> 1 of pair j & 1) comes from lane
+// r + 32(j & 1) by one ds_bpermute.  The X n-tiles stream one ahead of their conversion (the
+// operand registers of two workgroups per CU).
+__device__ __forceinline__ size_t mx_row(int h, int j) {
+  return (size_t)(32 * (2 * (h >> 1) + (j >> 1)) + 8 * (2 * (h & 1) + (j & 1)));
+}
+__device__ __forceinline__ int mx_scale(unsigned p, int lane) {
+  const int j = lane >> 4;
+  const unsigned pp = (unsigned)__builtin_amdgcn_ds_bpermute(((lane & 15) + 32 * (j & 1)) << 2, (int)p);
+  return 127 - mx_k((int)(pp >> (16 * (j >> 1))) & 0xffff);
+}
+// G, X: the layer's arena matrices (block-uniform: buffer resources, no 64-bit lane addresses);
+// fo, fi: this lane's first output / input feature (o0 + r, i0 + r); ct: the chunk's first row
+template <int NX>
+__device__ __forceinline__ void mx_dw_chunk(const __bf16* G, const __bf16* X, int fo, int fi, int ct, int Kg, int Kx,
+                                            f32x4 (&acc)[2][NX], float (&gs)[2], bool bias_tile) {
+  const int lane = threadIdx.x & 63, j = lane >> 4;
+  const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)G, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, 0x7fffffff, 0x00020000);
+  auto bo = [](int f, int row, int Kf) { return (((row >> 4) * Kf + f) * 16 + (row & 15)) * 2; };  // aoff, bytes
+  auto ld = [](__amdgpu_buffer_rsrc_t rs, int off) {
+    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+  };
+  int r[4];
+#pragma unroll
+  for (int h = 0; h < 4; ++h) r[h] = ct + (int)mx_row(h, j);
+  auto ldx = [&](bf16x8 (&d)[4], int n) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h) d[h] = ld(rx, bo(fi + 16 * n, r[h], Kx));
+  };
+  bf16x8 g[2][4], xa[4], xb[4];
+#pragma unroll
+  for (int h = 0; h < 4; ++h)
+#pragma unroll
+    for (int m = 0; m < 2; ++m) g[m][h] = ld(rg, bo(fo + 16 * m, r[h], Kg));
+  ldx(xa, 0);
+  l2 g8[2][2];
+  int sg[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    sg[m] = mx_scale(mx_block(g[m], g8[m][0], g8[m][1]), lane);
+    if (bias_tile) {
+#pragma unroll
+      for (int h = 0; h < 4; ++h)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) gs[m] += (float)g[m][h][e];
+    }
+  }
+  // one X n-tile ahead: n-tile n + 1 loads while n converts (operand registers for two workgroups per CU)
+#pragma unroll
+  for (int n = 0; n < NX; ++n) {
+    bf16x8 (&cur)[4] = (n & 1) ? xb : xa;
+    bf16x8 (&nxt)[4] = (n & 1) ? xa : xb;
+    if (n + 1 < NX) ldx(nxt, n + 1);
+    l2 x0, x1;
+    const int sx = mx_scale(mx_block(cur, x0, x1), lane);
+#pragma unroll
+    for (int m = 0; m < 2; ++m) acc[m][n] = mx_mfma(g8[m][0], g8[m][1], x0, x1, acc[m][n], sg[m], sx);
+  }
+}
+
 // One workgroup = tile td of layer L: 32 outputs × 32·NI inputs (NI = 2: two 32-wide input tiles
 // sharing the G rows).  loss_block: this workgroup also finishes the loss (S, D, Z: its shape).
-template <typename T, int MODE, int NI = 1>
+// MXW (NI = 2 only): the MX dW (mx_dw_chunk) in place of the bf16 MFMA loop; Bk % 128 == 0.
+template <typename T, int MODE, int NI = 1, bool MXW = false>
 __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td, int Bk, AdamArgs aa,
                                            const LossArgs& la, bool loss_block, int S, int D, int Z,
                                            float* red, float* dbp, SplitK sk = SplitK{1, 0, nullptr, nullptr, 0},
                                            const PeerArgs* px = nullptr) {
+  static_assert(!MXW || (NI == 2 && std::is_same<T, __bf16>::value), "the MX dW: bf16 arena, 32 × 64 tiles");
   using V = typename Op<T>::V;
   constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC;
   constexpr int NX = 2 * NI, TW = 32 * NI, LD = TW + 4;  // X fragments per chunk, tile width, image stride
@@ -467,7 +537,8 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
   for (int n = 0; n < NX; ++n) xp[n] = X + aoff(td.i0 + n * 16 + r16, kq, Kx);
   // this split's chunk range [c0, c0 + nk) (split-K; the whole batch when S == 1); this wave's
   // chunks: c0 + wave + WG_NW*j; PF chunks of loads kept in flight
-  const int nk_all = Bk / KC, per = (nk_all + sk.S - 1) / sk.S;
+  constexpr int KCH = MXW ? 128 : KC;  // batch rows per chunk
+  const int nk_all = Bk / KCH, per = (nk_all + sk.S - 1) / sk.S;
   const int c0 = sk.s * per, nk = max(0, min(per, nk_all - c0));
   const int nmine = nk > wave ? (nk - wave + WG_NW - 1) / WG_NW : 0;
   // chunks in flight per wave: 4; 2 for 32 × 64 tiles, whose 6 operand vectors per chunk would
@@ -483,10 +554,23 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
   };
   // the master state the epilogue updates (independent of the gradient), issued FIRST: the
   // compiler's waits inside loadn's paths then cover nothing but these loads, never the operands
+  // MXW: after the MX loop instead (its operands need the registers; the loads then overlap the
+  // cross-wave reduction)
   PreN<EPT> st = {};
-  if (tid < 32 * TPR) st = loadn<MODE, EPT>(L, td.o0 + o, td.i0 + iv, aa);
   PreB sb = {0.f, 0.f, 0.f, -1};
-  if (bias_tile && tid < 32) sb = loadb<MODE>(L, td.o0 + tid, aa);
+  if (!MXW) {
+    if (tid < 32 * TPR) st = loadn<MODE, EPT>(L, td.o0 + o, td.i0 + iv, aa);
+    if (bias_tile && tid < 32) sb = loadb<MODE>(L, td.o0 + tid, aa);
+  }
+  if constexpr (MXW) {
+    if (MODE == PM_ADAM) adam_resolve(aa, t_step);
+    if (loss_block && wave == WG_NW - 1 && la.partials) finish_loss(la, S, D, Z);
+    for (int jj = 0; jj < nmine; ++jj)
+      mx_dw_chunk<NX>((const __bf16*)G, (const __bf16*)X, td.o0 + r16, td.i0 + r16, (c0 + wave + WG_NW * jj) * KCH,
+                      Kg, Kx, acc, gs, bias_tile);
+    if (tid < 32 * TPR) st = loadn<MODE, EPT>(L, td.o0 + o, td.i0 + iv, aa);
+    if (bias_tile && tid < 32) sb = loadb<MODE>(L, td.o0 + tid, aa);
+  } else {
 #pragma unroll
   for (int u = 0; u < PF; ++u) load(u, u);
   // device-counter path: this step's Adam scalars (double pow), computed while the operands load
@@ -512,6 +596,7 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
       if (j + PF < nmine) load(u, j + PF);
     }
   }
+  }  // bf16 loop
   WSTAMP(1);
   float* rw = red + wave * 32 * LD;
 #pragma unroll

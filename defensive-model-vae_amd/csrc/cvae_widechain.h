@@ -328,7 +328,6 @@ __device__ __forceinline__ void ring_load(Ring<P>& ring, const char* AR, int wav
 // e4m3 activation images (F8): fragment order, 16 B per (64-wide K pair kp, row quad q, row r) —
 // lane (r, q) of an e4m3 X operand reads its two 32-wide chunks of pair kp (frag_k order, as the
 // e4m3 weight fragment, cvae_device.h f8_wf_off) with one ds_read_b128
-typedef long l2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ l2 x8frag(const void* img8, int kp) {
   const int lane = threadIdx.x & 63;
   return *(const l2*)((const uint8_t*)img8 + (((kp * 4 + (lane >> 4)) * 16 + (lane & 15)) << 4));
@@ -341,7 +340,7 @@ __device__ __forceinline__ void img8(void* im8, int f, bf16x4 h, int q) {
   const int b = threadIdx.x & 3, f0 = f - b;
   const int kc = f0 >> 5, kk = f0 & 31, qx = (kk & 15) >> 2, e0 = (kk >> 4) << 2;
   const f32x4 t = quad_t(from_bf4(h));  // features f0..f0+3 of row 4q + b
-  auto c = [](float x) { return fminf(fmaxf(x, -F8_MAX), F8_MAX); };
+  auto c = [](float x) { return f8_sat(x); };
   int w = __builtin_amdgcn_cvt_pk_fp8_f32(c(t[0]), c(t[1]), 0, false);
   w = __builtin_amdgcn_cvt_pk_fp8_f32(c(t[2]), c(t[3]), w, true);
   *(int*)((uint8_t*)im8 + ((((kc >> 1) * 4 + qx) * 16 + 4 * q + b) << 4) + (kc & 1) * 8 + e0) = w;
@@ -371,7 +370,6 @@ __device__ __forceinline__ f32x4 xmfma(XOp<F8> x, bf16x8 w, f32x4 acc) {
 // rate of the non-scaled fp8 form, which runs at the bf16 rate on gfx950).  A lane's 32 bytes
 // are its 16-B fragments of pairs kp and kp + 1, for A (activations) and B (weights) alike;
 // scripts/ubench/mxcheck.hip checks this equals four v_mfma_f32_16x16x32_fp8_fp8 on the GPU.
-typedef int i32x8 __attribute__((ext_vector_type(8)));
 template <class X>  // X = l2 (an e4m3 pair); the bf16 instantiation of the callers never reaches it
 __device__ __forceinline__ f32x4 mx2(X x0, X x1, bf16x8 w0, bf16x8 w1, f32x4 acc) {
   static_assert(std::is_same<X, l2>::value, "e4m3 pairs only");
@@ -504,51 +502,6 @@ __device__ __forceinline__ f32x4 mx2s(l2 x0, l2 x1, bf16x8 w0, bf16x8 w1, f32x4 
   const i32x8 a = __builtin_bit_cast(i32x8, l4{x0[0], x0[1], x1[0], x1[1]});
   const i32x8 b = __builtin_bit_cast(i32x8, l4{w0l[0], w0l[1], w1l[0], w1l[1]});
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, acc, 0, 0, 0, sa, 0, sb);
-}
-// k of a block whose max has biased exponent e: 2^k puts the max in [128, 256); 0 for an all-zero block
-__device__ __forceinline__ int mx_k(int e) { return e > 0 ? min(134 - e, 126) : 0; }
-// The lane's 8 values of each of four gradient chunks (frag_k order) → e4m3 bytes of 2^k·g, k of the
-// quarter's block; returns the two block exponents of the lane's pair (halves 0, 1 as two u16).  The
-// maxima are taken on the bf16 bit patterns (|x| = bits & 0x7fff orders like the values; the bf16
-// exponent field is fp32's), the pair's in one permlane16 swap (lanes L, L ^ 16), no LDS round trip.
-__device__ __forceinline__ unsigned mx_block(const bf16x8 (&c)[4], l2& x0, l2& x1) {
-  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-  unsigned eb[2];
-#pragma unroll
-  for (int hh = 0; hh < 2; ++hh) {
-    u16x2 m = {0, 0};
-#pragma unroll
-    for (int i = 2 * hh; i < 2 * hh + 2; ++i) {
-      const u32x4 w = __builtin_bit_cast(u32x4, c[i]);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) m = __builtin_elementwise_max(m, __builtin_bit_cast(u16x2, w[t] & 0x7fff7fffu));
-    }
-    eb[hh] = (unsigned)(m[0] > m[1] ? m[0] : m[1]) >> 7;  // biased exponent of the half's max (0: zero)
-  }
-  const unsigned p0 = eb[0] | eb[1] << 16;
-  const auto sw = __builtin_amdgcn_permlane16_swap(p0, p0, false, false);
-  const u16x2 p = __builtin_elementwise_max(__builtin_bit_cast(u16x2, (unsigned)sw[0]),
-                                            __builtin_bit_cast(u16x2, (unsigned)sw[1]));
-  // v_cvt_scalef32_pk_fp8_bf16 divides by its scale and rounds once (scripts/ubench/scalecvt.hip:
-  // bit-equal to RNE(x·2^k) over every bf16 input, e4m3 denormals included), so 2 bf16 → 2 e4m3
-  // per instruction with scale 2^−k; the block max lands in [128, 256): no saturation is needed
-  typedef short i16x2 __attribute__((ext_vector_type(2)));
-  long f[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float sinv = __builtin_bit_cast(float, (unsigned)(127 - mx_k(p[i >> 1])) << 23);  // 2^-k
-    // the operands as shufflevector pairs: a bit_cast of one dword of the vector made the compiler
-    // convert the first dword four times (hipcc of ROCm 7.2)
-    const bf16x8 x = c[i];
-    i16x2 lo = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(i16x2{0, 0}, __builtin_shufflevector(x, x, 0, 1), sinv, false);
-    lo = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(lo, __builtin_shufflevector(x, x, 2, 3), sinv, true);
-    i16x2 hi = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(i16x2{0, 0}, __builtin_shufflevector(x, x, 4, 5), sinv, false);
-    hi = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(hi, __builtin_shufflevector(x, x, 6, 7), sinv, true);
-    f[i] = (long)__builtin_bit_cast(unsigned, lo) | ((long)__builtin_bit_cast(unsigned, hi) << 32);
-  }
-  x0 = l2{f[0], f[1]};
-  x1 = l2{f[2], f[3]};
-  return __builtin_bit_cast(unsigned, p);
 }
 // The MX operand image of step S: wave w converts K-pair groups w, w + 8, .. of the bf16 gradient
 // image (its four chunk fragments, mx_block) into e4m3 operand halves at twin + g·2 KB + h·1 KB +
@@ -1117,7 +1070,8 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
       lv[k][i] = acc[1][i] + bl;
       const float sd = __expf(0.5f * lv[k][i]);
       z[i] = mu[k][i] + ep[k][i] * sd;
-      if (4 * q + i < nrows) s_kl += 1.f + lv[k][i] - mu[k][i] * mu[k][i] - __expf(lv[k][i]);
+      // the KL term (:243) of these latents is summed in the decoder-L0 backward, which computes
+      // exp(logvar) anyway (same expression, same per-lane order: the sum is bit-identical)
       if (TAP && 4 * q + i < nrows) {
         if (a.mu_out) a.mu_out[(size_t)(b0 + 4 * q + i) * Z + j] = mu[k][i];
         if (a.lv_out) a.lv_out[(size_t)(b0 + 4 * q + i) * Z + j] = lv[k][i];
@@ -1302,9 +1256,10 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const bool live = 4 * q + i < nrows;
-        const float sd = __expf(0.5f * lv[k][i]);
+        const float sd = __expf(0.5f * lv[k][i]), el = __expf(lv[k][i]);
+        if (live) s_kl += 1.f + lv[k][i] - mu[k][i] * mu[k][i] - el;  // KL (:243), from the fc epilogue
         gm[i] = live ? a.w_kld * mu[k][i] * inv_BZ + acc[k][i] : 0.f;
-        gl[i] = live ? a.w_kld * 0.5f * (__expf(lv[k][i]) - 1.f) * inv_BZ + acc[k][i] * ep[k][i] * 0.5f * sd : 0.f;
+        gl[i] = live ? a.w_kld * 0.5f * (el - 1.f) * inv_BZ + acc[k][i] * ep[k][i] * 0.5f * sd : 0.f;
       }
       img(GFC, j, to_bf4(gm));
       img(GFC, Z + j, to_bf4(gl));

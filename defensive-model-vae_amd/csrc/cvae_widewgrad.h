@@ -117,7 +117,9 @@ __host__ __device__ inline LayerDev wide_layer(int l, char* arena, int Bp) {
 
 // grid = total tiles × sk.S + 1 (split-major; the last block finishes the loss).  Two workgroups per
 // CU (4 waves per SIMD): the 436 tiles of cfg5 fit the 512 slots in one round.
-template <class A, int MODE>
+// MXW: the 32 × 64 tiles' dW GEMMs in e4m3 with MX block scales along the batch (mx_dw_chunk,
+// CVAE_FP8_DW=mx; Bk % 128 == 0); the 32 × 32 tiles (the K=2 condition layer) stay bf16
+template <class A, int MODE, bool MXW = false>
 __global__ __launch_bounds__(WG_THREADS, 4) void widewgrad_kernel(char* arena, float* params, float* mst, float* vst,
                                                                 int Bp, int Bk, AdamArgs a, LossArgs la, SplitK sk) {
   AdamArgs aa = a;
@@ -135,7 +137,7 @@ __global__ __launch_bounds__(WG_THREADS, 4) void widewgrad_kernel(char* arena, f
   const TileDesc td = WTiles<A>::at(sk.tile);
   const LayerDev L = wide_layer<A>(td.layer, arena, Bp);
   if (td.ni == 2)  // block-uniform
-    wgrad_body<__bf16, MODE, 2>(L, td, Bk, aa, la, false, A::S, A::D, A::Z, sh.red, sh.dbp, sk);
+    wgrad_body<__bf16, MODE, 2, MXW>(L, td, Bk, aa, la, false, A::S, A::D, A::Z, sh.red, sh.dbp, sk);
   else
     wgrad_body<__bf16, MODE, 1>(L, td, Bk, aa, la, false, A::S, A::D, A::Z, sh.red, sh.dbp, sk);
 }

@@ -138,6 +138,36 @@ def mx_dx(G, W, s):
     return (x8.astype(np.float64) @ w8.astype(np.float64)).astype(np.float32)
 
 
+def mx_dw(G, X):
+    """dW = Gᵀ·X of a layer whose weight-gradient GEMM runs in e4m3 with MX scales along the batch
+    (the wide fp8 dW, cvae_wgrad.h mx_dw_chunk; CVAE_FP8_DW=mx): G (B, N) and X (B, K) the bf16
+    arena rows.  Every 32 consecutive batch rows of one feature are one MX block of the block-scaled
+    MFMA (K = the batch: a 128-row chunk per instruction, block b = rows 32b..32b+31 of it); each
+    block is scaled by 2^kb, kb = 134 − (biased fp32 exponent of max|block|) (0 for an all-zero
+    block, at most 126), rounded to e4m3 and unscaled in the product — both operands alike."""
+    def blocks(A):
+        A = np.asarray(A, np.float32)
+        B, F = A.shape
+        Bp = (B + 31) // 32 * 32
+        Ap = np.zeros((Bp, F), np.float32)
+        Ap[:B] = A
+        a3 = Ap.reshape(Bp // 32, 32, F)
+        amax = np.abs(a3).max(axis=1, keepdims=True)
+        eb = ((amax.view(np.uint32) >> 23) & 0xFF).astype(np.int64)
+        kb = np.where(eb > 0, np.minimum(134 - eb, 126), 0).astype(np.float64)
+        sc = np.exp2(kb).astype(np.float32)
+        return (e4m3(a3 * sc) / sc).reshape(Bp, F)
+    return (blocks(G).astype(np.float64).T @ blocks(X).astype(np.float64)).astype(np.float32)
+
+
+def mxw_layers(p, n_enc=4, n_dec=4):
+    """The layers whose dW the wide fp8 MX dW kernel computes in e4m3 (its 32 × 64 tiles: padded K a
+    multiple of 64 — every layer but the K=2 condition layer); fc_mu / fc_logvar are one layer."""
+    names = ["condition_encoder.2"] + [f"encoder.{2 * i + 1}" for i in range(n_enc)] + ["fc_mu", "fc_logvar"] \
+        + [f"decoder.{2 * i}" for i in range(n_dec)]
+    return {n for n in names if (p[n + ".weight"].shape[1] + 31) // 32 * 32 % 64 == 0}
+
+
 def forward(p, x, eps, n_enc=4, n_dec=4, dt=np.float32, q=None, f8=None):
     """x: (B,S,D) absolute trajectories.  Returns (recon, mu, logvar, h_c, cache).
 
@@ -204,16 +234,17 @@ def dloss_drecon(r, x_rel, w=(0.1, 0.1, 1.0, 1.0), B_norm=None):
     return g
 
 
-def backward(p, c, r, mu, lv, w=(0.1, 0.1, 1.0, 1.0), n_enc=4, n_dec=4, dt=np.float32, f8b=None):
+def backward(p, c, r, mu, lv, w=(0.1, 0.1, 1.0, 1.0), n_enc=4, n_dec=4, dt=np.float32, f8b=None, mxw=None):
     """Gradients of the total loss w.r.t. every parameter (dict keyed like state_dict).
 
     With the cache of ``forward(..., q=bf16)`` every stored gradient G and every GEMM operand
     is rounded as the bf16 kernels round them (dz, the decoder's dh_c share, accumulations and
     the loss stay fp32).  f8b: {layer name: weight scale} (``fp8b_layers``) — those layers' dX
     GEMMs run in e4m3 with MX row-block scales (``mx_dx``; the wide chain's CVAE_FP8 form); their
-    dW stays bf16.
+    dW stays bf16 — unless the layer is in ``mxw`` (``mxw_layers``): then its dW is ``mx_dw``.
     """
     f8b = f8b or {}
+    mxw = mxw or set()
     q = c.get("q", _ident)
     p = {k: v.astype(dt) for k, v in p.items()}
     B, S, D = r.shape
@@ -222,7 +253,7 @@ def backward(p, c, r, mu, lv, w=(0.1, 0.1, 1.0, 1.0), n_enc=4, n_dec=4, dt=np.fl
 
     def lin_grads(name, G, X):
         G, X = q(G), q(X)
-        g[name + ".weight"] = G.T @ X
+        g[name + ".weight"] = mx_dw(G, X) if name in mxw else G.T @ X
         g[name + ".bias"] = G.sum(0)
         if name in f8b:
             return mx_dx(G, p[name + ".weight"], f8b[name])
