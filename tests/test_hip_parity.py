@@ -1094,9 +1094,12 @@ def test_wide_fp8_mx_dw_matches_emulation(cvae, monkeypatch, B):
     The fused step equals the split (data-parallel) step bit for bit."""
     monkeypatch.setenv("CVAE_FP8_DW", "mx")
     ref, m, eng, x, eps = _wide(cvae, "fp8", B)
-    m2 = cvae.ConditionalTrajectoryVAE(WIDE["S"], WIDE["D"], WIDE["Z"], 128, WIDE["n_enc"], WIDE["n_dec"])
-    m2.load_state_dict(ref.state_dict())
-    e2 = m2.attach(dtype="fp8", max_batch=B, device="cuda:0")
+    ef, es = [], []
+    for lst in (ef, es):  # fresh engines (device step counters at 0) for the fused / split comparison
+        mm = cvae.ConditionalTrajectoryVAE(WIDE["S"], WIDE["D"], WIDE["Z"], 128, WIDE["n_enc"], WIDE["n_dec"])
+        mm.load_state_dict(ref.state_dict())
+        lst.append(mm.attach(dtype="fp8", max_batch=B, device="cuda:0"))
+    e1, e2 = ef[0], es[0]
     monkeypatch.delenv("CVAE_FP8_DW")
     assert eng.train_kernel == "wide"
     x = x.to(torch.bfloat16).float()
@@ -1122,11 +1125,11 @@ def test_wide_fp8_mx_dw_matches_emulation(cvae, monkeypatch, B):
     assert e_mx < e_bf
     assert max(dev.values()) < 0.1 and np.median(list(dev.values())) < 0.05, dev
     for _ in range(2):  # fused step == split step, MX dW in both (PM_ADAM and PM_GRAD forms)
-        eng.train_step(x, eps=eps)
+        e1.train_step(x, eps=eps)
         e2.forward_backward(x, eps=eps)
         e2.adam_step(1.0)
     torch.cuda.synchronize()
-    assert torch.equal(eng.params, e2.params)
+    assert torch.equal(e1.params, e2.params)
 
 
 def test_fp8_mx_dw_loss_trajectory_vs_bf16_dw(cvae, monkeypatch):
