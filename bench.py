@@ -334,6 +334,9 @@ def main():
                     help="N>1 gradient exchange: peer = dW + reduce-scatter + Adam + all-gather inside the "
                          "weight-gradient launch over IPC-mapped peer memory (cvae_amd.peer); rccl = all-reduce of "
                          "the flat gradient, then Adam; auto = peer where the configuration has it")
+    ap.add_argument("--torch-allreduce", action="store_true",
+                    help="split step: torch.distributed's all_reduce instead of the library's own RCCL "
+                         "communicator on the step's stream (cvae_rccl_*; A/B)")
     ap.add_argument("--buckets", type=int, default=1, choices=[1, 2],
                     help="split step: 2 = decoder-gradient all-reduce overlapped with the rest of dW")
     ap.add_argument("--graph", action="store_true",
@@ -400,7 +403,8 @@ def main():
     model = ConditionalTrajectoryVAE(S, D, Z, H, NE, ND, n_classes=NC, class_dim=CE or 16)
     eng = model.attach(dtype=dtype, max_batch=B, device=dev, seed=4321)
     dp = DataParallelStep(eng, force_split=args.dp, buckets=args.buckets,
-                          exchange="rccl" if wl in ("cfg1", "cfg4") else args.exchange)
+                          exchange="rccl" if wl in ("cfg1", "cfg4") else args.exchange,
+                          native=False if args.torch_allreduce else None)
     dp.broadcast_params()
 
     if wl == "cfg1":
@@ -606,8 +610,8 @@ def main():
                "scaling": "weak", "vs_baseline": None, "dtype": dtype, "data": data,
                "config": {"workload": f"{wl}: Training_VAE step, B_local={B} S={S} D={D} Z={Z} H={H}, "
                                       f"{NE}+{ND} layers, {dtype} operands / fp32 master+Adam, {path} step"
-                                      + (f", rccl all-reduce, {args.buckets} buckets" if dp.split and dp.px is None
-                                         else "") + (f" [{dp.exchange_note}]" if dp.exchange_note else ""),
+                                      + (f", rccl all-reduce ({'library communicator on the step stream' if dp.rccl is not None else 'torch.distributed'}), {args.buckets} buckets"
+                                         if dp.split and dp.px is None else "") + (f" [{dp.exchange_note}]" if dp.exchange_note else ""),
                           "global_batch": B * world, "seq_len": S, "state_dim": D, "latent_dim": Z,
                           "hidden_dim": H, "parallelism": f"dp{world}" + (" (rehearsal: all ranks on GPU 0)"
                                                                           if share else "")},

@@ -2,6 +2,7 @@
 // launches.  All launches go to the caller's stream; nothing here synchronises.
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
+#include <rccl/rccl.h>
 
 #include <cmath>
 #include <cstdio>
@@ -79,6 +80,8 @@ struct cvae_handle {
   // every rank's arena / mailbox as mapped into this process
   int px_world = 0, px_rank = 0;
   char* px_mbox = nullptr;
+  ncclComm_t rccl = nullptr;   // cvae_rccl_init: this rank's communicator (the gradient all-reduce)
+  int rccl_world = 0, rccl_rank = 0;
   int64_t px_mbox_bytes = 0, px_done_off = 0, px_inbox_off = 0;
   char* px_arena[PX_MAX] = {};
   char* px_mb[PX_MAX] = {};
@@ -1111,6 +1114,7 @@ int cvae_destroy(cvae_handle* h) {
   if (h->arena) (void)hipFree(h->arena);
   if (h->fault_host) (void)hipHostFree(h->fault_host);
   cvae_px_close(h);
+  cvae_rccl_close(h);
   delete h;
   return CVAE_OK;
 }
@@ -1640,6 +1644,59 @@ int cvae_px_reset(cvae_handle* h, uint64_t base) {
   HIPCK(hipDeviceSynchronize());
   h->px_base = base;
   if (h->fault_host) __atomic_store_n(h->fault_host, 0u, __ATOMIC_RELEASE);
+  return CVAE_OK;
+}
+
+// ---- the gradient all-reduce over RCCL, issued by the library on the caller's stream (include/cvae.h)
+#define RCCLCK(x)                                                                       \
+  do {                                                                                  \
+    ncclResult_t r_ = (x);                                                              \
+    if (r_ != ncclSuccess) return fail(CVAE_E_HIP, std::string(#x ": ") + ncclGetErrorString(r_)); \
+  } while (0)
+
+int cvae_rccl_id_bytes(int64_t* bytes) {
+  if (!bytes) return fail(CVAE_E_INVALID, "null argument");
+  *bytes = (int64_t)sizeof(ncclUniqueId);
+  return CVAE_OK;
+}
+
+int cvae_rccl_unique_id(void* id) {
+  if (!id) return fail(CVAE_E_INVALID, "null argument");
+  ncclUniqueId u;
+  RCCLCK(ncclGetUniqueId(&u));
+  std::memcpy(id, &u, sizeof(u));
+  return CVAE_OK;
+}
+
+int cvae_rccl_init(cvae_handle* h, const void* id, int world, int rank) {
+  if (!h || !id) return fail(CVAE_E_INVALID, "null argument");
+  if (world < 1 || rank < 0 || rank >= world) return fail(CVAE_E_INVALID, "rank must lie in [0, world)");
+  cvae_rccl_close(h);
+  HIPCK(hipSetDevice(h->device));
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof(u));
+  RCCLCK(ncclCommInitRank(&h->rccl, world, u, rank));
+  h->rccl_world = world;
+  h->rccl_rank = rank;
+  return CVAE_OK;
+}
+
+int cvae_rccl_allreduce(cvae_handle* h, float* buf, int64_t count, void* stream) {
+  if (!h || (!buf && count > 0) || count < 0) return fail(CVAE_E_INVALID, "null argument or negative count");
+  if (!h->rccl) return fail(CVAE_E_INVALID, "cvae_rccl_init first");
+  if (count == 0) return CVAE_OK;
+  RCCLCK(ncclAllReduce(buf, buf, (size_t)count, ncclFloat32, ncclSum, h->rccl, (hipStream_t)stream));
+  return CVAE_OK;
+}
+
+int cvae_rccl_close(cvae_handle* h) {
+  if (!h) return fail(CVAE_E_INVALID, "null handle");
+  if (h->rccl) {
+    (void)hipSetDevice(h->device);
+    (void)ncclCommDestroy(h->rccl);
+    h->rccl = nullptr;
+  }
+  h->rccl_world = h->rccl_rank = 0;
   return CVAE_OK;
 }
 

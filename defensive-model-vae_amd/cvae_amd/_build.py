@@ -32,7 +32,7 @@ def _command(out):
            "-Wno-unused-result", "-Wno-pass-failed", "-mllvm", "-amdgpu-mfma-vgpr-form",
            "-mllvm", "-amdgpu-kernarg-preload-count=16", "-o", out]
     cmd += os.environ.get("CVAE_EXTRA_FLAGS", "").split()  # diagnostic builds only (with CVAE_LIB)
-    return cmd + [os.path.join(CSRC, s) for s in SOURCES]
+    return cmd + [os.path.join(CSRC, s) for s in SOURCES] + ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
 
 
 def source_digest() -> str:
@@ -94,7 +94,8 @@ def build_asan(out_dir, verbose=False) -> tuple:
     if not os.path.exists(so) or any(os.path.getmtime(f) > os.path.getmtime(so) for f in _inputs()):
         cmd = [hipcc, f"--offload-arch={ARCH}", "-O1", "-g", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
                "-Wno-pass-failed", "-mllvm", "-amdgpu-mfma-vgpr-form", "-Xarch_host", "-fsanitize=address",
-               "-Xarch_host", "-fno-omit-frame-pointer", "-o", so + ".tmp", os.path.join(CSRC, "cvae_capi.hip")]
+               "-Xarch_host", "-fno-omit-frame-pointer", "-o", so + ".tmp", os.path.join(CSRC, "cvae_capi.hip"),
+               "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True, cwd=CSRC)

@@ -82,6 +82,11 @@ _SIGS = {
     "cvae_px_stats": (_i, [_v, C.POINTER(C.c_uint64), _i]),
     "cvae_px_layout": (_i, [_v, C.POINTER(_i), C.POINTER(_i)]),  # h, ranks_on_gpu, tile_blocks
     "cvae_px_reset": (_i, [_v, _u64]),                            # h, base
+    "cvae_rccl_id_bytes": (_i, [c_i64p]),
+    "cvae_rccl_unique_id": (_i, [_v]),                             # id (host bytes)
+    "cvae_rccl_init": (_i, [_v, _v, _i, _i]),                      # h, id, world, rank
+    "cvae_rccl_allreduce": (_i, [_v, _v, _i64, _v]),               # h, buf, count, stream
+    "cvae_rccl_close": (_i, [_v]),
     "cvae_operand_checksum": (_i, [_v, _v, _v]),                  # h, out (device u64), stream
     "cvae_tap_outputs": (_i, [_v, _v, _v, _v]),                   # h, recon, mu, logvar
     # h, x, idx, batch, xflags, eps, seed, eps_row0, w, params, m, v, adam, rank_scales, loss_out, loss_accum,

@@ -17,10 +17,17 @@ eps: the in-kernel Philox draw is keyed by the GLOBAL row (``row0`` = lo_r, the 
 of the global batch) and every rank advances the same device offset, so the ranks of a global
 batch draw exactly the noise one process with that batch draws — not rank 0's noise B_r times.
 
+The all-reduce itself (``native``, the default on a GPU engine): the library's own RCCL
+communicator (``NativeRccl``: include/cvae.h cvae_rccl_*; the unique id broadcast over the group)
+issues ncclAllReduce on the stream the step's kernels run on — no framework stream between the
+dW and Adam launches, so a captured step graph is the chain, dW, the RCCL kernels and Adam on one
+stream.  ``native=False`` (and the CPU tests' engine) use torch.distributed's all_reduce.
+
 Two-bucket overlap (``buckets=2``): the dW launch is split into the decoder layers (a contiguous
-tail of the flat gradient, ready first) and the rest; the decoder bucket's all-reduce is issued
-asynchronously (RCCL runs it on the process group's stream) while the rest of the dW GEMMs run
-on the compute stream, then the second bucket follows.
+tail of the flat gradient, ready first) and the rest; the decoder bucket's all-reduce runs on a
+communication stream (every all-reduce of the communicator on that one stream, in one order on
+every rank) while the rest of the dW GEMMs run on the compute stream, then the second bucket
+follows on the communication stream and Adam waits for both.
 
 Row assignment (``shard_rows``): every rank draws the same global permutation, cuts it into
 global batches of ``batch_size * world`` and takes a contiguous slice of each, so a run over
@@ -64,6 +71,46 @@ def shard_rows(perm, batch_size, world_size, rank):
     return out
 
 
+class NativeRccl:
+    """The gradient all-reduce issued by libcvae_hip on a given stream (cvae_rccl_init /
+    cvae_rccl_allreduce): rank 0 makes the RCCL unique id, the group broadcasts it (any backend),
+    every rank joins the communicator on its engine's device."""
+
+    def __init__(self, engine, group=None):
+        import ctypes as C
+        from ._lib import check, lib
+        self.engine = engine
+        L = lib()
+        n = C.c_int64()
+        check(L.cvae_rccl_id_bytes(C.byref(n)), "cvae_rccl_id_bytes")
+        rank = dist.get_rank(group) if dist.is_initialized() else 0
+        world = dist.get_world_size(group) if dist.is_initialized() else 1
+        idb = (C.c_uint8 * n.value)()
+        if rank == 0:
+            check(L.cvae_rccl_unique_id(idb), "cvae_rccl_unique_id")
+        if world > 1:
+            nccl = dist.get_backend(group) == "nccl"
+            t = torch.tensor(list(bytes(idb)), dtype=torch.uint8, device=engine.device if nccl else "cpu")
+            src = dist.get_global_rank(group, 0) if group is not None else 0
+            dist.broadcast(t, src=src, group=group)
+            idb = (C.c_uint8 * n.value)(*t.cpu().tolist())
+        check(L.cvae_rccl_init(engine._h, idb, world, rank), "cvae_rccl_init")
+        self.world, self.rank = world, rank
+
+    def all_reduce(self, buf, stream=None):
+        """In-place float32 sum of ``buf`` over the ranks, enqueued on ``stream`` (default: the
+        current stream of the engine's device)."""
+        import ctypes as C
+        from ._lib import check, lib
+        st = stream if stream is not None else torch.cuda.current_stream(self.engine.device)
+        check(lib().cvae_rccl_allreduce(self.engine._h, C.c_void_p(buf.data_ptr()), buf.numel(),
+                                        C.c_void_p(st.cuda_stream)), "cvae_rccl_allreduce")
+
+    def close(self):
+        from ._lib import lib
+        lib().cvae_rccl_close(self.engine._h)
+
+
 class DataParallelStep:
     """fwd+bwd → gradient all-reduce → Adam on every rank (the fused single-GPU step split in two).
 
@@ -72,7 +119,7 @@ class DataParallelStep:
     ``buckets``: 1 = one all-reduce after the whole dW launch; 2 = decoder bucket overlapped with
     the rest of the dW GEMMs (see the module docstring)."""
 
-    def __init__(self, engine, group=None, force_split=False, buckets=1, exchange="rccl"):
+    def __init__(self, engine, group=None, force_split=False, buckets=1, exchange="rccl", native=None):
         self.engine = engine
         self.group = group
         self.rank, self.world_size = world()
@@ -102,6 +149,21 @@ class DataParallelStep:
                 if exchange == "peer":
                     raise
                 self.exchange_note = f"peer exchange unavailable ({type(e).__name__}: {e}); rccl"
+        # the all-reduce path: the library's own RCCL communicator on the step's stream (native), or
+        # torch.distributed's all_reduce (native=False; engines without a HIP handle)
+        self.rccl = None
+        self._comm_stream = None
+        if native is None:  # one rank per GPU (an RCCL group, or a lone rank); not beside the peer exchange
+            one_gpu_per_rank = self.world_size == 1 or (dist.is_initialized() and dist.get_backend(group) == "nccl")
+            native = hasattr(engine, "_h") and torch.cuda.is_available() and one_gpu_per_rank and self.px is None
+        if native and self.split:
+            try:
+                self.rccl = NativeRccl(engine, group)
+            except Exception as e:  # noqa: BLE001 — torch's all_reduce takes over, and the line says so
+                if native is True and exchange == "rccl" and self.world_size == 1:
+                    raise
+                self.exchange_note = (self.exchange_note + "; " if self.exchange_note else "") + \
+                    f"native RCCL unavailable ({type(e).__name__}: {e}); torch all_reduce"
 
     @property
     def split(self):
@@ -151,7 +213,24 @@ class DataParallelStep:
             eng.skip_step()
             ragged, scale = True, 1.0
         g = eng.grads
-        if two:
+        if two and self.rccl is not None:  # the communication stream: both buckets, in order
+            main = torch.cuda.current_stream(eng.device)
+            if self._comm_stream is None:
+                self._comm_stream = torch.cuda.Stream(device=eng.device)
+            cs = self._comm_stream
+            dec, rest = g[eng.bucket_split:], g[:eng.bucket_split]
+            if ragged:
+                dec.mul_(batch / global_batch)
+            cs.wait_stream(main)
+            self.rccl.all_reduce(dec, cs)
+            if batch > 0:
+                eng.wgrad_rest(batch)  # beside the decoder bucket's all-reduce
+            if ragged:
+                rest.mul_(batch / global_batch)
+            cs.wait_stream(main)
+            self.rccl.all_reduce(rest, cs)
+            main.wait_stream(cs)
+        elif two:
             dec, rest = g[eng.bucket_split:], g[:eng.bucket_split]
             if ragged:
                 dec.mul_(batch / global_batch)
@@ -166,7 +245,10 @@ class DataParallelStep:
         else:
             if ragged and batch > 0:
                 g.mul_(batch / global_batch)
-            dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group)
+            if self.rccl is not None:
+                self.rccl.all_reduce(g)  # on the compute stream, between the dW and Adam launches
+            else:
+                dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group)
         eng.adam_step(grad_scale=scale)
         return eng.loss
 
@@ -203,6 +285,9 @@ class DataParallelStep:
         if self.px is not None:
             self.px.close()
             self.px = None
+        if self.rccl is not None:
+            self.rccl.close()
+            self.rccl = None
 
     def epoch_loss_sums(self):
         """Σ over ranks of the device Σ loss·batch accumulators (5 doubles); resets them."""

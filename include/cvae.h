@@ -358,6 +358,22 @@ int cvae_px_probe(cvae_handle* h, int* ok);
  * (owner tile) or 3 (end of launch).  Synchronises the device. */
 int cvae_px_stats(cvae_handle* h, uint64_t* out, int reset);
 
+/* ---- The gradient all-reduce over RCCL on the caller's stream (Training_VAE.py:362-363
+ * across ranks; BASELINE configs[2] "RCCL grad all-reduce over xGMI"): the data-parallel split
+ * step's collective, issued by this library on the stream its kernels run on, so a captured step
+ * graph holds the RCCL kernels between the dW and Adam launches with no stream of a framework in
+ * between (cvae_amd.dist.DataParallelStep, exchange "rccl").  One communicator per handle.
+ *   cvae_rccl_id_bytes: size of the unique id (handle-free);
+ *   cvae_rccl_unique_id: a new id (rank 0; the caller broadcasts it to the other ranks);
+ *   cvae_rccl_init: join the world-rank communicator of that id on the handle's device (collective);
+ *   cvae_rccl_allreduce: in-place float32 sum over the ranks of `count` elements of `buf` (device);
+ *   cvae_rccl_close: destroy the communicator (also done by cvae_destroy). */
+int cvae_rccl_id_bytes(int64_t* bytes);
+int cvae_rccl_unique_id(void* id);
+int cvae_rccl_init(cvae_handle* h, const void* id, int world, int rank);
+int cvae_rccl_allreduce(cvae_handle* h, float* buf, int64_t count, void* stream);
+int cvae_rccl_close(cvae_handle* h);
+
 /* A data-parallel step in which this rank has no rows (a ragged last global batch shorter than the
  * world): advances the device counters exactly as a training step's launches would — counters[1]
  * += 1 with that step's Adam scalars, counters[0] += 1 — so the rank's following cvae_adam uses the

@@ -176,11 +176,13 @@ def test_philox_training_step_keyed_by_global_row(cvae):
 from conftest import free_port as _port  # noqa: E402
 
 
-def test_dp_split_buckets_graph_rccl_equal_fused(cvae):
+@pytest.mark.parametrize("native", [True, False], ids=["native-rccl", "torch-all-reduce"])
+def test_dp_split_buckets_graph_rccl_equal_fused(cvae, native):
     """The data-parallel step on the real backend (a world-1 RCCL group on this one-GPU box): the
     split step, the two-bucket split step (decoder-bucket all-reduce async beside the rest of the
     dW launch) and the split step captured into a hipGraph all equal the fused single-GPU step bit
-    for bit after 4 steps (Philox eps, device counters)."""
+    for bit after 4 steps (Philox eps, device counters) — with the library's own RCCL communicator
+    issuing the all-reduce on the step's stream (native, cvae_rccl_*), and with torch's."""
     import torch.distributed as tdist
     from cvae_amd.dist import DataParallelStep, GraphedStep
     assert not tdist.is_initialized()
@@ -192,9 +194,10 @@ def test_dp_split_buckets_graph_rccl_equal_fused(cvae):
         ref = OracleCVAE(100, 6, 8)
         engs = [_model(cvae, 100, 6, 8, sd=ref.state_dict(), dtype="bf16", max_batch=256)[1] for _ in range(4)]
         x = engs[0].as_input(torch.randn(256, 100, 6, generator=torch.Generator().manual_seed(7)))
-        dps = [DataParallelStep(engs[1], force_split=True),
-               DataParallelStep(engs[2], force_split=True, buckets=2),
-               DataParallelStep(engs[3], force_split=True)]
+        dps = [DataParallelStep(engs[1], force_split=True, native=native),
+               DataParallelStep(engs[2], force_split=True, buckets=2, native=native),
+               DataParallelStep(engs[3], force_split=True, native=native)]
+        assert all((d.rccl is not None) == native for d in dps), [d.exchange_note for d in dps]
         for _ in range(4):
             engs[0].train_step(x)
             dps[0].step(x, batch=256)
@@ -208,6 +211,8 @@ def test_dp_split_buckets_graph_rccl_equal_fused(cvae):
             assert torch.equal(engs[0].m, e.m) and torch.equal(engs[0].v, e.v), k
             assert torch.equal(engs[0].counters, e.counters), k
         assert torch.equal(engs[0].loss_accum, engs[1].loss_accum)
+        for d in dps:
+            d.close()
     finally:
         tdist.destroy_process_group()
 
