@@ -763,17 +763,19 @@ def test_wide_chain_matches_generic_and_emulation(cvae, monkeypatch, B):
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp8"])
-def test_wide_chain_repeatable_and_dw_tiles_bit_equal(cvae, monkeypatch, dtype):
+@pytest.mark.parametrize("B", [64, 1000])
+def test_wide_chain_repeatable_and_dw_tiles_bit_equal(cvae, monkeypatch, dtype, B):
     """The wide chain is race-free: eight forward_backward calls on the same input give bit-equal
     gradients and losses (an inline-asm store hazard once corrupted whole gradient columns in
-    14-22 of 40 calls).  The dW launch's 32 x 64 tiles (the default for this long tile list) give
-    the same bits as 32 x 32 tiles (CVAE_DW_NI2=0): each element is the same K sum in the same
-    chunk order."""
-    ref, m, eng, x, eps = _wide(cvae, dtype, 64)
+    14-22 of 40 calls).  The dW launch's 64 x 64 tiles (the default, widewgrad64_kernel), its
+    32 x 64 tiles (CVAE_DW64=0), the generic kernel over them (CVAE_GENERIC_DW=1) and 32 x 32 tiles
+    (CVAE_DW_NI2=0) give the same bits: each element is the same K sum in the same chunk order and
+    the same fixed-order cross-wave sum.  B = 1000: a ragged last row tile."""
+    ref, m, eng, x, eps = _wide(cvae, dtype, B)
     monkeypatch.setenv("CVAE_DW_NI2", "0")
     m2 = cvae.ConditionalTrajectoryVAE(WIDE["S"], WIDE["D"], WIDE["Z"], 128, WIDE["n_enc"], WIDE["n_dec"])
     m2.load_state_dict(ref.state_dict())
-    e2 = m2.attach(dtype=dtype, max_batch=64, device="cuda:0")
+    e2 = m2.attach(dtype=dtype, max_batch=B, device="cuda:0")
     monkeypatch.delenv("CVAE_DW_NI2")
     xd = x.to("cuda", torch.bfloat16)
     l0 = eng.forward_backward(xd, eps=eps).clone()
@@ -787,15 +789,16 @@ def test_wide_chain_repeatable_and_dw_tiles_bit_equal(cvae, monkeypatch, dtype):
     # the compile-time tile decode of the wide shape (widewgrad_kernel, the default), the generic
     # kernel over the same 32 x 64 tile list (CVAE_GENERIC_DW=1) and 32 x 32 tiles (CVAE_DW_NI2=0)
     fresh = []
-    for env in (None, ("CVAE_DW_NI2", "0"), ("CVAE_GENERIC_DW", "1")):
+    for env in (None, ("CVAE_DW64", "0"), ("CVAE_DW_NI2", "0"), ("CVAE_GENERIC_DW", "1")):
         if env:
             monkeypatch.setenv(*env)
         mm = cvae.ConditionalTrajectoryVAE(WIDE["S"], WIDE["D"], WIDE["Z"], 128, WIDE["n_enc"], WIDE["n_dec"])
         mm.load_state_dict(ref.state_dict())
-        ee = mm.attach(dtype=dtype, max_batch=64, device="cuda:0")
+        ee = mm.attach(dtype=dtype, max_batch=B, device="cuda:0")
         if env:
             monkeypatch.delenv(env[0])
-        ee.train_step(xd, eps=eps)
+        for _ in range(2):
+            ee.train_step(xd, eps=eps)
         fresh.append(ee)
     torch.cuda.synchronize()
     a3 = fresh[0]
