@@ -107,7 +107,6 @@ struct cvae_handle {
   bool wide_dw = false;     // ... and its dW ⊕ Adam runs wchain::widewgrad_kernel (compile-time tile decode)
   bool wide_mx = false;     // CVAE_FP8 at that shape: the large dX GEMMs e4m3 + MX scales (Cfg5F8), else bf16 (Cfg5F8B)
   bool wide_mxw = false;    // ... and (CVAE_FP8_DW=mx) its dW GEMMs e4m3 + MX scales along the batch
-  bool wide_dw64 = false;   // ... its dW ⊕ Adam on 64-output tiles (wchain::widewgrad64_kernel; CVAE_DW64=0: 32 × 64)
   int wide_lds = 0;
   bool ring = false;        // the fast configuration's training chain runs wchain::widechain_kernel<Cfg2>
   bool ring_cls = false;    // cfg4 (class embedding) at cfg2's shape: widechain_kernel<Cfg4>, generic dW
@@ -794,32 +793,6 @@ bool wide_dw_matches(const cvae_handle* h) {
   return true;
 }
 
-// the 64-output tile list (cvae_widewgrad.h WTiles64) covers every padded layer exactly once, in
-// 32 × 32 blocks, as the handle's own tile list does
-template <class A>
-bool wide_dw64_covers(const cvae_handle* h) {
-  using WT = wchain::WTiles64<A>;
-  std::vector<std::vector<int>> seen(A::NL);
-  for (int l = 0; l < A::NL; ++l) {
-    if (h->net.L[l].Np != A::Np(l) || h->net.L[l].Kp != A::Kp(l)) return false;
-    seen[l].assign((A::Np(l) / 32) * (A::Kp(l) / 32), 0);
-  }
-  for (int b = 0; b < WT::total(); ++b) {
-    const TileDesc t = WT::at(b);
-    if (t.layer < 0 || t.layer >= A::NL || t.o0 % 64 || t.i0 % 32) return false;
-    for (int r = 0; r < 2; ++r)
-      for (int s = 0; s < t.ni; ++s) {
-        const int ob = t.o0 / 32 + r, ib = t.i0 / 32 + s;
-        if (ob >= A::Np(t.layer) / 32 || ib >= A::Kp(t.layer) / 32) return false;
-        ++seen[t.layer][ob * (A::Kp(t.layer) / 32) + ib];
-      }
-  }
-  for (const auto& v : seen)
-    for (int k : v)
-      if (k != 1) return false;
-  return true;
-}
-
 template <class A>
 int plan_wide_as(cvae_handle* h) {
   // the wide chain stores to the arena through a buffer resource of 2^31 - 1 bytes
@@ -833,8 +806,6 @@ int plan_wide_as(cvae_handle* h) {
   // the MX dW (measured slower than the bf16 dW at B = 1024, DESIGN §4.5: an option, not the default)
   const char* mw = std::getenv("CVAE_FP8_DW");
   h->wide_mxw = std::is_same<A, wchain::Cfg5F8>::value && h->wide_dw && mw && std::strcmp(mw, "mx") == 0;
-  const char* d64 = std::getenv("CVAE_DW64");  // "0": the 32 × 64 tiles (A/B)
-  h->wide_dw64 = h->wide_dw && !(d64 && d64[0] == '0') && wide_dw64_covers<A>(h);
   return CVAE_OK;
 }
 
@@ -1019,17 +990,6 @@ int launch_wgrad(cvae_handle* h, int batch, const AdamArgs& aa, const LossArgs& 
     sk.pw = 32 * 64 + 32;
     const int g = wchain::WTiles<wchain::Cfg5>::total() * sk.S + 1;
     static_assert(wchain::WTiles<wchain::Cfg5>::total() == wchain::WTiles<wchain::Cfg5F8>::total(), "tile lists");
-    if (h->wide_dw64 && sk.S == 1 && !(h->wide_mxw && batch % 128 == 0)) {  // 64-output tiles
-      const int g64 = wchain::WTiles64<wchain::Cfg5>::total() + 1;
-      if (h->cfg.dtype == CVAE_FP8 && h->wide_mx)
-        return klaunch(h, wchain::widewgrad64_kernel<wchain::Cfg5F8, MODE>, dim3(g64), dim3(WG_THREADS), 0, s,
-                       h->arena, aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), aa, la);
-      if (h->cfg.dtype == CVAE_FP8)
-        return klaunch(h, wchain::widewgrad64_kernel<wchain::Cfg5F8B, MODE>, dim3(g64), dim3(WG_THREADS), 0, s,
-                       h->arena, aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), aa, la);
-      return klaunch(h, wchain::widewgrad64_kernel<wchain::Cfg5, MODE>, dim3(g64), dim3(WG_THREADS), 0, s,
-                     h->arena, aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), aa, la);
-    }
     if (h->cfg.dtype == CVAE_FP8 && h->wide_mxw && batch % 128 == 0)  // the MX dW: 128-row chunks
       return klaunch(h, wchain::widewgrad_kernel<wchain::Cfg5F8, MODE, true>, dim3(g), dim3(WG_THREADS), 0, s,
                      h->arena, aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), aa, la, sk);

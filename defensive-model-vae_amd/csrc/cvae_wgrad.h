@@ -110,18 +110,6 @@ constexpr int WT_LD = 36;
 template <int EPT> struct VecF;
 template <> struct VecF<2> { typedef float T __attribute__((ext_vector_type(2))); };
 template <> struct VecF<4> { typedef f32x4 T; };
-template <> struct VecF<8> { typedef float T __attribute__((ext_vector_type(8))); };
-
-// a per-thread run of the master state: st_wt takes 4-, 8- and 16-B pieces; 32-B runs go as two
-template <typename V>
-__device__ __forceinline__ void st_state(float* base, int64_t idx, V v) {
-  if constexpr (sizeof(V) == 32) {
-    st_wt(base, (size_t)idx * 4, f32x4{v[0], v[1], v[2], v[3]});
-    st_wt(base, (size_t)(idx + 4) * 4, f32x4{v[4], v[5], v[6], v[7]});
-  } else {
-    st_wt(base, (size_t)idx * 4, v);
-  }
-}
 
 // The fp32 master state of weights (o, i..i+EPT-1) of layer L (padded coordinates), loaded before
 // the gradient exists (it does not depend on it) so the epilogue is arithmetic and stores only.
@@ -202,9 +190,9 @@ __device__ __forceinline__ typename VecF<EPT>::T applyn(PreN<EPT> s, typename Ve
           mv[c] = s.m[c];
           vv[c] = s.v[c];
         }
-        st_state(a.params, s.base, pv);
-        st_state(a.m, s.base, mv);
-        st_state(a.v, s.base, vv);
+        st_wt(a.params, (size_t)s.base * 4, pv);
+        st_wt(a.m, (size_t)s.base * 4, mv);
+        st_wt(a.v, (size_t)s.base * 4, vv);
       }
     } else {
 #pragma unroll
@@ -337,31 +325,29 @@ __device__ __forceinline__ void store_operands(const LayerDev& L, int o0, int i0
   }
 }
 
-// Shared by wgrad_kernel and param_kernel.  The tile is 32·MI outputs × 32·NI inputs; thread
+// Shared by wgrad_kernel and param_kernel.  The tile is 32 outputs × 32·NI inputs; thread
 // (o = tid/TPR, i = EPT·(tid%TPR)), TPR = 32·NI/EPT, owns the gradient g of weights
-// (o0+o, i0+i..+EPT-1) (state st from loadn); threads < 32·MI own bias o0+tid (tiles with i0 == 0).
-// wt: an LDS tile image (32·MI rows of 32·NI + 4 floats) the caller no longer needs.  Every thread
-// of the block calls it (barrier inside).
-// returns (threads < 32·MI of a tile with i0 == 0) the new padded bias value, else 0
-template <typename T, int MODE, int NTHR, int EPT, int NI = 1, int MI = 1>
+// (o0+o, i0+i..+EPT-1) (state st from loadn); threads < 32 own bias o0+tid (tiles with i0 == 0).
+// wt: an LDS tile image (32 rows of 32·NI + 4 floats) the caller no longer needs.  Every thread of
+// the block calls it (barrier inside).
+// returns (threads < 32 of a tile with i0 == 0) the new padded bias value, else 0
+template <typename T, int MODE, int NTHR, int EPT, int NI = 1>
 __device__ __forceinline__ float tile_epilogue(const LayerDev& L, int o0, int i0, const PreN<EPT>& st, const PreB& sb,
                                               typename VecF<EPT>::T g, float db, const AdamArgs& aa, float* wt) {
   using V = typename VecF<EPT>::T;
   constexpr int TW = 32 * NI, LD = TW + 4, TPR = TW / EPT;  // tile width, image row stride, threads per row
   const int tid = threadIdx.x, o = tid / TPR, iv = (tid % TPR) * EPT;
   V w = {};
-  if (tid < 32 * MI * TPR) w = applyn<MODE, EPT>(st, g, aa);
+  if (tid < 32 * TPR) w = applyn<MODE, EPT>(st, g, aa);
   WSTAMP(4);
   float nb = 0.f;
-  if (i0 == 0 && tid < 32 * MI) nb = apply_bias<MODE>(L, o0 + tid, sb, db, aa);
+  if (i0 == 0 && tid < 32) nb = apply_bias<MODE>(L, o0 + tid, sb, db, aa);
   if (MODE == PM_GRAD || (CVAE_DIAG_NOWPACK && MODE == PM_ADAM)) return nb;
-  if (tid < 32 * MI * TPR) *(V*)(wt + o * LD + iv) = w;
+  if (tid < 32 * TPR) *(V*)(wt + o * LD + iv) = w;
   __syncthreads();
   WSTAMP(5);
 #pragma unroll
-  for (int r = 0; r < MI; ++r)
-#pragma unroll
-    for (int s = 0; s < NI; ++s) store_operands<T, NTHR, LD>(L, o0 + 32 * r, i0 + 32 * s, wt + 32 * r * LD + 32 * s);
+  for (int s = 0; s < NI; ++s) store_operands<T, NTHR, LD>(L, o0, i0 + 32 * s, wt + 32 * s);
   WSTAMP(6);
   return nb;
 }
@@ -421,10 +407,10 @@ __device__ void finish_loss(const LossArgs& l, int S, int D, int Z) {
 constexpr int WG_NW = 8, WG_THREADS = 64 * WG_NW;
 
 // LDS of one dW workgroup for tiles up to 32·NI inputs wide
-template <int NI, int MI = 1>
+template <int NI>
 struct WgradLds {
-  float red[WG_NW * 32 * MI * (32 * NI + 4)];  // per-wave partial tiles, then the new weights' image
-  float dbp[WG_NW * 32 * MI];                  // per-wave bias partials
+  float red[WG_NW * 32 * (32 * NI + 4)];  // per-wave partial tiles, then the new weights' image
+  float dbp[WG_NW * 32];                  // per-wave bias partials
 };
 
 // Split-K over the batch (large batches): split sk.s of sk.S computes the tile's partial dW/db over
@@ -512,46 +498,41 @@ __device__ __forceinline__ void mx_dw_chunk(const __bf16* G, const __bf16* X, in
 // One workgroup = tile td of layer L: 32 outputs × 32·NI inputs (NI = 2: two 32-wide input tiles
 // sharing the G rows).  loss_block: this workgroup also finishes the loss (S, D, Z: its shape).
 // MXW (NI = 2 only): the MX dW (mx_dw_chunk) in place of the bf16 MFMA loop; Bk % 128 == 0.
-// MI = 2: 64-output tiles (BASELINE cfg5's widewgrad64_kernel: one workgroup per CU, 8 operand
-// vectors per chunk in flight twice, 16 accumulators; no peer exchange, no MX dW)
-template <typename T, int MODE, int NI = 1, bool MXW = false, int MI = 1>
+template <typename T, int MODE, int NI = 1, bool MXW = false>
 __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td, int Bk, AdamArgs aa,
                                            const LossArgs& la, bool loss_block, int S, int D, int Z,
                                            float* red, float* dbp, SplitK sk = SplitK{1, 0, nullptr, nullptr, 0},
                                            const PeerArgs* px = nullptr) {
-  static_assert(!MXW || (NI == 2 && MI == 1 && std::is_same<T, __bf16>::value), "the MX dW: bf16 arena, 32 × 64 tiles");
+  static_assert(!MXW || (NI == 2 && std::is_same<T, __bf16>::value), "the MX dW: bf16 arena, 32 × 64 tiles");
   using V = typename Op<T>::V;
   constexpr int EPL = Op<T>::EPL, KC = Op<T>::KC;
   constexpr int NX = 2 * NI, TW = 32 * NI, LD = TW + 4;  // X fragments per chunk, tile width, image stride
-  constexpr int NM = 2 * MI, OR = 32 * MI;               // G fragments per chunk, tile rows (outputs)
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int r16 = lane & 15, kq = (lane >> 4) * EPL;
   const T* G = (const T*)L.gT;
   const T* X = (const T*)L.xT;
   const bool bias_tile = td.i0 == 0;
-  // epilogue ownership: EPT = 2·NI·MI weights per thread, all 512 threads (Adam's correctly rounded
+  // epilogue ownership: EPT = 2·NI weights per thread, all 512 threads (Adam's correctly rounded
   // sqrt and two divisions per weight are the epilogue's cost)
-  constexpr int EPT = 2 * NI * MI, TPR = TW / EPT;
+  constexpr int EPT = 2 * NI, TPR = TW / EPT;
   using VE = typename VecF<EPT>::T;
   const int o = tid / TPR, iv = (tid % TPR) * EPT;
 
   WSTAMP(0);
   const adam_f32x2 t_step = MODE == PM_ADAM ? adam_step_load(aa) : adam_f32x2{0.f, 0.f};
-  f32x4 acc[NM][NX];
+  f32x4 acc[2][NX];
 #pragma unroll
-  for (int m = 0; m < NM; ++m)
+  for (int m = 0; m < 2; ++m)
 #pragma unroll
     for (int n = 0; n < NX; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float gs[NM];  // bias partials: Σ of this lane's G fragment elements
-#pragma unroll
-  for (int m = 0; m < NM; ++m) gs[m] = 0.f;
+  float gs[2] = {0.f, 0.f};  // bias partials: Σ of this lane's G fragment elements
   // tile-major arena (aoff): this lane's 16-B pieces of rows o / i at batch offset kq of a chunk;
   // one chunk of KC batch rows advances KC/16 row tiles = (KC/16)·Kf·16 elements
   const int Kg = L.Np, Kx = L.Kp;
-  const T* gp[NM];
+  const T* gp[2];
   const T* xp[NX];
 #pragma unroll
-  for (int m = 0; m < NM; ++m) gp[m] = G + aoff(td.o0 + m * 16 + r16, kq, Kg);
+  for (int m = 0; m < 2; ++m) gp[m] = G + aoff(td.o0 + m * 16 + r16, kq, Kg);
 #pragma unroll
   for (int n = 0; n < NX; ++n) xp[n] = X + aoff(td.i0 + n * 16 + r16, kq, Kx);
   // this split's chunk range [c0, c0 + nk) (split-K; the whole batch when S == 1); this wave's
@@ -562,12 +543,12 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
   const int nmine = nk > wave ? (nk - wave + WG_NW - 1) / WG_NW : 0;
   // chunks in flight per wave: 4; 2 for 32 × 64 tiles, whose 6 operand vectors per chunk would
   // otherwise take the kernel past 128 VGPRs (one workgroup per CU instead of two)
-  constexpr int PF = NI == 2 || MI == 2 ? 2 : 4;
-  V ga[PF][NM], xb[PF][NX];
+  constexpr int PF = NI == 2 ? 2 : 4;
+  V ga[PF][2], xb[PF][NX];
   auto load = [&](int u, int j) {  // unconditional, clamped to this wave's last chunk
     const size_t ct = (size_t)(c0 + wave + WG_NW * min(j, nmine > 0 ? nmine - 1 : 0)) * (KC / 16) * 16;
 #pragma unroll
-    for (int m = 0; m < NM; ++m) ga[u][m] = gld<V>(gp[m] + ct * Kg);
+    for (int m = 0; m < 2; ++m) ga[u][m] = gld<V>(gp[m] + ct * Kg);
 #pragma unroll
     for (int n = 0; n < NX; ++n) xb[u][n] = gld<V>(xp[n] + ct * Kx);
   };
@@ -578,8 +559,8 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
   PreN<EPT> st = {};
   PreB sb = {0.f, 0.f, 0.f, -1};
   if (!MXW) {
-    if (tid < OR * TPR) st = loadn<MODE, EPT>(L, td.o0 + o, td.i0 + iv, aa);
-    if (bias_tile && tid < OR) sb = loadb<MODE>(L, td.o0 + tid, aa);
+    if (tid < 32 * TPR) st = loadn<MODE, EPT>(L, td.o0 + o, td.i0 + iv, aa);
+    if (bias_tile && tid < 32) sb = loadb<MODE>(L, td.o0 + tid, aa);
   }
   if constexpr (MXW) {
     if (MODE == PM_ADAM) adam_resolve(aa, t_step);
@@ -601,12 +582,12 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
       const int j = j0 + u;
       if (j < nmine) {
 #pragma unroll
-        for (int m = 0; m < NM; ++m)
+        for (int m = 0; m < 2; ++m)
 #pragma unroll
           for (int n = 0; n < NX; ++n) acc[m][n] = mfma_chunk(ga[u][m], xb[u][n], acc[m][n]);
         if (bias_tile) {
 #pragma unroll
-          for (int m = 0; m < NM; ++m)
+          for (int m = 0; m < 2; ++m)
 #pragma unroll
             for (int e = 0; e < EPL; ++e) gs[m] += (float)ga[u][m][e];
         }
@@ -617,34 +598,33 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
   }
   }  // bf16 loop
   WSTAMP(1);
-  float* rw = red + wave * OR * LD;
+  float* rw = red + wave * 32 * LD;
 #pragma unroll
-  for (int m = 0; m < NM; ++m)
+  for (int m = 0; m < 2; ++m)
 #pragma unroll
     for (int n = 0; n < NX; ++n)
 #pragma unroll
       for (int i = 0; i < 4; ++i) rw[(m * 16 + (lane >> 4) * 4 + i) * LD + n * 16 + r16] = acc[m][n][i];
   if (bias_tile) {
 #pragma unroll
-    for (int m = 0; m < NM; ++m) {
+    for (int m = 0; m < 2; ++m) {
       gs[m] += __shfl_xor(gs[m], 16, 64);
       gs[m] += __shfl_xor(gs[m], 32, 64);
-      if (lane < 16) dbp[wave * OR + m * 16 + lane] = gs[m];
+      if (lane < 16) dbp[wave * 32 + m * 16 + lane] = gs[m];
     }
   }
   __syncthreads();
   WSTAMP(2);
   VE g4 = {};
-  if (tid < OR * TPR) {
+  if (tid < 32 * TPR) {
 #pragma unroll
-    for (int w = 0; w < WG_NW; ++w) g4 += *(const VE*)(red + w * OR * LD + o * LD + iv);
+    for (int w = 0; w < WG_NW; ++w) g4 += *(const VE*)(red + w * 32 * LD + o * LD + iv);
   }
   float db = 0.f;
-  if (bias_tile && tid < OR) {
+  if (bias_tile && tid < 32) {
 #pragma unroll
-    for (int w = 0; w < WG_NW; ++w) db += dbp[w * OR + tid];
+    for (int w = 0; w < WG_NW; ++w) db += dbp[w * 32 + tid];
   }
-  if constexpr (MI == 1) {
   if (px) {  // peer exchange (cvae_peer.h): PM_GRAD = a non-owner's tile, PM_ADAM = the owner's
     if (MODE == PM_GRAD) {
       px_push(*px, sk.tile, o, iv, g4, db, bias_tile);
@@ -657,12 +637,11 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
       db = db * aa.grad_scale;
     }
   }
-  }
   if (sk.S > 1) {  // split-K: publish this split's partial; the last of the S blocks finishes the tile
-    const int PW = sk.pw ? sk.pw : OR * TW + OR;
-    static_assert(EPT % 2 == 0, "partial vectors of 8-B pieces");
+    const int PW = sk.pw ? sk.pw : 32 * TW + 32;
+    static_assert(EPT == 2 || EPT == 4, "partial vectors of 8 or 16 B");
     float* mine = sk.ws + ((size_t)sk.tile * sk.S + sk.s) * PW;
-    if (tid < OR * TPR) {
+    if (tid < 32 * TPR) {
       if constexpr (EPT == 2)
         __hip_atomic_store((uint64_t*)(mine + o * TW + iv), __builtin_bit_cast(uint64_t, g4), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
@@ -672,8 +651,8 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
                              __builtin_bit_cast(uint64_t, VecF<2>::T{g4[c], g4[c + 1]}), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (bias_tile && tid < OR)
-      __hip_atomic_store((unsigned*)(mine + OR * TW + tid), __builtin_bit_cast(unsigned, db), __ATOMIC_RELAXED,
+    if (bias_tile && tid < 32)
+      __hip_atomic_store((unsigned*)(mine + 32 * TW + tid), __builtin_bit_cast(unsigned, db), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
     // the hand-off in MI355X_MICROARCH.md's sc1 form (its table of valid hand-offs, first row):
     // every partial store above is sc1 (relaxed agent-scope atomic stores), every storing wave
@@ -695,7 +674,7 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
     db = 0.f;
     for (int k = 0; k < sk.S; ++k) {
       const float* pk = sk.ws + ((size_t)sk.tile * sk.S + k) * PW;
-      if (tid < OR * TPR) {
+      if (tid < 32 * TPR) {
 #pragma unroll
         for (int c = 0; c < EPT; c += 2) {
           const uint64_t u = __hip_atomic_load((const uint64_t*)(pk + o * TW + iv + c), __ATOMIC_RELAXED,
@@ -705,16 +684,15 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
           g4[c + 1] += v2[1];
         }
       }
-      if (bias_tile && tid < OR)
-        db += __builtin_bit_cast(float, __hip_atomic_load((const unsigned*)(pk + OR * TW + tid), __ATOMIC_RELAXED,
+      if (bias_tile && tid < 32)
+        db += __builtin_bit_cast(float, __hip_atomic_load((const unsigned*)(pk + 32 * TW + tid), __ATOMIC_RELAXED,
                                                           __HIP_MEMORY_SCOPE_AGENT));
     }
     if (tid == 0) sk.tickets[sk.tile] = 0u;  // every split has added: reset for the next launch
   }
   __syncthreads();  // red becomes the image of the new weights
-  const float nb = tile_epilogue<T, MODE, WG_THREADS, EPT, NI, MI>(L, td.o0, td.i0, st, sb, g4, db, aa, red);
-  if constexpr (MI == 1)
-    if (MODE == PM_ADAM && px) px_broadcast<T, WG_THREADS>(*px, L, td.o0, td.i0, red, nb);
+  const float nb = tile_epilogue<T, MODE, WG_THREADS, EPT, NI>(L, td.o0, td.i0, st, sb, g4, db, aa, red);
+  if (MODE == PM_ADAM && px) px_broadcast<T, WG_THREADS>(*px, L, td.o0, td.i0, red, nb);
 #if CVAE_DIAG_STAMPS
   __syncthreads();
   WSTAMP(3);

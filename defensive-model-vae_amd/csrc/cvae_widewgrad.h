@@ -142,85 +142,4 @@ __global__ __launch_bounds__(WG_THREADS, 4) void widewgrad_kernel(char* arena, f
     wgrad_body<__bf16, MODE, 1>(L, td, Bk, aa, la, false, A::S, A::D, A::Z, sh.red, sh.dbp, sk);
 }
 
-// ---- 64-output tiles (round 5): every layer whose padded N is a multiple of 64 takes 64 × 64 tiles
-// (64 × 32 where the padded K is 32: the condition layer), so BASELINE cfg5's 436 32 × 64 tiles
-// become 218 — one per CU, none doubled, and a G row is read by half as many tiles (the dW's operand
-// traffic through L2 −32 %).  One workgroup per CU (139 KB of cross-wave partials); the K split, the
-// MFMA order and the fixed-order cross-wave sum are those of the 32-output tiles, so the gradients
-// and the Adam update are bit-identical to widewgrad_kernel's.  Same list order as WTiles (layer
-// by layer, the longer dimension outermost, XCD chunks).  Split-K launches keep widewgrad_kernel.
-template <class A>
-struct WTiles64 {
-  static constexpr int NL = A::NL;
-  __host__ __device__ static constexpr int ni(int l) { return A::Kp(l) % 64 == 0 && l != A::LCE ? 2 : 1; }
-  __host__ __device__ static constexpr int mi(int l) { return A::Np(l) % 64 == 0 ? 2 : 1; }
-  __host__ __device__ static constexpr int count(int l) { return (A::Np(l) / (32 * mi(l))) * (A::Kp(l) / (32 * ni(l))); }
-  __host__ __device__ static constexpr int start(int l) {
-    int t = 0;
-    for (int k = 0; k < l; ++k) t += count(k);
-    return t;
-  }
-  __host__ __device__ static constexpr int total() { return start(NL); }
-  __host__ __device__ static constexpr int log2i(int v) { return v <= 1 ? 0 : 1 + log2i(v / 2); }
-  __host__ __device__ static constexpr bool i_outer(int l) { return A::Kp(l) > A::Np(l); }
-  __host__ __device__ static constexpr int inner(int l) {
-    return i_outer(l) ? A::Np(l) / (32 * mi(l)) : A::Kp(l) / (32 * ni(l));
-  }
-  __host__ __device__ static constexpr bool uniform_mi() {
-    for (int l = 0; l < NL; ++l)
-      if (mi(l) != 2) return false;
-    return true;
-  }
-  __host__ __device__ static constexpr bool pow2_inner() {
-    for (int l = 0; l < NL; ++l)
-      if (inner(l) & (inner(l) - 1)) return false;
-    return true;
-  }
-  static_assert(pow2_inner() && uniform_mi(), "64-row tiles on every layer; power-of-two inner tile counts");
-  __host__ __device__ static TileDesc at(int b) {
-    constexpr int NTL = total(), q = NTL / 8, r = NTL % 8;
-    const int x = b & 7, j = b >> 3;
-    const int s = x * q + (x < r ? x : r) + j;
-#ifdef __HIP_DEVICE_COMPILE__
-    int l = 0;
-#pragma unroll
-    for (int k = 1; k < NL; ++k) l += s >= start(k) ? 1 : 0;
-    const int loc = s - (int)fchain::pick<NL>(l, [](int k) { return (int64_t)start(k); });
-    const int sh = (int)fchain::pick<NL>(l, [](int k) { return (int64_t)log2i(inner(k)); });
-    const bool io = fchain::pick<NL>(l, [](int k) { return (int64_t)i_outer(k); }) != 0;
-    const int n = (int)fchain::pick<NL>(l, [](int k) { return (int64_t)ni(k); });
-    const int a = loc >> sh, c = loc & ((1 << sh) - 1);
-    return TileDesc{l, 64 * (io ? c : a), 32 * n * (io ? a : c), n};
-#else
-    int l = 0;
-    while (l + 1 < NL && s >= start(l + 1)) ++l;
-    const int loc = s - start(l), a = loc / inner(l), c = loc % inner(l);
-    return TileDesc{l, 64 * (i_outer(l) ? c : a), 32 * ni(l) * (i_outer(l) ? a : c), ni(l)};
-#endif
-  }
-};
-
-// grid = WTiles64 total + 1 (the last block finishes the loss); one workgroup per CU
-template <class A, int MODE>
-__global__ __launch_bounds__(WG_THREADS, 2) void widewgrad64_kernel(char* arena, float* params, float* mst,
-                                                                  float* vst, int Bp, int Bk, AdamArgs a, LossArgs la) {
-  AdamArgs aa = a;
-  aa.params = params;
-  aa.m = mst;
-  aa.v = vst;
-  constexpr int NTL = WTiles64<A>::total();
-  if ((int)blockIdx.x == NTL) {
-    if (threadIdx.x < 64 && la.partials) finish_loss(la, A::S, A::D, A::Z);
-    return;
-  }
-  __shared__ __attribute__((aligned(16))) WgradLds<2, 2> sh;
-  const SplitK sk{1, 0, nullptr, nullptr, (int)blockIdx.x, 0};
-  const TileDesc td = WTiles64<A>::at(blockIdx.x);
-  const LayerDev L = wide_layer<A>(td.layer, arena, Bp);
-  if (td.ni == 2)  // block-uniform
-    wgrad_body<__bf16, MODE, 2, false, 2>(L, td, Bk, aa, la, false, A::S, A::D, A::Z, sh.red, sh.dbp, sk);
-  else
-    wgrad_body<__bf16, MODE, 1, false, 2>(L, td, Bk, aa, la, false, A::S, A::D, A::Z, sh.red, sh.dbp, sk);
-}
-
 }  // namespace wchain

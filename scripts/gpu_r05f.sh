@@ -13,3 +13,8 @@ for r in 1 2; do
   CVAE_DW64=0 $B > $O/wbf16_32_$r.json 2> $O/wbf16_32_$r.err || { tail -5 $O/*.err; exit 1; }
 done
 for f in $O/*.json; do python3 -c "import json;d=json.load(open('$f'));r=d['roofline'];print('$f',d['value'],d['ms_per_step'],r.get('kernels_ms'))"; done
+for r in 1 2; do
+  CVAE_LIB=$GRAFT_REPO_ROOT/build/ab/pf4.so $B --dtype fp8 > $O/wfp8_64pf4_$r.json 2> $O/wfp8_64pf4_$r.err &&
+  $B --dtype fp8 > $O/wfp8_64b_$r.json 2> $O/wfp8_64b_$r.err || { tail -5 $O/*.err; exit 1; }
+done
+for f in $O/wfp8_64*.json; do python3 -c "import json;d=json.load(open('$f'));r=d['roofline'];print('$f',d['value'],d['ms_per_step'],r.get('kernels_ms'))"; done

@@ -767,8 +767,8 @@ def test_wide_chain_matches_generic_and_emulation(cvae, monkeypatch, B):
 def test_wide_chain_repeatable_and_dw_tiles_bit_equal(cvae, monkeypatch, dtype, B):
     """The wide chain is race-free: eight forward_backward calls on the same input give bit-equal
     gradients and losses (an inline-asm store hazard once corrupted whole gradient columns in
-    14-22 of 40 calls).  The dW launch's 64 x 64 tiles (the default, widewgrad64_kernel), its
-    32 x 64 tiles (CVAE_DW64=0), the generic kernel over them (CVAE_GENERIC_DW=1) and 32 x 32 tiles
+    14-22 of 40 calls).  The dW launch's 32 x 64 tiles (the default for this long tile list:
+    widewgrad_kernel), the generic kernel over them (CVAE_GENERIC_DW=1) and 32 x 32 tiles
     (CVAE_DW_NI2=0) give the same bits: each element is the same K sum in the same chunk order and
     the same fixed-order cross-wave sum.  B = 1000: a ragged last row tile."""
     ref, m, eng, x, eps = _wide(cvae, dtype, B)
@@ -789,7 +789,7 @@ def test_wide_chain_repeatable_and_dw_tiles_bit_equal(cvae, monkeypatch, dtype, 
     # the compile-time tile decode of the wide shape (widewgrad_kernel, the default), the generic
     # kernel over the same 32 x 64 tile list (CVAE_GENERIC_DW=1) and 32 x 32 tiles (CVAE_DW_NI2=0)
     fresh = []
-    for env in (None, ("CVAE_DW64", "0"), ("CVAE_DW_NI2", "0"), ("CVAE_GENERIC_DW", "1")):
+    for env in (None, ("CVAE_DW_NI2", "0"), ("CVAE_GENERIC_DW", "1")):
         if env:
             monkeypatch.setenv(*env)
         mm = cvae.ConditionalTrajectoryVAE(WIDE["S"], WIDE["D"], WIDE["Z"], 128, WIDE["n_enc"], WIDE["n_dec"])
