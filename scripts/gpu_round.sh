@@ -5,7 +5,7 @@
 # (SQ instruction mix, HBM traffic, L2 hit/miss).  Every GPU step has its own limit; the script
 # stops at the first failure.  SKIP_TESTS=1 skips the suite; PASSES overrides the PMC pass list.
 set -u
-T=${TAG:-r04x}
+T=${TAG:-r05x}
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$T
 mkdir -p $OUT
 cd $GRAFT_REPO_ROOT
@@ -24,12 +24,17 @@ $B --steps 200 --warmup 20 --dp --buckets 2 > $OUT/bench_dp_b2.json 2> $OUT/benc
 $B --steps 200 --warmup 20 --workload cfg4 > $OUT/bench_cfg4.json 2> $OUT/bench_cfg4.err &&
 $B --steps 100 --warmup 10 --workload wide > $OUT/bench_wide_bf16.json 2> $OUT/bench_wide_bf16.err &&
 $B --steps 100 --warmup 10 --workload wide --dtype fp8 > $OUT/bench_wide_fp8.json 2> $OUT/bench_wide_fp8.err &&
+CVAE_FP8_DW=mx $B --steps 100 --warmup 10 --workload wide --dtype fp8 > $OUT/bench_wide_fp8_mxdw.json 2> $OUT/bench_wide_fp8_mxdw.err &&
 timeout -k 10 180 python3 bench.py --workload cfg1 --steps 50 --warmup 5 > $OUT/bench_cfg1.json 2> $OUT/bench_cfg1.err || { tail -5 $OUT/*.err; exit 1; }
-for n in 2 4; do
-  CVAE_BENCH_SHARE_GPU=1 CVAE_PX_TIMEOUT_MS=30000 timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 \
-    --nproc-per-node $n --master-addr 127.0.0.1 --master-port 2958$n bench.py --gpus $n --steps 20 --warmup 5 \
+# the N > 1 path rehearsed on the one GPU: bench.py starting its own N ranks (the plain --gpus N form),
+# and once under torch.distributed.run (the driver's form)
+for n in 2 4 8; do
+  CVAE_BENCH_SHARE_GPU=1 CVAE_PX_TIMEOUT_MS=30000 timeout -k 10 400 python3 bench.py --gpus $n --steps 20 --warmup 5 \
     > $OUT/bench_share$n.json 2> $OUT/bench_share$n.err || { tail -5 $OUT/bench_share$n.err; exit 1; }
 done
+CVAE_BENCH_SHARE_GPU=1 CVAE_PX_TIMEOUT_MS=30000 timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 \
+  --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29582 bench.py --gpus 2 --steps 20 --warmup 5 \
+  > $OUT/bench_share2_torchrun.json 2> $OUT/bench_share2_torchrun.err || { tail -5 $OUT/bench_share2_torchrun.err; exit 1; }
 for f in $OUT/bench_*.json; do python3 -c "import json;d=json.load(open('$f'));r=d['roofline'];print('$f',d['value'],d['ms_per_step'],r.get('kernels_ms'),r['frac'])"; done
 [ "${SKIP_PROF:-0}" = 1 ] && exit 0
 # kernel trace of the driver's exact command (program directly after --)
