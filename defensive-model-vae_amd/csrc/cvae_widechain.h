@@ -275,17 +275,36 @@ constexpr int kPreFill = 4;
 #endif
 template <class A>
 constexpr int kEpsProWide = A::F8 ? CVAE_DIAG_EPS_PRO_F8 : 0;
-// one 16-B piece of fragment item at byte offset `off` from the arena base.  bf16: a
-// buffer load — lane·16 is a loop-invariant voffset, the item's offset a scalar soffset (2-3 SALU
-// per item); the 64-bit global address cost 3 VALU (one a 64-bit shift-add) + ~7 SALU per item
-// (cfg2 step 26.6 -> 26.0 us, profiles/r03g).  Not in the e4m3 form (F8): there the buffer-load
-// build failed the wide fp8 chain's run-to-run repeatability test (two runs of two, the global-load
-// build passing), cause not found.  F8: global loads with a scalar 64-bit base
-// and a 32-bit lane offset where the compiler keeps that form (2 SALU, 0 VALU per item): chain
-// 41.4 -> 40.5 us at cfg5 fp8, repeatability tests green (profiles/r03g/saddr_ab.txt)
+// one 16-B piece of fragment item at byte offset `off` from the arena base: a buffer load — lane·16
+// is a loop-invariant voffset, the item's offset a scalar soffset (2-3 SALU per item); the 64-bit
+// global address cost 3 VALU (one a 64-bit shift-add) + ~7 SALU per item (cfg2 step 26.6 -> 26.0
+// us, profiles/r03g).  The e4m3 form needs the pad below (f8_pad): rounds 3-4 found its buffer-load
+// build not repeatable and kept global loads with a scalar base (CVAE_F8_BUFLOAD=0; chain 41.4 ->
+// 40.5 us then, profiles/r03g/saddr_ab.txt) — round 5 found the cause
+// The e4m3 form's fragments are buffer loads too, with CVAE_F8_MFMA_PAD wait states between each
+// e4m3 MFMA and the refill load that reuses its B operand's ring registers (round 5).  Without the pad
+// the buffer-load build is not repeatable: 300 of 300 forward_backward calls differ
+// (scripts/repeat_check.py, profiles/r05i/) — the refill's data lands in registers an e4m3 MFMA
+// queued behind its predecessors has not read yet, a hazard hipcc does not pad for these
+// instructions; with 16 states 0 of 300 differ.  The scalar-base global-load form (CVAE_F8_BUFLOAD=0)
+// spends ~8 SALU and a 64-bit VALU add on each item's address, which happened to cover the hazard
+// (0 of 300); buffer loads + pad run the chain 0.2 us faster.
+#ifndef CVAE_F8_BUFLOAD
+#define CVAE_F8_BUFLOAD 1
+#endif
+#ifndef CVAE_F8_MFMA_PAD
+#define CVAE_F8_MFMA_PAD 16
+#endif
+// CVAE_F8_MFMA_PAD wait states after an e4m3 MFMA, before the refill load that reuses its operand registers
+__device__ __forceinline__ void f8_pad() {
+  if constexpr (CVAE_F8_MFMA_PAD > 0) {
+    asm volatile("s_nop %0" ::"n"(CVAE_F8_MFMA_PAD > 8 ? 7 : CVAE_F8_MFMA_PAD - 1));
+    if constexpr (CVAE_F8_MFMA_PAD > 8) asm volatile("s_nop %0" ::"n"(CVAE_F8_MFMA_PAD - 9));
+  }
+}
 template <bool F8>
 __device__ __forceinline__ bf16x8 wload(const char* AR, int64_t off, int lane) {
-  if constexpr (!F8) {
+  if constexpr (!F8 || CVAE_F8_BUFLOAD) {
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)AR, (short)0, 0x7fffffff, 0x00020000);
     return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, (int)off, 0));
   } else {  // global_load with a scalar base + a 32-bit lane offset
@@ -420,6 +439,7 @@ __device__ __forceinline__ void gemm(Ring<P>& ring, const void* img, f32x4 (&acc
         constexpr int u = decltype(t)::value, g0 = G0 + (c - 1) * TS + u, g = G0 + c * TS + u;
         acc[u] = mx2(xe, xf, ring.r[g0 % P], ring.r[g % P], acc[u]);
         asm volatile("" : "+v"(acc[u]));  // MFMA before the refills, as below
+        f8_pad();
         ring_load<A, P, g0 + P>(ring, AR, wave, lane);
         ring_load<A, P, g + P>(ring, AR, wave, lane);
       });
@@ -431,6 +451,7 @@ __device__ __forceinline__ void gemm(Ring<P>& ring, const void* img, f32x4 (&acc
       // step's refills first and sinks its MFMA chains, and every ring slot then needs a second
       // register (spills).
       asm volatile("" : "+v"(acc[u]));
+      if constexpr (F8) f8_pad();
       ring_load<A, P, g + P>(ring, AR, wave, lane);
     });
     side(kc);
@@ -464,6 +485,7 @@ __device__ __forceinline__ void gemm_grouped(Ring<P>& ring, const void* img, con
           constexpr int u = decltype(i)::value, g0 = G0 + (p * KC + c - 1) * GS + u, g = G0 + (p * KC + c) * GS + u;
           acc[u] = mx2(xf[c - 1], xf[c], ring.r[g0 % P], ring.r[g % P], acc[u]);
           asm volatile("" : "+v"(acc[u]));
+          f8_pad();
           ring_load<A, P, g0 + P>(ring, AR, wave, lane);
           ring_load<A, P, g + P>(ring, AR, wave, lane);
         });
@@ -560,6 +582,7 @@ __device__ __forceinline__ void gemm_mxb(Ring<P>& ring, const char* twin, f32x4 
       constexpr int u = decltype(t)::value, ga = G0 + p0 * TS + u, gb = G0 + (two ? p1 : p0) * TS + u;
       acc[u] = mx2s(x0, x1, ring.r[ga % P], ring.r[gb % P], acc[u], sa, sb);
       asm volatile("" : "+v"(acc[u]));  // MFMA before the refills (as gemm)
+      f8_pad();
       ring_load<A, P, ga + P>(ring, AR, wave, lane);
       if constexpr (two) ring_load<A, P, gb + P>(ring, AR, wave, lane);
     });

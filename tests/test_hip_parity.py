@@ -807,6 +807,23 @@ def test_wide_chain_repeatable_and_dw_tiles_bit_equal(cvae, monkeypatch, dtype, 
         assert torch.equal(a3.loss, a4.loss) and torch.equal(a3.counters, a4.counters)
 
 
+def test_wide_fp8_chain_repeatable_stress(cvae):
+    """200 forward_backward calls of the e4m3 wide chain on one input give the same bits.  Its
+    weight fragments are buffer loads with a 16-state pad after every e4m3 MFMA (f8_pad,
+    cvae_widechain.h): without the pad every call differed (the refill load wrote ring registers a
+    queued e4m3 MFMA had not read yet; scripts/repeat_check.py, profiles/r05i/)."""
+    ref, m, eng, x, eps = _wide(cvae, "fp8", 64)
+    xd = x.to("cuda", torch.bfloat16)
+    l0 = eng.forward_backward(xd, eps=eps).clone()
+    g0 = eng.grads.clone()
+    bad = 0
+    for _ in range(200):
+        l = eng.forward_backward(xd, eps=eps)
+        bad += 0 if torch.equal(l, l0) and torch.equal(eng.grads, g0) else 1
+    torch.cuda.synchronize()
+    assert bad == 0, f"{bad} of 200 calls differ"
+
+
 @pytest.mark.parametrize("dtype", ["bf16", "fp8"])
 def test_wide_dw_decode_split_k_equals_generic(cvae, monkeypatch, dtype):
     """B = 8192 at the cfg5 shape: the dW launch splits K (the batch) over 4 blocks per tile with the
