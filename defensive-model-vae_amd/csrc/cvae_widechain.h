@@ -807,45 +807,44 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   // x_f32 (CVAE_X_F32: real data with ~200 m absolute coordinates): fp32 rows, the start point
   // subtracted in fp32 and the relative offsets rounded to bf16 once
   {
-    constexpr int U = (R * A::NKI * 4 + NT - 1) / NT;  // 16-B vectors per thread
-    constexpr int VPR = I / 8, NV = R * VPR;
+    // Task = one timestep pair (12 features: 24 B of a bf16 row, 48 B of an fp32 row) of the four
+    // rows of one row quad: the thread holds all 4 rows of every feature it writes, so the
+    // feature-major image is a register transpose (v_perm / v_cvt_pk), with no DPP or selects; only
+    // the features with d = 1, 2 are rebased, the rest of a bf16 row are copied bit for bit (x − 0
+    // rounds to x).  Round 5: this was 719 VALU per wave for 16-B row vectors + quad transposes.
+    static_assert(D == 6 && I % 12 == 0, "x_rel transform: 12-feature timestep pairs (D == 6)");
+    constexpr int NKT = I / 12, NTASK = 4 * NKT;  // timestep pairs per row; tasks per tile
+    static_assert(NTASK <= NT, "x_rel transform: one task per thread");
     const int last = max(a.batch - 1, 0);
-    const __bf16* xg = (const __bf16*)a.x;
-    const float* xg32 = (const float*)a.x;
     const bool x32 = a.x_f32 != 0;
-    typedef float f32x8 __attribute__((ext_vector_type(8)));
-    f32x8 xv[U], x0[U];
-    int64_t gr[U];
-    int cc[U];
+    const int xt = min(tid, NTASK - 1), xrq = xt / NKT, xk = xt - xrq * NKT;  // idle threads: task NTASK-1, no store
+    uint32_t xw[4][12];  // row 4xrq + i: dwords of its 12 features (bf16: [0..5])
+    uint32_t xs[4][2];   // its start point x[:,0,1:3] (Training_VAE.py:345): bf16 dwords 0, 1 / fp32 features 1, 2
 #pragma unroll
-    for (int u = 0; u < U; ++u) {  // task v: vector c of row 4rq + (v & 3) — quads = 4 rows, same c
-      const int v = min(u * NT + tid, NV - 1);
-      const int w = v >> 2, rq = w / VPR, c = w - rq * VPR, row = 4 * rq + (v & 3);
-      gr[u] = min(b0 + row, last);
-      cc[u] = c;
-    }
-    if (a.idx) {
+    for (int i = 0; i < 4; ++i) {
+      int64_t g = min(b0 + 4 * xrq + i, last);
+      if (a.idx) g = gld<int64_t>(a.idx + g);
+      if (x32) {  // wave-uniform: before the weight stream starts
+        const uint32_t* const p = (const uint32_t*)a.x + g * I;
 #pragma unroll
-      for (int u = 0; u < U; ++u) gr[u] = gld<int64_t>(a.idx + gr[u]);
-    }
-    if (x32) {  // wave-uniform: before the weight stream starts
+        for (int j = 0; j < 3; ++j) {
+          const u32x4 v = gld<u32x4>(p + 12 * xk + 4 * j);
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const f32x4 lo = gld<f32x4>(xg32 + gr[u] * I + cc[u] * 8), hi = gld<f32x4>(xg32 + gr[u] * I + cc[u] * 8 + 4);
-        const f32x4 s0 = gld<f32x4>(xg32 + gr[u] * I);  // the row's start point x[:,0,1:3] (Training_VAE.py:345)
-        xv[u] = f32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        x0[u] = f32x8{s0[0], s0[1], s0[2], s0[3], 0.f, 0.f, 0.f, 0.f};
-      }
-    } else {
+          for (int e = 0; e < 4; ++e) xw[i][4 * j + e] = v[e];
+        }
+        xs[i][0] = gld<uint32_t>(p + 1);
+        xs[i][1] = gld<uint32_t>(p + 2);
+      } else {
+        const uint32_t* const p = (const uint32_t*)((const __bf16*)a.x + g * I);
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const bf16x8 v = gld<bf16x8>(xg + gr[u] * I + cc[u] * 8);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) xv[u][e] = (float)v[e];
-        // the row's start point x[:,0,1:3] (Training_VAE.py:345): elements 0..3, one 8-B load
-        const bf16x4 v0 = gld<bf16x4>(xg + gr[u] * I);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) x0[u][e] = e < 4 ? (float)v0[e & 3] : 0.f;
+        for (int j = 0; j < 3; ++j) {
+          const u32x2 v = gld<u32x2>(p + 6 * xk + 2 * j);
+          xw[i][2 * j] = v[0];
+          xw[i][2 * j + 1] = v[1];
+        }
+        const u32x2 v0 = gld<u32x2>(p);
+        xs[i][0] = v0[0];
+        xs[i][1] = v0[1];
       }
     }
     // EPS_PRO: the host-eps load right behind the x tile (the x wait then covers it)
@@ -916,34 +915,57 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
       sfor<0, A::NL>([&](auto ll) { f8l = f8l || (A::f8(decltype(ll)::value) && tid == decltype(ll)::value); });
       if (tid < A::NL) INVS[tid] = f8l ? invv : 1.f;
     }
+    if (nrows < R) {  // block-uniform: the batch's last tile; rows past it are zero
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int v = u * NT + tid;
-      if (v < NV) {  // NV % 4 == 0: quads are whole
-        const int w = v >> 2, rq = w / VPR, c = w - rq * VPR;
-        const int qd = lane & 3, f0 = c * 8;
-        const f32x4 xlo = quad_t(f32x4{xv[u][0], xv[u][1], xv[u][2], xv[u][3]});
-        const f32x4 xhi = quad_t(f32x4{xv[u][4], xv[u][5], xv[u][6], xv[u][7]});
-        const float s0 = x0[u][1], s1 = x0[u][2];
-        const f32x4 S0 = fchain::quad_all(s0), S1 = fchain::quad_all(s1);
-        const int fl = f0 + qd, fh = fl + 4;
-        const int dl = fl % D, dh = fh % D;
-        const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-        f32x4 rl = xlo - (dl == 1 ? S0 : dl == 2 ? S1 : zero);
-        f32x4 rh = xhi - (dh == 1 ? S0 : dh == 2 ? S1 : zero);
-        f32x4 cv = qd == 0 ? S0 : qd == 1 ? S1 : zero;
-        if (nrows < R) {
+      for (int i = 0; i < 4; ++i) {
+        const bool live = 4 * xrq + i < nrows;
+#pragma unroll
+        for (int e = 0; e < 12; ++e) xw[i][e] = live ? xw[i][e] : 0u;
+        xs[i][0] = live ? xs[i][0] : 0u;
+        xs[i][1] = live ? xs[i][1] : 0u;
+      }
+    }
+    auto f32 = [](uint32_t u) { return __builtin_bit_cast(float, u); };
+    auto pk = [](float lo, float hi) {  // two fp32 → bf16 (RNE), lo in bits 0..15
+      typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+      return __builtin_bit_cast(uint32_t, bf16x2{(__bf16)lo, (__bf16)hi});
+    };
+    float S0[4], S1[4];  // the rows' start point as fp32
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      S0[i] = x32 ? f32(xs[i][0]) : f32(xs[i][0] & 0xffff0000u);
+      S1[i] = x32 ? f32(xs[i][1]) : f32(xs[i][1] << 16);
+    }
+    if (tid < NTASK) {
+      char* const xb = (char*)XIN + 384 * xk;  // features 12xk .. 12xk+11, 32 B each (ioff)
+      int sw[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) sw[c] = 8 * (xrq ^ ((3 * xk + c) & 3));
+#pragma unroll
+      for (int f = 0; f < 12; ++f) {
+        const int d = f % D;
+        u32x2 o;
+        if (x32 || d == 1 || d == 2) {  // x32 is block-uniform
+          float v[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const bool live = 4 * rq + i < nrows;
-            rl[i] = live ? rl[i] : 0.f;
-            rh[i] = live ? rh[i] : 0.f;
-            cv[i] = live ? cv[i] : 0.f;
+            const float x = x32 ? f32(xw[i][f]) : f32((f & 1) ? (xw[i][f >> 1] & 0xffff0000u) : (xw[i][f >> 1] << 16));
+            v[i] = d == 1 ? x - S0[i] : d == 2 ? x - S1[i] : x;
           }
+          o = u32x2{pk(v[0], v[1]), pk(v[2], v[3])};
+        } else {  // bf16, not rebased: the halves as they are
+          const uint32_t sel = (f & 1) ? 0x07060302u : 0x05040100u;
+          o = u32x2{__builtin_amdgcn_perm(xw[1][f >> 1], xw[0][f >> 1], sel),
+                    __builtin_amdgcn_perm(xw[3][f >> 1], xw[2][f >> 1], sel)};
         }
-        *(bf16x4*)(XIN + ioff(fl, rq)) = to_bf4(rl);
-        *(bf16x4*)(XIN + ioff(fh, rq)) = to_bf4(rh);
-        if (c == 0) *(bf16x4*)(CIN + ioff(qd, rq)) = to_bf4(cv);
+        *(u32x2*)(xb + 32 * f + sw[f >> 2]) = o;
+      }
+      if (xk == 0) {  // the condition input (x, y, 0, 0) of the rows (c_start, :345): CIN features 0..3
+        char* const cb = (char*)CIN + 8 * xrq;
+        *(u32x2*)(cb) = u32x2{pk(S0[0], S0[1]), pk(S0[2], S0[3])};
+        *(u32x2*)(cb + 32) = u32x2{pk(S1[0], S1[1]), pk(S1[2], S1[3])};
+        *(u32x2*)(cb + 64) = u32x2{0u, 0u};
+        *(u32x2*)(cb + 96) = u32x2{0u, 0u};
       }
     }
   }
