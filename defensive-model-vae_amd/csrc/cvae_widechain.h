@@ -855,7 +855,9 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
 #pragma unroll
     for (int k = 0; k < UB; ++k) bv[k] = gld<f32x4>((const float*)(AR + A::bias_base) + 4 * min(k * NT + tid, NB4 - 1));
     float invv = 1.f;  // F8: 1/s of layer tid (F8Scale::inv_s in front of its Wf)
-    if constexpr (A::F8) {  // offsets selected from compile-time constants (a runtime A::wf(tid) is a loop)
+    // wave 0 only (lanes < NL; wave-uniform branch): the selects cost ~50 VALU, on the prologue's
+    // critical path in every wave that ran them
+    if (A::F8 && wave == 0) {  // offsets selected from compile-time constants (a runtime A::wf(tid) is a loop)
       int64_t o = A::bias_base;
       sfor<0, A::NL>([&](auto ll) {
         constexpr int l = decltype(ll)::value;
@@ -910,7 +912,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
       if (tid < R) ((int*)(smem + A::L_CLSID))[tid] = cid;
       if (tid < 2 * A::Np(A::LCE) * A::Kp(A::LCE) / 16) ((u32x4*)(smem + A::L_CTAB))[tid] = tab;
     }
-    if constexpr (A::F8) {
+    if (A::F8 && wave == 0) {
       bool f8l = false;
       sfor<0, A::NL>([&](auto ll) { f8l = f8l || (A::f8(decltype(ll)::value) && tid == decltype(ll)::value); });
       if (tid < A::NL) INVS[tid] = f8l ? invv : 1.f;
@@ -1153,6 +1155,13 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     typedef float f32x2 __attribute__((ext_vector_type(2)));
     const float cr = a.w_recon * 2.f;
     f32x2 sr2 = {0.f, 0.f};
+    // per-lane parts of the epilogue's indices, feature f = 16t + n16 of n-tile t = wave + NW·g: the
+    // image slot ioff(f, q) = 256t + ioff(n16, q) (its swizzle (f >> 2) & 3 = n16 >> 2 for every t)
+    // and the bias 16t + n16 — lane bases plus compile-time LDS offsets; f mod D from the lane's
+    // (16·wave + n16) mod D and the group's (16·NW·g) mod D
+    __bf16* const XIL = XIN + ioff(n16, q) + 256 * wave;
+    const float* const BIL = BIAS + A::bias_off(A::LDL) + 16 * wave + n16;
+    const int dlane = (16 * wave + n16) % D;
     gemm_grouped<A, P, PL::sDL>(ring, opnd(integral_constant<int, PL::sDL>{}, std::conditional_t<((ND - 2) & 1), IA1, IA0>{}), AR, wave, lane, [&](auto gg, f32x4(&accs)[1]) {
       constexpr int g = decltype(gg)::value;
       if constexpr (g == 0) img_copy<H, 0, 1>(DLIN, dst, XT(A::LDL), H, 0, b0);
@@ -1162,9 +1171,9 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
       const int f = 16 * t + n16;
       f32x4 gi = {0.f, 0.f, 0.f, 0.f};
       if (f < I) {
-        const float b = bias(A::LDL, f);
-        const f32x4 xr = from_bf4(*(const bf16x4*)(XIN + ioff(f, q)));
-        const int s = f / D, d = f - s * D;
+        const float b = BIL[16 * NW * g];
+        const f32x4 xr = from_bf4(*(const bf16x4*)(XIL + 256 * NW * g));
+        const int dg = dlane + (16 * NW * g) % D, d = dg >= D ? dg - D : dg;
         const f32x2 r01 = f32x2{acc[0], acc[1]} + b, r23 = f32x2{acc[2], acc[3]} + b;
         f32x2 d01 = r01 - f32x2{xr[0], xr[1]}, d23 = r23 - f32x2{xr[2], xr[3]};
         if (nrows < R) {
@@ -1189,22 +1198,23 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             if (4 * q + i >= nrows) continue;
-            if (s == 0 && (d == 1 || d == 2) && use_start) {
+            if (f < D && (d == 1 || d == 2) && use_start) {  // timestep 0
               s_start += df[i] * df[i];
               gi[i] += a.w_start * 2.f * df[i] * inv_2B;
             }
-            if (d == 0 && s == 0 && use_time) {
+            if (d == 0 && f < D && use_time) {
               s_t0 += r[i] * r[i];
               gi[i] += a.w_time * 2.f * r[i] * inv_B;
             }
           }
         }
         if (d == 0) {
+          const int s = f / D;
           *(f32x4*)(RCH0 + s * R + 4 * q) = r;
           *(f32x4*)(GD0 + s * R + 4 * q) = gi;
         }
       }
-      *(bf16x4*)(XIN + ioff(f, q)) = to_bf4(gi);  // pad features f >= I: 0
+      *(bf16x4*)(XIL + 256 * NW * g) = to_bf4(gi);  // pad features f >= I: 0
     }, scl(integral_constant<int, PL::sDL>{}));
     s_recon += sr2[0] + sr2[1];
   }
