@@ -353,15 +353,30 @@ __device__ __forceinline__ l2 x8frag(const void* img8, int kp) {
 }
 // rows 4q..4q+3 of feature f (f & 3 == lane & 3: a quad of lanes holds 4 consecutive features):
 // e4m3 of the bf16 activation (RNE, saturated at ±448 as f8x8).  The quad's 4 x 4 block is
-// transposed (quad_t) so lane b writes row 4q + b's 4 features as one dword; byte stores of single
-// features were 16-way bank conflicts (the x_rel image cost 3.8 us of prologue that way).
+// transposed so lane b writes row 4q + b's 4 features as one dword; byte stores of single features
+// were 16-way bank conflicts (the x_rel image cost 3.8 us of prologue that way).  The transpose is
+// of the converted bytes (round 5): each lane packs its feature's 4 rows into one dword, takes the
+// quad's four dwords by DPP broadcasts and gathers byte b of each with v_perm (≈17 VALU; transposing
+// the fp32 values first, quad_t, cost ≈30)
 __device__ __forceinline__ void img8(void* im8, int f, bf16x4 h, int q) {
   const int b = threadIdx.x & 3, f0 = f - b;
   const int kc = f0 >> 5, kk = f0 & 31, qx = (kk & 15) >> 2, e0 = (kk >> 4) << 2;
-  const f32x4 t = quad_t(from_bf4(h));  // features f0..f0+3 of row 4q + b
+  // feature f, rows 4q..4q+3: fp32 from the two packed dwords (left to itself the compiler re-rounds
+  // each value from fp32 instead, two more VALU per value)
+  u32x2 hw = __builtin_bit_cast(u32x2, h);
+  asm volatile("" : "+v"(hw));
+  const f32x4 v = {__builtin_bit_cast(float, hw[0] << 16), __builtin_bit_cast(float, hw[0] & 0xffff0000u),
+                   __builtin_bit_cast(float, hw[1] << 16), __builtin_bit_cast(float, hw[1] & 0xffff0000u)};
   auto c = [](float x) { return f8_sat(x); };
-  int w = __builtin_amdgcn_cvt_pk_fp8_f32(c(t[0]), c(t[1]), 0, false);
-  w = __builtin_amdgcn_cvt_pk_fp8_f32(c(t[2]), c(t[3]), w, true);
+  int m = __builtin_amdgcn_cvt_pk_fp8_f32(c(v[0]), c(v[1]), 0, false);
+  m = __builtin_amdgcn_cvt_pk_fp8_f32(c(v[2]), c(v[3]), m, true);  // byte i: row 4q + i
+  const unsigned d0 = __builtin_amdgcn_update_dpp(0, m, 0x00, 0xF, 0xF, false),
+                 d1 = __builtin_amdgcn_update_dpp(0, m, 0x55, 0xF, 0xF, false),
+                 d2 = __builtin_amdgcn_update_dpp(0, m, 0xAA, 0xF, 0xF, false),
+                 d3 = __builtin_amdgcn_update_dpp(0, m, 0xFF, 0xF, 0xF, false);
+  const unsigned sel = (unsigned)b | ((unsigned)(b + 4) << 8);  // byte b of src1, byte b of src0
+  const unsigned lo = __builtin_amdgcn_perm(d1, d0, sel), hi = __builtin_amdgcn_perm(d3, d2, sel);
+  const int w = (int)__builtin_amdgcn_perm(hi, lo, 0x05040100u);  // byte j: feature f0 + j, row 4q + b
   *(int*)((uint8_t*)im8 + ((((kc >> 1) * 4 + qx) * 16 + 4 * q + b) << 4) + (kc & 1) * 8 + e0) = w;
 }
 
