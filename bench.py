@@ -245,12 +245,20 @@ def _free_port():
 
 def rank_envs(n, env, port):
     """The environment of each of the n rank processes: torch.distributed.run's variables for one
-    node (rendezvous on 127.0.0.1), everything else inherited (HSA_ENABLE_IPC_MODE_LEGACY=0 too)."""
+    node (rendezvous on 127.0.0.1), everything else inherited (HSA_ENABLE_IPC_MODE_LEGACY=0 too).
+    Ranks sharing one GPU (CVAE_BENCH_SHARE_GPU=1, a rehearsal) get one HIP hardware queue each
+    (GPU_MAX_HW_QUEUES=1, whatever the environment says): with HIP's default 4 per process, 8
+    processes oversubscribe the GPU's queue slots, the scheduler time-slices them, and every
+    exchange wait becomes milliseconds (46 ms per step at 8 ranks against 0.18 ms with one queue
+    each, profiles/r05w/)."""
     out = []
+    share = env.get("CVAE_BENCH_SHARE_GPU") == "1"
     for r in range(n):
         e = dict(env)
         e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
                   "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+        if share:
+            e["GPU_MAX_HW_QUEUES"] = "1"
         out.append(e)
     return out
 

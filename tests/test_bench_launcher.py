@@ -51,6 +51,10 @@ def test_rank_envs():
         assert e["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and e["PATH"] == "/bin"
     # every rank with the plan the bench takes under a launcher
     assert all(bench.launch_plan(3, e, 3) == ("run", 3) for e in envs)
+    assert all("GPU_MAX_HW_QUEUES" not in e for e in envs)
+    # ranks sharing one GPU: one hardware queue each (the GPU box exports HIP's default 4)
+    shared = bench.rank_envs(2, {"CVAE_BENCH_SHARE_GPU": "1", "GPU_MAX_HW_QUEUES": "4"}, 29999)
+    assert [e["GPU_MAX_HW_QUEUES"] for e in shared] == ["1", "1"]
 
 
 CHILD = r"""

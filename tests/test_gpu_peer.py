@@ -40,6 +40,10 @@ def _worker(rank, world, port, sizes, steps, out):
     import torch.distributed as dist
     from cvae_amd.dist import DataParallelStep
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    # one HIP hardware queue per rank (before HIP starts): with the default 4 (the GPU box exports
+    # it), eight ranks oversubscribe the GPU's queue slots and are time-sliced (bench.py
+    # rank_envs, profiles/r05w/)
+    os.environ["GPU_MAX_HW_QUEUES"] = "1"
     # ranks sharing one GPU are scheduled by the GPU's process scheduler, which can hold one
     # rank's queue off the GPU for milliseconds to seconds: a longer bound than the 10 s default
     # (one rank per GPU, cvae_capi.hip px_timeout_ticks); a protocol deadlock still fails the test
