@@ -816,7 +816,11 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   constexpr bool EPS_PRO = A::SZ;  // the draw sits in the prologue
   // wide latent (NZT tiles per wave): draws 0 .. NPRO-1 in the prologue, the rest in the E0 GEMM
   constexpr int NPRO = EPS_PRO ? 1 : (kEpsProWide<A> < NZT ? kEpsProWide<A> : NZT);
-  const bool eps_mine = !A::SZ || wave == 0;  // wave-uniform
+  // SZ: the draw runs on the last wave — no x-transform task at cfg2's 200 tasks, and its SIMD's
+  // other wave (3) has the lightest one — and reaches wave 0's lanes (which hold mu, logvar)
+  // through LDS across the prologue barrier (the recon time-channel buffer, idle until the loss)
+  const bool eps_mine = !A::SZ || wave == NW - 1;  // wave-uniform
+  float* const EPSX = (float*)(smem + A::L_RCH0);
 
   // ---- prologue: x tile (relative transform, Training_VAE.py:345-348), biases, LDS pads
   // x_f32 (CVAE_X_F32: real data with ~200 m absolute coordinates): fp32 rows, the start point
@@ -900,11 +904,14 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
       if (CVAE_DIAG_NOPHILOX || !eps_mine) ep[k] = f32x4{0.f, 0.f, 0.f, 0.f};
       else eps_make(kk, eh0[k]);
     });
+    if constexpr (A::SZ)
+      if (wave == NW - 1) *(f32x4*)(EPSX + 4 * lane) = ep[0];
     // device counters: this launch begins optimizer step ctr[1] + 1 and precomputes its Adam
-    // scalars for the dW kernel behind it.  Wave 0 of block 0, wave-uniformly, while it waits for
+    // scalars for the dW kernel behind it.  One wave of block 0, wave-uniformly, while it waits for
     // the x tile: the step count by scalar load, the f64 pow on every lane, one lane stores (at
-    // the kernel's end, one lane's f64 pow delays the chain's completion)
-    if (a.ctr && blk == 0 && wave == NW - 1) {  // wave 0 draws eps (EPS_PRO): another SIMD
+    // the kernel's end, one lane's f64 pow delays the chain's completion).  Not the eps wave (SZ:
+    // the last one) and, at cfg2's 200 transform tasks, a wave without one
+    if (a.ctr && blk == 0 && wave == (A::SZ ? NW - 2 : NW - 1)) {
       const uint64_t t = *(const __attribute__((address_space(4))) uint64_t*)(a.ctr + 1) + 1;
       float s0 = 0.f, s1 = 0.f;
       if (a.adam_pre && !CVAE_DIAG_NOADAMPRE) adam_scalars(a.lr, a.beta1, a.beta2, (double)t, s0, s1);
@@ -989,6 +996,8 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   sfor<PF0, P>([&](auto g) { ring_load<A, P, decltype(g)::value>(ring, AR, wave, lane); });
   sub();
   bar();
+  if constexpr (A::SZ)
+    if (wave == 0) ep[0] = *(const f32x4*)(EPSX + 4 * lane);
   if constexpr (A::CLS) {
     // the one-hot class image (xT(LCE)) and e = table[class] into both concatenations at 2H + k and
     // Z + H + k (bf16: what one-hot · Wf(LCE) gives the generic chain; zeros in the K padding)

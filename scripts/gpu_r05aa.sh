@@ -1,0 +1,16 @@
+#!/bin/bash
+# round 5: cfg2's eps drawn on the last wave (no transform task; via LDS to wave 0) and the Adam
+# scalars on wave 6 — parity, then alternating bench lines against the previous library
+set -u
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/${TAG:-r05aa}; mkdir -p $O
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+for r in 1 2 3; do
+  for v in new old; do
+    L=""; [ $v = old ] && L=$GRAFT_REPO_ROOT/build/ab/old.so
+    CVAE_LIB=$L timeout -k 10 180 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-b2b > $O/s20_${v}_$r.json 2> $O/s20_${v}_$r.err &&
+    CVAE_LIB=$L timeout -k 10 180 python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-b2b > $O/s200_${v}_$r.json 2> $O/s200_${v}_$r.err || exit 1
+  done
+done
+for f in $O/*.json; do python3 -c "import json;d=json.load(open('$f'));r=d['roofline'];print('$f',d['value'],d['ms_per_step'],r.get('kernels_ms'))"; done
