@@ -839,32 +839,51 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     const int xt = min(tid, NTASK - 1), xrq = xt / NKT, xk = xt - xrq * NKT;  // idle threads: task NTASK-1, no store
     uint32_t xw[4][12];  // row 4xrq + i: dwords of its 12 features (bf16: [0..5])
     uint32_t xs[4][2];   // its start point x[:,0,1:3] (Training_VAE.py:345): bf16 dwords 0, 1 / fp32 features 1, 2
+    // x tile loads, as four straight-line paths (with and without a row gather, fp32 or bf16 rows:
+    // block-uniform branches outside the loads).  A gather load, or the x32 branch, inside the row
+    // loop made the compiler wait for each row's x loads before the next row's (its wait counts
+    // merge at every join, and the no-gather bf16 path paid for the others too) — four serial round
+    // trips in the prologue
+    auto x_loads = [&](auto gather, auto f32rows) {
+      const uint32_t* pr[4];  // row starts, all before the first x load (a gather: one wait)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int64_t g = min(b0 + 4 * xrq + i, last);
-      if (a.idx) g = gld<int64_t>(a.idx + g);
-      if (x32) {  // wave-uniform: before the weight stream starts
-        const uint32_t* const p = (const uint32_t*)a.x + g * I;
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const u32x4 v = gld<u32x4>(p + 12 * xk + 4 * j);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) xw[i][4 * j + e] = v[e];
-        }
-        xs[i][0] = gld<uint32_t>(p + 1);
-        xs[i][1] = gld<uint32_t>(p + 2);
-      } else {
-        const uint32_t* const p = (const uint32_t*)((const __bf16*)a.x + g * I);
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const u32x2 v = gld<u32x2>(p + 6 * xk + 2 * j);
-          xw[i][2 * j] = v[0];
-          xw[i][2 * j + 1] = v[1];
-        }
-        const u32x2 v0 = gld<u32x2>(p);
-        xs[i][0] = v0[0];
-        xs[i][1] = v0[1];
+      for (int i = 0; i < 4; ++i) {
+        int64_t g = min(b0 + 4 * xrq + i, last);
+        if constexpr (decltype(gather)::value) g = gld<int64_t>(a.idx + g);
+        pr[i] = decltype(f32rows)::value ? (const uint32_t*)a.x + g * I
+                                         : (const uint32_t*)((const __bf16*)a.x + g * I);
       }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t* const p = pr[i];
+        if constexpr (decltype(f32rows)::value) {
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            const u32x4 v = gld<u32x4>(p + 12 * xk + 4 * j);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) xw[i][4 * j + e] = v[e];
+          }
+          xs[i][0] = gld<uint32_t>(p + 1);
+          xs[i][1] = gld<uint32_t>(p + 2);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            const u32x2 v = gld<u32x2>(p + 6 * xk + 2 * j);
+            xw[i][2 * j] = v[0];
+            xw[i][2 * j + 1] = v[1];
+          }
+          const u32x2 v0 = gld<u32x2>(p);
+          xs[i][0] = v0[0];
+          xs[i][1] = v0[1];
+        }
+      }
+    };
+    if (a.idx) {
+      if (x32) x_loads(std::true_type{}, std::true_type{});
+      else x_loads(std::true_type{}, std::false_type{});
+    } else {
+      if (x32) x_loads(std::false_type{}, std::true_type{});
+      else x_loads(std::false_type{}, std::false_type{});
     }
     // EPS_PRO: the host-eps load right behind the x tile (the x wait then covers it)
     f32x4 eh0[NPRO > 0 ? NPRO : 1];
