@@ -733,6 +733,13 @@ bool wide_layout_matches(const cvae_handle* h) {
 // register prefetch: the per-CU L2 stream stays busy across step barriers.  The default for this
 // shape (row chain 17.8 vs 18.35 us at B = 1024); CVAE_RING=0 at creation keeps
 // fastchain_kernel.
+// the chain instance for the rows' format: bf16 rows (the bench's and the peer step's data) run the
+// form with the fp32-row loads compiled out (wchain::wide_body's XB)
+template <class A>
+auto chain_for(const RowArgs& ra) {
+  return ra.x_f32 ? wchain::widechain_kernel<A> : wchain::widechain_kernel<A, false, true>;
+}
+
 int plan_ring(cvae_handle* h) {
   using A = wchain::Cfg2;
   const cvae_config& c = h->cfg;
@@ -742,6 +749,8 @@ int plan_ring(cvae_handle* h) {
   if (!wide_layout_matches<A>(h) || h->arena_bytes >= ((int64_t)1 << 31)) return CVAE_OK;
   HIPCK(hipFuncSetAttribute((const void*)wchain::widechain_kernel<A>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             A::L_TOTAL));
+  HIPCK(hipFuncSetAttribute((const void*)wchain::widechain_kernel<A, false, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, A::L_TOTAL));
   HIPCK(hipFuncSetAttribute((const void*)wchain::widechain_kernel<A, true>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, A::L_TOTAL));
   h->ring = true;
@@ -765,6 +774,8 @@ int plan_ring_cls(cvae_handle* h) {
   if (!wide_layout_matches<A>(h) || h->arena_bytes >= ((int64_t)1 << 31)) return CVAE_OK;
   HIPCK(hipFuncSetAttribute((const void*)wchain::widechain_kernel<A>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             A::L_TOTAL));
+  HIPCK(hipFuncSetAttribute((const void*)wchain::widechain_kernel<A, false, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, A::L_TOTAL));
   h->ring_cls = true;
   h->ring_lds = A::L_TOTAL;
   return CVAE_OK;
@@ -799,6 +810,8 @@ int plan_wide_as(cvae_handle* h) {
   if (!wide_layout_matches<A>(h) || h->arena_bytes >= ((int64_t)1 << 31)) return CVAE_OK;
   HIPCK(hipFuncSetAttribute((const void*)wchain::widechain_kernel<A>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             A::L_TOTAL));
+  HIPCK(hipFuncSetAttribute((const void*)wchain::widechain_kernel<A, false, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, A::L_TOTAL));
   h->wide = true;
   h->wide_lds = A::L_TOTAL;
   const char* g = std::getenv("CVAE_GENERIC_DW");  // "1": the generic tile-list dW kernel (A/B)
@@ -909,13 +922,13 @@ int launch_train_chain(cvae_handle* h, RowArgs ra, hipStream_t s, bool tap_ok = 
   if (std::is_same<T, __bf16>::value && ring_ok(h, ra)) {
     ra.stamps = h->d_stamps;
     const int grid = rup_i(ra.batch, 32) / wchain::R;
-    return klaunch(h, wchain::widechain_kernel<wchain::Cfg2>, dim3(grid), dim3(wchain::NT), h->ring_lds, s,
+    return klaunch(h, chain_for<wchain::Cfg2>(ra), dim3(grid), dim3(wchain::NT), h->ring_lds, s,
                    h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra.ctr, ra);
   }
   if (std::is_same<T, __bf16>::value && ring_cls_ok(h, ra)) {
     ra.stamps = h->d_stamps;
     const int grid = rup_i(ra.batch, 32) / wchain::R;
-    return klaunch(h, wchain::widechain_kernel<wchain::Cfg4>, dim3(grid), dim3(wchain::NT), h->ring_lds, s,
+    return klaunch(h, chain_for<wchain::Cfg4>(ra), dim3(grid), dim3(wchain::NT), h->ring_lds, s,
                    h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra.ctr, ra);
   }
   if (std::is_same<T, __bf16>::value && fast_ok(h, ra)) {
@@ -930,12 +943,12 @@ int launch_train_chain(cvae_handle* h, RowArgs ra, hipStream_t s, bool tap_ok = 
     ra.stamps = h->d_stamps;
     const int grid = rup_i(ra.batch, 32) / wchain::R;
     if (h->cfg.dtype == CVAE_FP8 && h->wide_mx)
-      return klaunch(h, wchain::widechain_kernel<wchain::Cfg5F8>, dim3(grid), dim3(wchain::NT), h->wide_lds, s,
+      return klaunch(h, chain_for<wchain::Cfg5F8>(ra), dim3(grid), dim3(wchain::NT), h->wide_lds, s,
                      h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra.ctr, ra);
     if (h->cfg.dtype == CVAE_FP8)
-      return klaunch(h, wchain::widechain_kernel<wchain::Cfg5F8B>, dim3(grid), dim3(wchain::NT), h->wide_lds, s,
+      return klaunch(h, chain_for<wchain::Cfg5F8B>(ra), dim3(grid), dim3(wchain::NT), h->wide_lds, s,
                      h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra.ctr, ra);
-    return klaunch(h, wchain::widechain_kernel<wchain::Cfg5>, dim3(grid), dim3(wchain::NT), h->wide_lds, s,
+    return klaunch(h, chain_for<wchain::Cfg5>(ra), dim3(grid), dim3(wchain::NT), h->wide_lds, s,
                    h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra.ctr, ra);
   }
   return launch_rowchain<T, RC_TRAIN>(h, ra, s);

@@ -657,7 +657,11 @@ __device__ __forceinline__ void img_copy(const __bf16* img, const ArenaDst& dst,
 // TAP (parity tests only, cvae_tap_outputs): the chain also writes what its epilogues computed —
 // recon (the last decoder layer's output before the loss, fp32 (batch, S, D)), mu and logvar (fp32
 // (batch, Z)) — to a.recon_out / a.mu_out / a.lv_out: the training step's own rounding points
-template <class A, int P, bool TAP = false>
+// XB: bf16 rows only (the bench's and the peer step's data) — the fp32-row load path compiled out.
+// Both row formats behind a runtime branch share the x registers, and the compiler's merged wait
+// counts then hold the first Philox draw until the whole x tile has landed; fp32 rows keep the
+// runtime form (a compile-time fp32 form needs 142 VGPRs: tests/test_kernel_resources.py)
+template <class A, int P, bool TAP = false, bool XB = false>
 __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const RowArgs& a, char* smem, int blk) {
   using PL = Plan<A>;
   constexpr int Ip = A::Ip, S = A::S, D = A::D, I = A::I, Z = A::Z, NE = A::NE, ND = A::ND;
@@ -808,7 +812,11 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   auto eps_make = [&](auto kk, f32x4 eh) {
     constexpr int k = decltype(kk)::value;
     const int j0 = eps_j0(k);
-    f32x4 e = a.eps ? eh : philox_normal4(a.seed, rng_off, (uint32_t)(a.eps_row0 + b0 + rowq), (uint32_t)j0);
+    // the draw first and the host value picked last: with the pick first the compiler copied the
+    // host-eps registers before the draw, and the draw waited for that load — in flight behind the
+    // x tile — even when the kernel draws (the host-eps path draws for nothing: parity tests only)
+    const f32x4 d = philox_normal4(a.seed, rng_off, (uint32_t)(a.eps_row0 + b0 + rowq), (uint32_t)j0);
+    f32x4 e = a.eps ? eh : d;
     if (rowq >= nrows) e = f32x4{0.f, 0.f, 0.f, 0.f};
     ep[k] = quad_t(e);
   };
@@ -835,7 +843,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     constexpr int NKT = I / 12, NTASK = 4 * NKT;  // timestep pairs per row; tasks per tile
     static_assert(NTASK <= NT, "x_rel transform: one task per thread");
     const int last = max(a.batch - 1, 0);
-    const bool x32 = a.x_f32 != 0;
+    const bool x32 = !XB && a.x_f32 != 0;
     const int xt = min(tid, NTASK - 1), xrq = xt / NKT, xk = xt - xrq * NKT;  // idle threads: task NTASK-1, no store
     uint32_t xw[4][12];  // row 4xrq + i: dwords of its 12 features (bf16: [0..5])
     uint32_t xs[4][2];   // its start point x[:,0,1:3] (Training_VAE.py:345): bf16 dwords 0, 1 / fp32 features 1, 2
@@ -1457,7 +1465,7 @@ constexpr int RING = CVAE_WIDE_RING;
 // ctr (the device step counters) rides in the preloaded kernel-argument SGPRs beside the x-tile
 // arguments: read from RowArgs, the Philox-offset load waited for a kernel-argument fetch before
 // the first x load could issue
-template <class A, bool TAP = false>
+template <class A, bool TAP = false, bool XB = false>
 __global__ __launch_bounds__(NT) void widechain_kernel(char* arena, const void* x, const int64_t* idx, int Bp,
                                                        int batch, uint64_t* ctr, RowArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1466,7 +1474,7 @@ __global__ __launch_bounds__(NT) void widechain_kernel(char* arena, const void* 
   ra.idx = idx;
   ra.batch = batch;
   ra.ctr = ctr;
-  wide_body<A, A::SZ ? CVAE_RING_P : RING, TAP>(arena, Bp, ra, smem, blockIdx.x);
+  wide_body<A, A::SZ ? CVAE_RING_P : RING, TAP, XB>(arena, Bp, ra, smem, blockIdx.x);
 }
 
 }  // namespace wchain

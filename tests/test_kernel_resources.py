@@ -38,9 +38,11 @@ def _pick(res, *subs):
 
 def test_ring_chain_fits_128_vgprs_without_scratch(res):
     ks = _pick(res, "widechain_kernel", RING)
-    tap = [k for k in ks if ">, true>(" in k["demangled"]]
+    # widechain_kernel<Arch<...>, TAP, XB>: XB = bf16 rows only (the fp32-row loads compiled out)
+    tap = [k for k in ks if ">, true, false>(" in k["demangled"]]
     prod = [k for k in ks if k not in tap]
-    assert len(prod) == 2, [k["demangled"] for k in ks]  # cfg2 and cfg4 (class embedding)
+    # cfg2 and cfg4 (class embedding), each with both row formats and bf16 rows only
+    assert len(prod) == 4 and sum(", false, true>(" in k["demangled"] for k in prod) == 2, [k["demangled"] for k in ks]
     assert len(tap) == 1, [k["demangled"] for k in ks]   # cfg2's parity-tap form (cvae_tap_outputs)
     for k in prod:
         assert k["vgpr"] <= 128 and k["scratch"] == 0, k
