@@ -874,8 +874,8 @@ RowArgs row_args(cvae_handle* h, const CallX& c) {
 bool fast_ok(const cvae_handle* h, const RowArgs& ra) {
   return h->fast_nki > 0 && (((uintptr_t)ra.x) & 15) == 0 && !ra.x_f32 && !ra.ext && !ra.x_relative;
 }
-// the ring chain (cvae_widechain.h Cfg2 / Cfg4) also takes fp32 rows (CVAE_X_F32, the train loop's
-// real data): its prologue subtracts the start point in fp32 and rounds once
+// the ring and wide chains (cvae_widechain.h Cfg2 / Cfg4 / Cfg5*) also take fp32 rows (CVAE_X_F32,
+// the train loop's real data): the prologue subtracts the start point in fp32 and rounds once
 bool ring_ok(const cvae_handle* h, const RowArgs& ra) {
   return h->ring && h->fast_nki > 0 && (((uintptr_t)ra.x) & 15) == 0 && (((uintptr_t)ra.eps) & 15) == 0 && !ra.ext &&
          !ra.x_relative;
@@ -885,7 +885,7 @@ bool ring_cls_ok(const cvae_handle* h, const RowArgs& ra) {
          !ra.x_relative;
 }
 bool wide_ok(const cvae_handle* h, const RowArgs& ra) {
-  return h->wide && (((uintptr_t)ra.x) & 15) == 0 && (((uintptr_t)ra.eps) & 15) == 0 && !ra.x_f32 && !ra.ext &&
+  return h->wide && (((uintptr_t)ra.x) & 15) == 0 && (((uintptr_t)ra.eps) & 15) == 0 && !ra.ext &&
          !ra.x_relative;
 }
 // rows per workgroup of the training row chain a call runs (its loss partials are per workgroup)
@@ -1465,12 +1465,16 @@ int cvae_px_export(cvae_handle* h, int world, int rank, void* blob) {
 
 // Workgroups of the exchange's launches one CU holds at once, from the compiled kernels' resources
 // (the residency precondition of cvae_peer.h was a constant): the minimum of what the
-// occupancy calculator gives the row chain (its dynamic LDS) and both px_wgrad forms, capped at
-// PX_SLOTS_PER_CU.  Falls below 2 only if a kernel's VGPRs or LDS grow past the two-per-CU budget.
+// occupancy calculator gives the row chain (both row formats, its dynamic LDS) and both px_wgrad
+// forms, capped at PX_SLOTS_PER_CU.  Falls below 2 only if a kernel's VGPRs or LDS grow past the
+// two-per-CU budget.
 int px_slots_per_cu(const cvae_handle* h, int* out) {
-  int a = 0, b = 0, c = 0;
+  int a = 0, a2 = 0, b = 0, c = 0;
   HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, (const void*)wchain::widechain_kernel<wchain::Cfg2>,
                                                      wchain::NT, h->ring_lds));
+  HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &a2, (const void*)wchain::widechain_kernel<wchain::Cfg2, false, true>, wchain::NT, h->ring_lds));
+  a = std::min(a, a2);
   HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, (const void*)fchain::px_wgrad_kernel<19, true>,
                                                      WG_THREADS, 0));
   HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&c, (const void*)fchain::px_wgrad_kernel<19>, WG_THREADS, 0));

@@ -555,6 +555,41 @@ def test_ring_chain_fp32_rows_relative_transform(cvae, monkeypatch, B):
     assert np.abs(l1 - want).sum() < np.abs(lb - want).sum(), (l1, lb, want)
 
 
+@pytest.mark.parametrize("kind", ["ring", "wide_bf16", "wide_fp8"])
+def test_chain_row_formats_bit_equal(cvae, kind):
+    """fp32 rows and bf16 rows run different instances of the chain (bf16 rows: the fp32-row loads
+    compiled out, wide_body's XB).  On bf16-representable data with absolute coordinates they give
+    the same bits: the fp32 form subtracts the start point in fp32 and rounds once, which is what
+    the bf16 form computes from the same values.  With and without a row gather (idx), and with a
+    ragged last row tile (B = 77)."""
+    B, N = 77, 200
+    if kind == "ring":
+        torch.manual_seed(0)
+        _, eng = _model(cvae, 100, 6, 8, dtype="bf16", max_batch=N)
+        S, D, Z = 100, 6, 8
+    else:
+        _, _, eng, _, _ = _wide(cvae, kind[5:], N)
+        S, D, Z = WIDE["S"], WIDE["D"], WIDE["Z"]
+    assert eng.train_kernel == ("ring" if kind == "ring" else "wide")
+    gen = torch.Generator().manual_seed(7)
+    x = torch.randn(N, S, D, generator=gen)
+    x[:, :, 1] += 180.0 + 40.0 * torch.rand(N, 1, generator=gen)   # absolute world coordinates
+    x[:, :, 2] -= 150.0 + 40.0 * torch.rand(N, 1, generator=gen)
+    x = x.to(torch.bfloat16)
+    eps = torch.randn(B, Z, generator=gen)
+    idx = torch.randperm(N, generator=gen)[:B]
+    eng.keep_f32 = True
+    x32, x16 = x.float().cuda(), x.cuda()
+    for ix in (None, idx):
+        out = []
+        for xx in (x32, x16):
+            assert eng._xflags(eng.as_input(xx, keep_f32=True)) == (1 if xx.dtype == torch.float32 else 0)
+            l = eng.forward_backward(xx if ix is not None else xx[:B], idx=ix, eps=eps, batch=B).clone()
+            out.append((l, eng.grads.clone()))
+        assert torch.equal(out[0][0], out[1][0]), (ix is not None, out[0][0], out[1][0])
+        assert torch.equal(out[0][1], out[1][1]), (ix is not None, (out[0][1] - out[1][1]).abs().max())
+
+
 def test_ring_chain_philox_training_and_determinism(cvae, monkeypatch):
     """In-kernel Philox eps keyed by the global row: the ring chain draws fastchain's noise (same
     losses up to summation order); five training steps (device counters, dW ⊕ Adam behind each
