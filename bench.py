@@ -14,7 +14,9 @@ Workloads:
        from the committed fixture tests/golden/sce_fixed.npz), B=32 (--batch 38 = the
        reference's default), fp32, the reference loop: one host permutation per epoch
        (DataLoader(shuffle=True)), batches 32|6, host eps — what `python Training_VAE.py`
-       runs, with the epoch's rows gathered on the device.
+       runs, with the epoch's rows gathered on the device; the timed steps' permutations and eps
+       are drawn on the host inside the timed region, uploaded once, and issued through one
+       cvae_train_epochs call (the fp32 ring chain, cvae_f32chain.h).
   wide (BASELINE configs[4] shape): S=200, Z=512, 8+8 layers, bf16 (or --dtype fp8).
 
 Prints ONE JSON line (rank 0).  `roofline` is the dominant kernel's algorithmic
@@ -429,7 +431,15 @@ def main():
 
         def run(k):
             """k batches of the reference loop: a fresh permutation each epoch (host, DataLoader
-            shuffle), uploaded once per epoch; host eps per batch (randn_like on the CPU, :205)."""
+            shuffle) and host eps per batch (randn_like on the CPU, :205).  One GPU: the k steps'
+            epochs drawn on the host, uploaded once and issued through one cvae_train_epochs call
+            (what cvae_amd.train does); data-parallel: per step."""
+            if not dp.split:
+                E = (k + len(sizes) - 1) // len(sizes)  # epochs touched (the last may be cut short)
+                perms = torch.stack([torch.randperm(n_rows, generator=gen) for _ in range(E)])
+                eps = torch.randn(E * n_rows, Z, generator=gen)
+                eng.train_epochs(x, perms.to(dev), B, n_steps=k, eps=eps.to(dev))
+                return
             for _ in range(k):
                 if state["k"] == len(sizes):
                     idx_dev.copy_(torch.randperm(n_rows, generator=gen), non_blocking=True)

@@ -22,6 +22,7 @@
 #include "cvae_fastwgrad.h"
 #include "cvae_widechain.h"
 #include "cvae_widewgrad.h"
+#include "cvae_f32chain.h"
 #include "cvae_extract.h"
 #include "cvae_mpc.h"
 
@@ -111,6 +112,8 @@ struct cvae_handle {
   bool ring = false;        // the fast configuration's training chain runs wchain::widechain_kernel<Cfg2>
   bool ring_cls = false;    // cfg4 (class embedding) at cfg2's shape: widechain_kernel<Cfg4>, generic dW
   int ring_lds = 0;
+  bool f32c = false;        // fp32 training at the reference's own shape (seq_len 10, dim 3): f32c::f32chain_kernel<Cfg1>
+  int f32c_lds = 0;
   bool timing = false;
   // timing: per call, a chain of events on the caller's stream; segment i of a
   // call spans ev[i] → ev[i+1] and is named by the kernel launched after ev[i]
@@ -781,6 +784,45 @@ int plan_ring_cls(cvae_handle* h) {
   return CVAE_OK;
 }
 
+// The reference's own configuration in fp32 (Training_VAE.py:274-282: seq_len 10, dim 3, latent 8,
+// hidden 128, 4+4 layers; BASELINE configs[0]) on the fp32 ring chain (cvae_f32chain.h) instead of the
+// generic interpreter.  Its compile-time arena offsets are checked against the handle's layout.
+template <class A>
+bool f32c_layout_matches(const cvae_handle* h) {
+  const NetDev& n = h->net;
+  if (n.n_layers != f32c::NL || n.nbias != A::nbias || n.Bp % 32 != 0 ||
+      (const char*)n.bias_all != h->arena + A::bias_base)
+    return false;
+  const int64_t Bp4 = 4 * (int64_t)n.Bp;
+  for (int l = 0; l < f32c::NL; ++l) {
+    const LayerDev& L = n.L[l];
+    if (L.Kp != A::Kp(l) || L.Np != A::Np(l) || n.bias_off[l] != A::bias_off(l) || L.f8 || L.f8b ||
+        (char*)L.Wf != h->arena + A::wf(l) || (char*)L.Wb != h->arena + A::wb(l) ||
+        (char*)L.xT != h->arena + A::act0 + Bp4 * A::xrows(l) || (char*)L.gT != h->arena + A::act0 + Bp4 * A::grows(l))
+      return false;
+    const bool relu = !(l == f32c::LFC || l == f32c::LD3);
+    if (L.relu != (relu ? 1 : 0)) return false;
+  }
+  return true;
+}
+
+int plan_f32c(cvae_handle* h) {
+  using A = f32c::Cfg1;
+  const cvae_config& c = h->cfg;
+  h->f32c = false;
+  const char* gen = std::getenv("CVAE_GENERIC");
+  if ((gen && gen[0] == '1') || c.dtype != CVAE_F32 || c.n_classes > 0 || c.hidden_dim != f32c::H ||
+      c.latent_dim != f32c::Z || c.n_enc != 4 || c.n_dec != 4 || c.seq_len != A::S || c.dim != A::D)
+    return CVAE_OK;
+  // the chain stores to the arena and streams its weights through 32-bit buffer offsets
+  if (!f32c_layout_matches<A>(h) || h->arena_bytes >= ((int64_t)1 << 31)) return CVAE_OK;
+  HIPCK(hipFuncSetAttribute((const void*)f32c::f32chain_kernel<A>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            A::L_TOTAL));
+  h->f32c = true;
+  h->f32c_lds = A::L_TOTAL;
+  return CVAE_OK;
+}
+
 // the compile-time dW decode of the wide shape (cvae_widewgrad.h) restates the handle's 32 × 64 tile
 // list and layer table exactly (CVAE_DW_NI2=0 or any other difference keeps the generic kernel)
 template <class A>
@@ -884,6 +926,10 @@ bool ring_cls_ok(const cvae_handle* h, const RowArgs& ra) {
   return h->ring_cls && (((uintptr_t)ra.x) & 15) == 0 && (((uintptr_t)ra.eps) & 15) == 0 && !ra.ext &&
          !ra.x_relative;
 }
+// fp32 rows of S·D = 30 floats are 8-B aligned (the x-tile loads are feature pairs)
+bool f32c_ok(const cvae_handle* h, const RowArgs& ra) {
+  return h->f32c && (((uintptr_t)ra.x) & 7) == 0 && (((uintptr_t)ra.eps) & 15) == 0 && !ra.ext && !ra.x_relative;
+}
 bool wide_ok(const cvae_handle* h, const RowArgs& ra) {
   return h->wide && (((uintptr_t)ra.x) & 15) == 0 && (((uintptr_t)ra.eps) & 15) == 0 && !ra.ext &&
          !ra.x_relative;
@@ -893,6 +939,7 @@ int chain_rows(const cvae_handle* h, const RowArgs& ra) {
   if (fast_ok(h, ra)) return fchain::R;
   if (ring_ok(h, ra) || ring_cls_ok(h, ra)) return wchain::R;
   if (wide_ok(h, ra)) return wchain::R;
+  if (f32c_ok(h, ra)) return f32c::R;
   return h->R;
 }
 
@@ -950,6 +997,12 @@ int launch_train_chain(cvae_handle* h, RowArgs ra, hipStream_t s, bool tap_ok = 
                      h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra.ctr, ra);
     return klaunch(h, chain_for<wchain::Cfg5>(ra), dim3(grid), dim3(wchain::NT), h->wide_lds, s,
                    h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra.ctr, ra);
+  }
+  if (std::is_same<T, float>::value && f32c_ok(h, ra)) {
+    ra.stamps = h->d_stamps;
+    const int grid = rup_i(ra.batch, 32) / f32c::R;
+    return klaunch(h, f32c::f32chain_kernel<f32c::Cfg1>, dim3(grid), dim3(f32c::NT), h->f32c_lds, s, h->arena, ra.x,
+                   ra.idx, h->net.Bp, ra.batch, ra.ctr, ra);
   }
   return launch_rowchain<T, RC_TRAIN>(h, ra, s);
 }
@@ -1116,6 +1169,7 @@ int cvae_create(const cvae_config* cfg, int device, cvae_handle** out) {
   if (!rc) rc = plan_wide(h);
   if (!rc) rc = plan_ring(h);
   if (!rc) rc = plan_ring_cls(h);
+  if (!rc) rc = plan_f32c(h);
   if (rc) { cvae_destroy(h); return rc; }
   *out = h;
   return CVAE_OK;
@@ -1171,6 +1225,7 @@ int cvae_train_kernel(const cvae_handle* h, int* kind) {
   *kind = h->ring || h->ring_cls ? CVAE_KERNEL_RING
            : h->fast_nki > 0      ? CVAE_KERNEL_FAST
            : h->wide              ? CVAE_KERNEL_WIDE
+           : h->f32c              ? CVAE_KERNEL_F32
                                   : CVAE_KERNEL_GENERIC;
   return CVAE_OK;
 }
@@ -1323,6 +1378,27 @@ int cvae_train_steps(cvae_handle* h, const void* x, const int64_t* idx, const in
     const int rc = cvae_train_step(h, x, idx ? idx + (size_t)i * batch : nullptr, classes, batch, xflags,
                                    eps ? eps + (size_t)i * batch * Z : nullptr, seed, offset + (uint64_t)i, eps_row0,
                                    w, params, m, v, step0 + i, adam, loss_out, loss_accum, counters, stream);
+    if (rc) return rc;
+  }
+  return CVAE_OK;
+}
+
+int cvae_train_epochs(cvae_handle* h, const void* x, const int64_t* idx, const int32_t* classes, int n_rows,
+                      int batch, int n_steps, int xflags, const float* eps, uint64_t seed, uint64_t offset,
+                      int64_t eps_row0, const cvae_loss_weights* w, float* params, float* m, float* v, int64_t step0,
+                      const cvae_adam_config* adam, float* loss_out, double* loss_accum, uint64_t* counters,
+                      void* stream) {
+  if (!h) return fail(CVAE_E_INVALID, "null handle");
+  if (!idx || n_rows < 1 || batch < 1 || n_steps < 0) return fail(CVAE_E_INVALID, "idx, n_rows >= 1, batch >= 1, n_steps >= 0");
+  const int Z = h->cfg.latent_dim;
+  const int spe = (n_rows + batch - 1) / batch;
+  for (int s = 0; s < n_steps; ++s) {
+    const int e = s / spe, k = s % spe;
+    const int64_t r0 = (int64_t)e * n_rows + (int64_t)k * batch;  // first visited row of this step
+    const int b = std::min(batch, n_rows - k * batch);
+    const int rc = cvae_train_step(h, x, idx + r0, classes, b, xflags, eps ? eps + r0 * Z : nullptr, seed,
+                                   offset + (uint64_t)s, eps_row0, w, params, m, v, step0 + s, adam, loss_out,
+                                   loss_accum ? loss_accum + 5 * (int64_t)e : nullptr, counters, stream);
     if (rc) return rc;
   }
   return CVAE_OK;
@@ -1755,6 +1831,20 @@ int cvae_operand_checksum(cvae_handle* h, uint64_t* out, void* stream) {
   hipLaunchKernelGGL(checksum_kernel, dim3(64), dim3(256), 0, s, (const uint64_t*)h->arena, bytes / 8,
                      (unsigned long long*)out);
   HIPCK(hipGetLastError());
+  return CVAE_OK;
+}
+
+int cvae_read_activation(cvae_handle* h, int layer, int which, int rows, void* dst, int* features, void* stream) {
+  if (!h || layer < 0 || layer >= h->net.n_layers || (which != 0 && which != 1) || rows < 0)
+    return fail(CVAE_E_INVALID, "bad argument");
+  const LayerDev& L = h->net.L[layer];
+  const int kf = which ? L.Np : L.Kp;
+  if (features) *features = kf;
+  if (!dst) return CVAE_OK;
+  const int r16 = rup_i(rows, 16);
+  if (r16 > h->net.Bp) return fail(CVAE_E_CAPACITY, "rows beyond the arena's row capacity");
+  HIPCK(hipMemcpyAsync(dst, which ? L.gT : L.xT, (size_t)r16 * kf * h->tsize, hipMemcpyDeviceToDevice,
+                       (hipStream_t)stream));
   return CVAE_OK;
 }
 

@@ -69,6 +69,10 @@ _SIGS = {
                              _v]),
     "cvae_train_steps": (_i, [_v, _v, _v, _v, _i, _i, _i, _v, _u64, _u64, _i64, _W, _v, _v, _v, _i64, _A, _v, _v,
                               _v, _v]),
+    # h, x, idx, classes, n_rows, batch, n_steps, xflags, eps, seed, offset, eps_row0, w, params, m, v, step0,
+    # adam, loss_out, loss_accum, counters, stream
+    "cvae_train_epochs": (_i, [_v, _v, _v, _v, _i, _i, _i, _i, _v, _u64, _u64, _i64, _W, _v, _v, _v, _i64, _A, _v,
+                               _v, _v, _v]),
     "cvae_bench_kernels": (_i, [_v, _v, _v, _i, _i, _v, _v, _v, _i64, C.POINTER(_f), _v]),
     "cvae_fault": (_i, [_v, C.POINTER(C.c_uint)]),
     "cvae_clear_fault": (_i, [_v]),
@@ -89,6 +93,7 @@ _SIGS = {
     "cvae_rccl_close": (_i, [_v]),
     "cvae_operand_checksum": (_i, [_v, _v, _v]),                  # h, out (device u64), stream
     "cvae_tap_outputs": (_i, [_v, _v, _v, _v]),                   # h, recon, mu, logvar
+    "cvae_read_activation": (_i, [_v, _i, _i, _i, _v, C.POINTER(_i), _v]),  # h, layer, which, rows, dst, features, stream
     # h, x, idx, batch, xflags, eps, seed, eps_row0, w, params, m, v, adam, rank_scales, loss_out, loss_accum,
     # counters, stream
     "cvae_px_train_step": (_i, [_v, _v, _v, _i, _i, _v, _u64, _i64, _W, _v, _v, _v, _A, _v, _v, _v, _v, _v]),
@@ -109,7 +114,7 @@ _SIGS = {
     "cvae_last_error": (C.c_char_p, []),
     "cvae_abi_version": (_i, []),
 }
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 _lib = None
 

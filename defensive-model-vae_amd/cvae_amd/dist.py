@@ -17,11 +17,13 @@ eps: the in-kernel Philox draw is keyed by the GLOBAL row (``row0`` = lo_r, the 
 of the global batch) and every rank advances the same device offset, so the ranks of a global
 batch draw exactly the noise one process with that batch draws — not rank 0's noise B_r times.
 
-The all-reduce itself (``native``, the default on a GPU engine): the library's own RCCL
-communicator (``NativeRccl``: include/cvae.h cvae_rccl_*; the unique id broadcast over the group)
-issues ncclAllReduce on the stream the step's kernels run on — no framework stream between the
-dW and Adam launches, so a captured step graph is the chain, dW, the RCCL kernels and Adam on one
-stream.  ``native=False`` (and the CPU tests' engine) use torch.distributed's all_reduce.
+The all-reduce itself: the library's own RCCL communicator (``NativeRccl``: include/cvae.h
+cvae_rccl_*; the unique id broadcast over the group with rank 0's status, the ranks agreeing on
+success before any uses it) issues ncclAllReduce on the stream the step's kernels run on — no
+framework stream between the dW and Adam launches, so a captured step graph is the chain, dW, the
+RCCL kernels and Adam on one stream.  It is the default at world 1 (``bench.py --dp``) and opt-in
+(``native=True``) at world > 1, where torch.distributed's all_reduce (RCCL under the nccl backend)
+runs until a multi-GPU run has checked the library's communicator; the CPU tests' engine uses it too.
 
 Two-bucket overlap (``buckets=2``): the dW launch is split into the decoder layers (a contiguous
 tail of the flat gradient, ready first) and the rest; the decoder bucket's all-reduce runs on a
@@ -86,15 +88,34 @@ class NativeRccl:
         rank = dist.get_rank(group) if dist.is_initialized() else 0
         world = dist.get_world_size(group) if dist.is_initialized() else 1
         idb = (C.c_uint8 * n.value)()
+        ok, why = 1, ""
         if rank == 0:
-            check(L.cvae_rccl_unique_id(idb), "cvae_rccl_unique_id")
+            rc = L.cvae_rccl_unique_id(idb)
+            if rc < 0:
+                ok, why = 0, f"cvae_rccl_unique_id failed ({rc}): {L.cvae_last_error().decode(errors='replace')}"
         if world > 1:
-            nccl = dist.get_backend(group) == "nccl"
-            t = torch.tensor(list(bytes(idb)), dtype=torch.uint8, device=engine.device if nccl else "cpu")
+            # the id travels with rank 0's status: a rank-0 failure reaches every rank in
+            # the same broadcast, so no rank is left waiting in a collective the others skipped
+            dev = engine.device if dist.get_backend(group) == "nccl" else "cpu"
+            t = torch.tensor([ok] + list(bytes(idb)), dtype=torch.uint8, device=dev)
             src = dist.get_global_rank(group, 0) if group is not None else 0
             dist.broadcast(t, src=src, group=group)
-            idb = (C.c_uint8 * n.value)(*t.cpu().tolist())
-        check(L.cvae_rccl_init(engine._h, idb, world, rank), "cvae_rccl_init")
+            tl = t.cpu().tolist()
+            ok = tl[0]
+            idb = (C.c_uint8 * n.value)(*tl[1:])
+        if not ok:
+            raise RuntimeError(why or "rank 0 could not create the RCCL unique id")
+        rc = L.cvae_rccl_init(engine._h, idb, world, rank)
+        if world > 1:
+            # every rank joins the library's communicator or none does: one agreed flag
+            dev = engine.device if dist.get_backend(group) == "nccl" else "cpu"
+            f = torch.tensor([1 if rc >= 0 else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(f, op=dist.ReduceOp.MIN, group=group)
+            if int(f.item()) == 0:
+                if rc >= 0:
+                    L.cvae_rccl_close(engine._h)
+                raise RuntimeError("cvae_rccl_init failed on at least one rank")
+        check(rc, "cvae_rccl_init")
         self.world, self.rank = world, rank
 
     def all_reduce(self, buf, stream=None):
@@ -153,14 +174,16 @@ class DataParallelStep:
         # torch.distributed's all_reduce (native=False; engines without a HIP handle)
         self.rccl = None
         self._comm_stream = None
-        if native is None:  # one rank per GPU (an RCCL group, or a lone rank); not beside the peer exchange
-            one_gpu_per_rank = self.world_size == 1 or (dist.is_initialized() and dist.get_backend(group) == "nccl")
-            native = hasattr(engine, "_h") and torch.cuda.is_available() and one_gpu_per_rank and self.px is None
+        if native is None:
+            # a lone rank (world 1: bench --dp, the split step's measurement).  At world > 1 the library's
+            # communicator is opt-in (native=True) until a multi-GPU run has checked it against
+            # torch's all-reduce bit for bit: torch.distributed's RCCL all-reduce by default
+            native = hasattr(engine, "_h") and torch.cuda.is_available() and self.world_size == 1 and self.px is None
         if native and self.split:
             try:
                 self.rccl = NativeRccl(engine, group)
             except Exception as e:  # noqa: BLE001 — torch's all_reduce takes over, and the line says so
-                if native is True and exchange == "rccl" and self.world_size == 1:
+                if native is True:  # asked for explicitly: every rank raises (NativeRccl agrees on failure)
                     raise
                 self.exchange_note = (self.exchange_note + "; " if self.exchange_note else "") + \
                     f"native RCCL unavailable ({type(e).__name__}: {e}); torch all_reduce"

@@ -323,6 +323,48 @@ class CVAEEngine:
         self._ctr[1] += n_steps
         return self.loss
 
+    def train_epochs(self, x, idx, batch, n_steps=None, eps=None, loss_accum=None, weights=None, row0=0):
+        """Shuffled epochs of the reference loop (Training_VAE.py:338-370) in ONE C call
+        (cvae_train_epochs): ``idx`` holds E epochs' permutations of the ``n_rows`` rows of ``x``
+        ((E, n_rows) or flat, device or host int64); epoch e runs the DataLoader's batches of
+        ``batch`` rows over its permutation (the last one ragged), ``n_steps`` steps in all (default
+        every step of the E epochs; step s is batch s % spe of epoch s // spe).  ``eps``: one row per
+        visited row ((E·n_rows, Z)) or None (Philox).  ``loss_accum``: a device fp64 (E, 5) tensor
+        that receives each epoch's Σ loss·batch (zeroed here; default a fresh one).  Returns it; no
+        host sync.  Only the last epoch may be cut short by ``n_steps``."""
+        x = self.as_input(x, keep_f32=self.keep_f32)
+        idx = torch.as_tensor(idx)
+        E = idx.shape[0] if idx.dim() == 2 else 1
+        n_rows = idx.shape[1] if idx.dim() == 2 else idx.numel()
+        idx = self._idx(idx.reshape(-1), x.shape[0])
+        B = int(batch)
+        spe = (n_rows + B - 1) // B
+        n_steps = E * spe if n_steps is None else int(n_steps)
+        if n_steps > E * spe:
+            raise ValueError(f"{n_steps} steps > the {E * spe} steps of {E} epochs")
+        self._check_rows(x, idx[:min(B, n_rows)], min(B, n_rows))
+        e = None
+        if eps is not None:
+            e = torch.as_tensor(eps).to(device=self.device, dtype=torch.float32).contiguous()
+            if e.shape != (E * n_rows, self.shape[2]):
+                raise ValueError(f"eps must be ({E * n_rows},{self.shape[2]})")
+        if loss_accum is None:
+            loss_accum = torch.zeros(E, 5, device=self.device, dtype=torch.float64)
+        elif loss_accum.shape != (E, 5) or loss_accum.dtype != torch.float64 or loss_accum.device != self.device:
+            raise ValueError(f"loss_accum must be a ({E}, 5) float64 tensor on {self.device}")
+        else:
+            loss_accum.zero_()
+        self.ensure_packed()
+        w = self._weights(weights)
+        a = self._adam()
+        check(lib().cvae_train_epochs(
+            self._h, ptr(x), ptr(idx), None, n_rows, B, n_steps, self._xflags(x), ptr(e), self.seed, 0, int(row0),
+            C.byref(w), ptr(self.params), ptr(self.m), ptr(self.v), 0, C.byref(a), ptr(self.loss), ptr(loss_accum),
+            ptr(self.counters), self._stream()), "cvae_train_epochs")
+        self._ctr[0] += n_steps
+        self._ctr[1] += n_steps
+        return loss_accum
+
     def prepare_steps(self, x, batch=None, weights=None, accumulate=True, row0=0, classes=None):
         """A callable ``run(n)`` that enqueues ``n`` fused steps on rows 0..batch-1 of the resident
         ``x`` with Philox eps (cvae_train_steps) — what ``train_steps(x, n, batch=batch)`` does,
@@ -392,6 +434,21 @@ class CVAEEngine:
         finally:
             lib().cvae_tap_outputs(self._h, None, None, None)  # one-shot even if the call failed early
         return recon, mu, lv
+
+    def activation(self, layer, which="x", rows=None):
+        """The arena matrix the last training row chain wrote for ``layer`` (state_dict layer order:
+        C0, C1, E0.., fc, D0..): ``which="x"`` its input, ``"g"`` the gradient of its pre-activation —
+        as a (rows, features) fp32 tensor (cvae_read_activation; parity tests)."""
+        w = 0 if which == "x" else 1
+        rows = int(self.max_batch if rows is None else rows)
+        f = C.c_int()
+        check(lib().cvae_read_activation(self._h, int(layer), w, rows, None, C.byref(f), None), "cvae_read_activation")
+        r16 = (rows + 15) // 16 * 16
+        buf = torch.empty(r16 * f.value, device=self.device, dtype=self.tdtype)
+        check(lib().cvae_read_activation(self._h, int(layer), w, rows, ptr(buf), C.byref(f), self._stream()),
+              "cvae_read_activation")
+        # tile-major [rows/16][features][16] → (rows, features)
+        return buf.view(r16 // 16, f.value, 16).permute(0, 2, 1).reshape(r16, f.value)[:rows].float()
 
     def operand_checksum(self):
         """cvae_operand_checksum of the device operand copies (W, Wᵀ, biases) as a Python int
@@ -540,11 +597,12 @@ class CVAEEngine:
     @property
     def train_kernel(self):
         """'generic', 'fast' / 'ring' (reference architecture, bf16; 'ring' = the single weight-stream
-        chain, S=100 D=6) or 'wide' (BASELINE cfg5 shape, bf16):
+        chain, S=100 D=6), 'wide' (BASELINE cfg5 shape, bf16) or 'f32' (the reference's own
+        configuration in fp32: S=10 D=3, the fp32-MFMA ring chain):
         the training row chain this engine runs (cvae_train_kernel)."""
         k = C.c_int()
         check(lib().cvae_train_kernel(self._h, C.byref(k)))
-        return ("generic", "fast", "wide", "ring")[k.value]
+        return ("generic", "fast", "wide", "ring", "f32")[k.value]
 
     def workspace_bytes(self):
         b = C.c_int64()

@@ -55,6 +55,20 @@ class _Rows(torch.utils.data.Dataset):
         return i
 
 
+def loader_permutation(n):
+    """The row order of one epoch of ``DataLoader(dataset_of_n, shuffle=True)`` (Training_VAE.py:327,
+    num_workers=0), drawn from the global CPU generator exactly as iterating that loader draws it:
+    the iterator's base seed (``_BaseDataLoaderIter``: one int64 ``random_()``), then
+    ``RandomSampler``'s own seed (a second one) for a fresh generator's ``randperm(n)``.  Nothing
+    else of the loader touches the global generator, so a run that draws its epochs ahead replays
+    the reference's stream (tests/test_train_dp.py checks it against the DataLoader)."""
+    torch.empty((), dtype=torch.int64).random_()                    # the iterator's _base_seed
+    seed = int(torch.empty((), dtype=torch.int64).random_().item())  # RandomSampler.__iter__
+    g = torch.Generator()
+    g.manual_seed(seed)
+    return torch.randperm(n, generator=g)
+
+
 def epoch_line(epoch, means):
     """Training_VAE.py:373 print format."""
     t, r, k, s, ti = means
@@ -105,7 +119,7 @@ def save_checkpoint(path, model, eng, epoch, loss_history):
 def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidden_dim=128,
           weights=(0.1, 0.1, 1.0, 1.0), model_save_path=None, loss_save_path=None, dtype="fp32",
           eps="host", device=None, seed=None, engine_seed=0, log=print, model=None, buckets=1,
-          checkpoint_path=None, resume=None, classes=None, class_dim=0, exchange="auto"):
+          checkpoint_path=None, resume=None, classes=None, class_dim=0, exchange="auto", epochs_per_call=64):
     """Train like ``python Training_VAE.py`` (mode='training').
 
     data: path to the (N, seq_len, dim) ``.npy`` (TrajectoryDataset, :105-115) or an array; or a
@@ -124,6 +138,12 @@ def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidd
     checkpoint_path: write a resume point (save_checkpoint) after every epoch; resume: continue
     from one — ``epochs`` counts the total, so train(epochs=4, resume=ckpt_after_2) runs epochs 3-4
     and ends where an uninterrupted 4-epoch run ends.
+
+    On one device (no data parallelism, no class embedding) up to ``epochs_per_call`` epochs run as
+    ONE C call (cvae_train_epochs): their permutations (loader_permutation) and host eps are drawn
+    ahead in the reference's RNG order and uploaded once, the steps are enqueued without host work,
+    and the per-epoch loss sums are read once per call (so the epoch lines of a call print
+    together); with ``checkpoint_path`` a call is one epoch.
 
     Returns (model, loss_history, weighted_loss_history).
     """
@@ -181,7 +201,35 @@ def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidd
         first = ck["epoch"]
         step.broadcast_params()
         step.counters_changed()  # the peer exchange counts its flag epochs from the device step counter
-    for epoch in range(first, epochs):
+    fused = world_size == 1 and classes is None and not step.split and step.px is None
+    if fused:  # whole epochs per C call: the host draws, uploads once, and reads the losses once
+        chunk = 1 if checkpoint_path else max(1, int(epochs_per_call))
+        spe = (n + gb - 1) // gb
+        epoch = first
+        while epoch < epochs:
+            k = min(chunk, epochs - epoch)
+            perms, eps_rows = [], []
+            for _ in range(k):
+                perms.append(loader_permutation(n))      # (:340) the epoch's DataLoader order
+                if eps == "host":
+                    for lo in range(0, n, gb):            # reparameterize's randn_like (:205), per batch
+                        eps_rows.append(torch.randn(min(gb, n - lo), Z))
+                elif eps != "philox":
+                    raise ValueError("eps must be 'host' or 'philox'")
+            idx = torch.stack(perms).to(x_dev.device)
+            e = torch.cat(eps_rows).to(x_dev.device) if eps == "host" else None
+            acc = eng.train_epochs(x_dev, idx, gb, n_steps=k * spe, eps=e)
+            sums = acc.cpu().numpy()                      # the only host sync of the k epochs
+            for j in range(k):
+                means = sums[j] / n
+                for key, v in zip(LOSS_KEYS, means):
+                    loss_history[key].append(float(v))
+                if log:
+                    log(epoch_line(epoch + j, means))
+            epoch += k
+            if checkpoint_path:
+                save_checkpoint(checkpoint_path, model, eng, epoch, loss_history)
+    for epoch in range(first, epochs if not fused else first):
         for rows in loader:                               # (:340) one global batch
             g = rows.numel()
             lo, hi = dp.split_rows(g, world_size, rank)

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CVAE_ABI_VERSION 2
+#define CVAE_ABI_VERSION 3
 
 enum cvae_dtype {
   CVAE_F32 = 0,
@@ -138,10 +138,12 @@ int cvae_bucket_split(const cvae_handle* h, int64_t* split);
  * (bf16, the reference architecture: hidden 128, latent 8, 4+4 layers, seq_len*dim 600) or
  * CVAE_KERNEL_WIDE (bf16, BASELINE cfg5's shape: seq_len 200, dim 6, latent 512, 8+8 layers) or
  * CVAE_KERNEL_RING (the fast configuration at seq_len 100, dim 6 on the single-ring weight-stream
- * chain: the default at that shape; CVAE_RING=0 at creation keeps CVAE_KERNEL_FAST).
+ * chain: the default at that shape; CVAE_RING=0 at creation keeps CVAE_KERNEL_FAST) or
+ * CVAE_KERNEL_F32 (fp32, the reference's own configuration Training_VAE.py:274-282: seq_len 10, dim 3,
+ * latent 8, hidden 128, 4+4 layers, on the fp32-MFMA ring chain).
  * Introspection only (no reference counterpart); CVAE_GENERIC=1 at creation forces the generic. */
 enum cvae_train_kernel_kind {
-  CVAE_KERNEL_GENERIC = 0, CVAE_KERNEL_FAST = 1, CVAE_KERNEL_WIDE = 2, CVAE_KERNEL_RING = 3
+  CVAE_KERNEL_GENERIC = 0, CVAE_KERNEL_FAST = 1, CVAE_KERNEL_WIDE = 2, CVAE_KERNEL_RING = 3, CVAE_KERNEL_F32 = 4
 };
 int cvae_train_kernel(const cvae_handle* h, int* kind);
 
@@ -246,6 +248,21 @@ int cvae_train_steps(cvae_handle* h, const void* x, const int64_t* idx, const in
                      const cvae_adam_config* adam, float* loss_out, double* loss_accum,
                      uint64_t* counters, void* stream);
 
+/* The reference's shuffled epochs (Training_VAE.py:340-370 under `for epoch in range(epochs)`),
+ * n_steps fused steps enqueued by one call: epoch e visits the n_rows rows idx[e*n_rows ..
+ * (e+1)*n_rows) of x (that epoch's permutation, uploaded once) in DataLoader order — batches of
+ * `batch` rows, the last one ragged (drop_last=False) — and step s is batch s % spe of epoch s / spe
+ * (spe = ceil(n_rows / batch) steps per epoch), so an epoch may be split across calls.  eps: one
+ * row per visited row in the same order (NULL: Philox(seed, offset + s)).  loss_accum (NULL, or
+ * fp64[5 * epochs]) receives epoch e's Σ loss * batch at 5 * e; loss_out = the last step's losses.
+ * The host draws the permutations and eps with the reference's RNG order (cvae_amd.train): the
+ * host does no work per step. */
+int cvae_train_epochs(cvae_handle* h, const void* x, const int64_t* idx, const int32_t* classes, int n_rows,
+                      int batch, int n_steps, int xflags, const float* eps, uint64_t seed, uint64_t offset,
+                      int64_t eps_row0, const cvae_loss_weights* w, float* params, float* m, float* v, int64_t step0,
+                      const cvae_adam_config* adam, float* loss_out, double* loss_accum, uint64_t* counters,
+                      void* stream);
+
 /* Standalone conditional_vae_loss (Training_VAE.py:229-268), forward only, for
  * callers holding (recon, x, mu, logvar) fp32 device tensors; x is the RELATIVE
  * batch as at the reference call site (:356-359).  loss_out fp32[5] =
@@ -295,6 +312,13 @@ int cvae_clear_fault(cvae_handle* h);
  * rank, and equal to the checksum after a repack from the gathered master state, show the
  * broadcast delivered every byte.  Queued on `stream`. */
 int cvae_operand_checksum(cvae_handle* h, uint64_t* out, void* stream);
+
+/* Parity introspection (tests): copy the arena matrix of layer `layer` (state_dict layer order: C0, C1,
+ * E0.., fc, D0..) that the last training row chain wrote — which = 0: its input xT, 1: the gradient of
+ * its pre-activation gT — for the first roundup(rows, 16) batch rows, in the arena's own layout
+ * (tile-major [rows/16][features][16 rows], the operand dtype: fp32, or bf16 for CVAE_BF16/CVAE_FP8),
+ * to the device buffer `dst` (NULL: only report).  *features = the matrix's padded feature count. */
+int cvae_read_activation(cvae_handle* h, int layer, int which, int rows, void* dst, int* features, void* stream);
 
 /* Parity taps (tests): the NEXT training call's row chain also writes what its epilogues computed
  * at the training step's own rounding points — recon fp32 (batch,S,D) (the last decoder layer's

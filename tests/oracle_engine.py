@@ -100,6 +100,28 @@ class OracleEngine:
         self.adam_step()
         return self.loss
 
+    def train_epochs(self, x, idx, batch, n_steps=None, eps=None, loss_accum=None, weights=None, row0=0):
+        """cvae_train_epochs' schedule: epoch e's permutation idx[e], DataLoader batches of ``batch``
+        rows (the last ragged), eps rows in visiting order, epoch e's Σ loss·batch in row e."""
+        idx = torch.as_tensor(idx)
+        idx = idx.view(1, -1) if idx.dim() == 1 else idx
+        E, n = idx.shape
+        spe = (n + batch - 1) // batch
+        n_steps = E * spe if n_steps is None else int(n_steps)
+        acc = torch.zeros(E, 5, dtype=torch.float64)
+        saved = self.loss_accum
+        for s in range(n_steps):
+            e, k = divmod(s, spe)
+            lo, b = k * batch, min(batch, n - k * batch)
+            self.loss_accum = acc[e]
+            self.train_step(x, idx=idx[e, lo:lo + b], eps=None if eps is None else eps[e * n + lo:e * n + lo + b],
+                            batch=b, weights=weights)
+        self.loss_accum = saved
+        if loss_accum is not None:
+            loss_accum.copy_(acc)
+            return loss_accum
+        return acc
+
 
 class OracleModel(OracleCVAE):
     """An OracleCVAE already 'attached' to an OracleEngine (what cvae_amd.train expects)."""

@@ -23,7 +23,7 @@ def test_library_exports_every_header_symbol(cl):
     L = cl.lib()
     for n in names:
         assert hasattr(L, n), n
-    assert L.cvae_abi_version() == 2
+    assert L.cvae_abi_version() == 3
     assert cl.missing_signatures(os.path.join(ROOT, "include", "cvae.h")) == []  # ctypes covers the whole ABI
 
 
