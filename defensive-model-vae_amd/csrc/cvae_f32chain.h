@@ -20,8 +20,9 @@
 //    barriers; every offset is compile-time from the arena base (Layout below, checked against the
 //    handle by plan_f32c);
 //  * the two small-N steps (fc: 16 outputs, the last decoder layer: 32) split K over the 8 waves and
-//    reduce the partial tiles through LDS in a fixed order (deterministic); every wave forms z itself
-//    from those partials (no extra barrier before the decoder);
+//    reduce the partial tiles through LDS in a fixed order (deterministic); wave 0 forms z from the fc
+//    partials while every wave multiplies the h_c part of the decoder input (chunks 1..8), and z's
+//    chunk 0 follows behind one more barrier;
 //  * arena stores: a quad transpose (4 DPP) turns a lane's 4 features of one row into 4 rows of one
 //    feature, one 16-B write-through store per lane (a wave stores 1 KB contiguous).
 // MFMA work per workgroup: 500 v_mfma_f32_16x16x4_f32 per wave (fp32 MFMA is 1/16 of the bf16 rate),
@@ -132,6 +133,7 @@ __device__ __forceinline__ int item_off(int w) {
   int frag;
   if constexpr (s == sFC) frag = 2 * w + j;                                // tile 0, chunks 2w, 2w+1
   else if constexpr (s == sD3) frag = (w >> 2) * kch + 2 * (w & 3) + j;   // tile w/4, chunks 2(w%4), +1
+  else if constexpr (s == sD0) frag = w * kch + (j < 8 ? j + 1 : 0);     // chunks 1..8, then 0 (z)
   else if constexpr (s == sD0b) frag = j < 8 ? w * kch + j : 8 * kch + w; // tile w; tile 8 chunk w
   else if constexpr (s == sFCb) frag = (j == 0 ? w : 8 + w) * kch;        // tiles w, 8+w, chunk 0
   else frag = w * kch + j;                                                // tile w, chunk j
@@ -329,8 +331,10 @@ __device__ __forceinline__ void f32_body(char* const AR, const int Bp, const Row
     if (kb >= 0 && kb < NB4) bv0 = gld<f32x4>((const float*)(AR + A::bias_base) + 4 * kb);
     if (kb >= 0 && kb + 256 < NB4) bv1 = gld<f32x4>((const float*)(AR + A::bias_base) + 4 * (kb + 256));
     sfor<0, P>([&](auto g) { ring_load<A, P, decltype(g)::value>(ring, AR, wave, lane); });
-    // eps while the x tile is in flight: Philox keyed by the GLOBAL row (eps_row0 = a rank's first row)
-    {
+    // eps while the x tile is in flight (wave 0, which forms z): Philox keyed by the GLOBAL row
+    // (eps_row0 = a rank's first row)
+    ep = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (wave == 0) {
       const f32x4 d = philox_normal4(a.seed, rng_off, (uint32_t)(a.eps_row0 + b0 + b), (uint32_t)(4 * (q & 1)));
       ep = a.eps ? eh : d;
       if (b >= nrows) ep = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -425,33 +429,40 @@ __device__ __forceinline__ void f32_body(char* const AR, const int Bp, const Row
     sts4(PART, wave, acc);
   }
   bar();
-  // every wave: mu, logvar (lanes q < 2: latents 4q .. 4q+3 of row b) from the partials in a fixed
-  // order, reparameterize (:199-206) → z, its own X fragment of the decoder input's chunk 0
+  // D0 over [z ‖ h_c]: every wave multiplies the h_c chunks 1..8 while wave 0 forms mu, logvar (lanes
+  // q < 2: latents 4q .. 4q+3 of row b) from the fc partials in a fixed order, reparameterizes
+  // (:199-206) and writes z into chunk 0; chunk 0 after one more barrier
   f32x4 mu = {}, lv = {}, zz = {};
+  f32x4 acc0;
   {
-    const int qq = q & 1;
-    f32x4 sm = lds_slot(PART, 0, qq, b), sl = lds_slot(PART, 0, qq + 2, b);
+    if (wave == 0) {
+      const int qq = q & 1;
+      f32x4 sm = lds_slot(PART, 0, qq, b), sl = lds_slot(PART, 0, qq + 2, b);
 #pragma unroll
-    for (int v = 1; v < NW; ++v) {
-      sm += lds_slot(PART, v, qq, b);
-      sl += lds_slot(PART, v, qq + 2, b);
+      for (int v = 1; v < NW; ++v) {
+        sm += lds_slot(PART, v, qq, b);
+        sl += lds_slot(PART, v, qq + 2, b);
+      }
+      mu = sm + bias4(LFC, 4 * qq);
+      lv = sl + bias4(LFC, Z + 4 * qq);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) zz[i] = mu[i] + ep[i] * expf(0.5f * lv[i]);
+      if (q < 2) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (b < nrows) s_kl += 1.f + lv[i] - mu[i] * mu[i] - expf(lv[i]);  // KL (:243)
+        sts_slot(DCAT, 0, q, b, zz);
+      }
     }
-    mu = sm + bias4(LFC, 4 * qq);
-    lv = sl + bias4(LFC, Z + 4 * qq);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) zz[i] = mu[i] + ep[i] * expf(0.5f * lv[i]);
-    if (wave == 0 && q < 2)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (b < nrows) s_kl += 1.f + lv[i] - mu[i] * mu[i] - expf(lv[i]);  // KL (:243)
+    acc0 = gemm<A, P, sD0, 0, 8>(ring, DCAT, [](int j) { return j + 1; }, AR, wave, lane);
+    if (wave == 0) ast(XT(LD0), A::Kp(LD0), 4 * q, zz, q < 2);  // z → xT(D0) features 0..7
   }
-  {  // D0: [z ‖ h_c]
-    const f32x4 acc = gemm<A, P, sD0, 0, 9>(ring, DCAT, cid, AR, wave, lane,
-                                            [&](int j, f32x4 x) { return j == 0 && q < 2 ? zz : x; });
+  bar();
+  {  // D0 chunk 0: [z ‖ h_c 0..7]
+    const f32x4 acc = acc0 + gemm<A, P, sD0, 8, 9>(ring, DCAT, [](int) { return 0; }, AR, wave, lane);
     const f32x4 y = relu(acc, bias4(LD0, n4), integral_constant<int, MD0>{});
     sts4(A0, wave, y);
     ast(XT(LD1), H, n4, y);
-    if (wave == 0) ast(XT(LD0), A::Kp(LD0), 4 * q, zz, q < 2);  // z → xT(D0) features 0..7
   }
   bar();
   {  // D1
@@ -639,6 +650,7 @@ __device__ __forceinline__ void f32_body(char* const AR, const int Bp, const Row
     __hip_atomic_store((unsigned*)(a.partials + blk * 8 + tid), __builtin_bit_cast(unsigned, s), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   }
+  if (CVAE_DIAG_STAMPS) lbar();  // the last stamp (thread 0, after the final barrier) before it is read
   if (CVAE_DIAG_STAMPS && a.stamps && tid < 64)
     gst<unsigned long long>(a.stamps + blk * 64 + tid, tid < stamp_i ? STAMPS[tid] : 0ull);
 }

@@ -168,18 +168,20 @@ def mxw_layers(p, n_enc=4, n_dec=4):
     return {n for n in names if (p[n + ".weight"].shape[1] + 31) // 32 * 32 % 64 == 0}
 
 
-def forward(p, x, eps, n_enc=4, n_dec=4, dt=np.float32, q=None, f8=None):
+def forward(p, x, eps, n_enc=4, n_dec=4, dt=np.float32, q=None, f8=None, q_layers=None):
     """x: (B,S,D) absolute trajectories.  Returns (recon, mu, logvar, h_c, cache).
 
     q: operand quantiser (``bf16`` emulates the bf16 kernel path exactly: GEMM operands and
     stored activations rounded, accumulation and recon/loss in fp32, loss target = q(x_rel)).
     f8: {layer name: scale} (``fp8_layers``) — those forward GEMMs run as e4m3 x e4m3 (CVAE_FP8).
+    q_layers: the layers whose GEMM operands ``q`` rounds (default every layer) — attribution
+    experiments: one layer rounded at a time (tests/test_attribution.py).
     """
     q = q or _ident
     f8 = f8 or {}
 
     def lin(x, p, name, q=q):  # the layer's fp8 scale, if it has one
-        return _lin(x, p, name, q, f8.get(name))
+        return _lin(x, p, name, q if q_layers is None or name in q_layers else _ident, f8.get(name))
 
     p = {k: v.astype(dt) for k, v in p.items()}
     x = x.astype(dt)
@@ -234,7 +236,8 @@ def dloss_drecon(r, x_rel, w=(0.1, 0.1, 1.0, 1.0), B_norm=None):
     return g
 
 
-def backward(p, c, r, mu, lv, w=(0.1, 0.1, 1.0, 1.0), n_enc=4, n_dec=4, dt=np.float32, f8b=None, mxw=None):
+def backward(p, c, r, mu, lv, w=(0.1, 0.1, 1.0, 1.0), n_enc=4, n_dec=4, dt=np.float32, f8b=None, mxw=None,
+             trace=None):
     """Gradients of the total loss w.r.t. every parameter (dict keyed like state_dict).
 
     With the cache of ``forward(..., q=bf16)`` every stored gradient G and every GEMM operand
@@ -242,6 +245,7 @@ def backward(p, c, r, mu, lv, w=(0.1, 0.1, 1.0, 1.0), n_enc=4, n_dec=4, dt=np.fl
     the loss stay fp32).  f8b: {layer name: weight scale} (``fp8b_layers``) — those layers' dX
     GEMMs run in e4m3 with MX row-block scales (``mx_dx``; the wide chain's CVAE_FP8 form); their
     dW stays bf16 — unless the layer is in ``mxw`` (``mxw_layers``): then its dW is ``mx_dw``.
+    trace: a dict that receives {layer name: (G, X)}, the rounded operands of each dW GEMM.
     """
     f8b = f8b or {}
     mxw = mxw or set()
@@ -253,6 +257,8 @@ def backward(p, c, r, mu, lv, w=(0.1, 0.1, 1.0, 1.0), n_enc=4, n_dec=4, dt=np.fl
 
     def lin_grads(name, G, X):
         G, X = q(G), q(X)
+        if trace is not None:  # the operands of the layer's dW GEMM (gT, xT of the arena)
+            trace[name] = (G, X)
         g[name + ".weight"] = mx_dw(G, X) if name in mxw else G.T @ X
         g[name + ".bias"] = G.sum(0)
         if name in f8b:

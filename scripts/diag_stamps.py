@@ -18,9 +18,14 @@ B = int(os.environ.get("B", "1024"))
 dtype = os.environ.get("DT", "bf16")
 torch.manual_seed(0)
 WIDE = os.environ.get("WIDE") == "1"  # BASELINE cfg5's shape (the wide chain)
-m = ConditionalTrajectoryVAE(200, 6, 512, 128, 8, 8) if WIDE else ConditionalTrajectoryVAE(100, 6, 8)
+F32 = os.environ.get("F32") == "1"    # the reference's own shape in fp32 (the fp32 ring chain)
+if F32:
+    dtype = "fp32"
+    m = ConditionalTrajectoryVAE(10, 3, 8)
+else:
+    m = ConditionalTrajectoryVAE(200, 6, 512, 128, 8, 8) if WIDE else ConditionalTrajectoryVAE(100, 6, 8)
 eng = m.attach(dtype=dtype, max_batch=B)
-x = eng.as_input(torch.randn(B, 200, 6) if WIDE else torch.randn(B, 100, 6))
+x = eng.as_input(torch.randn(B, 10, 3) * 5 if F32 else torch.randn(B, 200, 6) if WIDE else torch.randn(B, 100, 6))
 L = lib()
 L.cvae_diag_set_stamps.argtypes = [C.c_void_p, C.c_void_p]
 L.cvae_diag_set_wstamps.argtypes = [C.c_void_p]
@@ -67,6 +72,9 @@ if os.environ.get("RING") == "1":  # the reference architecture on the ring chai
         names = (["pro:issue", "pro:transform", "pro:bar", "C0+copies", "E0 gemm", "E0 epi", "C1|E1", "E2", "E3",
                   "FC", "reparam", "D0", "D1", "D2", "D3+loss", "fixup", "D3b", "D2b", "D1b", "D0b", "FCb gemm",
                   "FCb epi", "E3b", "E2b", "E1b|C1b", "partials"])
+if F32:  # cvae_f32chain.h's barriers
+    names = ["prologue", "C0|E0", "C1|E1", "E2", "E3", "FC", "reparam|D0 h_c", "D0 z", "D1", "D2", "D3", "loss",
+             "fixup", "D3b", "D2b", "D1b", "D0b", "FCb", "E3b", "E2b", "E1b|C1b", "partials"]
 for i in range(k - 1):
     print(f"{names[i]:>14s} {i:2d}: median {np.median(d[:, i]) / 1000:7.3f} us   max {d[:, i].max() / 1000:7.3f} us"
           f"   block0 {d[0, i] / 1000:7.3f} us")
