@@ -347,6 +347,9 @@ def main():
     ap.add_argument("--torch-allreduce", action="store_true",
                     help="split step: torch.distributed's all_reduce instead of the library's own RCCL "
                          "communicator on the step's stream (cvae_rccl_*; A/B)")
+    ap.add_argument("--shard-adam", action="store_true",
+                    help="split step (rccl): reduce-scatter of the gradient, Adam on this rank's 1/N of the flat "
+                         "state, all-gather of the parameters, repack (instead of all-reduce + the whole Adam)")
     ap.add_argument("--buckets", type=int, default=1, choices=[1, 2],
                     help="split step: 2 = decoder-gradient all-reduce overlapped with the rest of dW")
     ap.add_argument("--graph", action="store_true",
@@ -413,8 +416,8 @@ def main():
     model = ConditionalTrajectoryVAE(S, D, Z, H, NE, ND, n_classes=NC, class_dim=CE or 16)
     eng = model.attach(dtype=dtype, max_batch=B, device=dev, seed=4321)
     dp = DataParallelStep(eng, force_split=args.dp, buckets=args.buckets,
-                          exchange="rccl" if wl in ("cfg1", "cfg4") else args.exchange,
-                          native=False if args.torch_allreduce else None)
+                          exchange="rccl" if wl in ("cfg1", "cfg4") or args.shard_adam else args.exchange,
+                          native=False if args.torch_allreduce else None, shard_adam=args.shard_adam)
     dp.broadcast_params()
 
     if wl == "cfg1":
@@ -628,7 +631,8 @@ def main():
                "scaling": "weak", "vs_baseline": None, "dtype": dtype, "data": data,
                "config": {"workload": f"{wl}: Training_VAE step, B_local={B} S={S} D={D} Z={Z} H={H}, "
                                       f"{NE}+{ND} layers, {dtype} operands / fp32 master+Adam, {path} step"
-                                      + (f", rccl all-reduce ({'library communicator on the step stream' if dp.rccl is not None else 'torch.distributed'}), {args.buckets} buckets"
+                                      + ((", sharded Adam (reduce-scatter, Adam on 1/N, all-gather, repack)" if dp.shard_adam else
+                                          f", rccl all-reduce ({'library communicator on the step stream' if dp.rccl is not None else 'torch.distributed'}), {args.buckets} buckets")
                                          if dp.split and dp.px is None else "") + (f" [{dp.exchange_note}]" if dp.exchange_note else ""),
                           "global_batch": B * world, "seq_len": S, "state_dim": D, "latent_dim": Z,
                           "hidden_dim": H, "parallelism": f"dp{world}" + (" (rehearsal: all ranks on GPU 0)"

@@ -1350,6 +1350,37 @@ int cvae_adam(cvae_handle* h, float* params, const float* grads, float* m, float
                  (const TileDesc*)h->d_tiles, aa);
 }
 
+namespace {
+// elementwise Adam over params/m/v[lo, lo + count) with the shard's gradient g[0, count) (cvae_adam_flat)
+__global__ void adam_flat_kernel(float* params, const float* g, float* m, float* v, int64_t lo, int64_t count,
+                                 AdamArgs a) {
+  adam_resolve(a, adam_step_load(a));
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (int64_t)gridDim.x * blockDim.x) {
+    float mm = m[lo + i], vv = v[lo + i];
+    const float p = adam_math(params[lo + i], g[i] * a.grad_scale, mm, vv, a);
+    params[lo + i] = p;
+    m[lo + i] = mm;
+    v[lo + i] = vv;
+  }
+}
+}  // namespace
+
+int cvae_adam_flat(cvae_handle* h, float* params, const float* grads, float* m, float* v, int64_t lo, int64_t count,
+                   int64_t step, const cvae_adam_config* adam, float grad_scale, const uint64_t* counters,
+                   void* stream) {
+  if (!h || !params || !m || !v || (count > 0 && !grads)) return fail(CVAE_E_INVALID, "null argument");
+  if (lo < 0 || count < 0 || lo + count > h->nparams) return fail(CVAE_E_INVALID, "range outside the parameters");
+  if (!counters && step < 1) return fail(CVAE_E_INVALID, "step must be >= 1");
+  int rc = check_adam(adam);
+  if (!rc) rc = check_fault(h);
+  if (rc || count == 0) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const AdamArgs aa = make_adam(params, (float*)grads, m, v, step, *adam, grad_scale, counters);
+  if ((rc = tmark(h, s, "adam_flat"))) return rc;
+  const int blocks = (int)std::min<int64_t>((count + 255) / 256, 2048);
+  return klaunch(h, adam_flat_kernel, dim3(blocks), dim3(256), 0, s, params, grads, m, v, lo, count, aa);
+}
+
 int cvae_train_step(cvae_handle* h, const void* x, const int64_t* idx, const int32_t* classes, int batch, int xflags,
                     const float* eps,
                     uint64_t seed, uint64_t offset, int64_t eps_row0, const cvae_loss_weights* w, float* params,

@@ -91,7 +91,12 @@ struct LossArgs {
 #define CVAE_DIAG_NOADAM 0  // timing only: the update is p − lr·g (no moments)
 #endif
 // One element of torch's Adam, in its op order; m and v are updated in place.
+// No FMA contraction inside (hipcc contracts across statements by default): every kernel that applies
+// Adam — the fused dW ⊕ Adam epilogues, param_kernel, the peer exchange's owners, the sharded flat Adam
+// (cvae_adam_flat) — rounds each torch op separately, so they agree bit for bit whatever code
+// surrounds the inlined call.
 __device__ __forceinline__ float adam_math(float p, float g, float& m, float& v, const AdamArgs& a) {
+#pragma clang fp contract(off)
   if (CVAE_DIAG_NOADAM) return p + a.lr_neg_step * g;
   // exp_avg.lerp_(grad, 1 - beta1): weight < 0.5 branch of at::lerp
   m = a.beta1_w < 0.5f ? m + a.beta1_w * (g - m) : g - (g - m) * (1.f - a.beta1_w);

@@ -63,6 +63,8 @@ _SIGS = {
     "cvae_backward": (_i, [_v, _v, _v, _v, _i, _i, _v, _v, _u64, _u64, _i64, _v, _v, _v, _v, _v, _v]),
     # h, params, grads, m, v, step, adam, grad_scale, counters, stream
     "cvae_adam": (_i, [_v, _v, _v, _v, _v, _i64, _A, _f, _v, _v]),
+    # h, params, grads (the shard), m, v, lo, count, step, adam, grad_scale, counters, stream
+    "cvae_adam_flat": (_i, [_v, _v, _v, _v, _v, _i64, _i64, _i64, _A, _f, _v, _v]),
     # h, x, idx, classes, batch, xflags, eps, seed, offset, eps_row0, w, params, m, v, step, adam, loss_out,
     # loss_accum, counters, stream
     "cvae_train_step": (_i, [_v, _v, _v, _v, _i, _i, _v, _u64, _u64, _i64, _W, _v, _v, _v, _i64, _A, _v, _v, _v,

@@ -140,8 +140,14 @@ class DataParallelStep:
     ``buckets``: 1 = one all-reduce after the whole dW launch; 2 = decoder bucket overlapped with
     the rest of the dW GEMMs (see the module docstring)."""
 
-    def __init__(self, engine, group=None, force_split=False, buckets=1, exchange="rccl", native=None):
+    def __init__(self, engine, group=None, force_split=False, buckets=1, exchange="rccl", native=None,
+                 shard_adam=False):
         self.engine = engine
+        # shard_adam (the RCCL path, one bucket): reduce-scatter of the flat gradient, Adam on this rank's
+        # 1/world of the flat state (cvae_adam_flat), all-gather of the parameters, repack — instead of an
+        # all-reduce and the whole Adam on every rank (ZeRO-1: m, v current on their shard only)
+        self.shard_adam = bool(shard_adam)
+        self._sh = None
         self.group = group
         self.rank, self.world_size = world()
         if group is not None:
@@ -179,7 +185,9 @@ class DataParallelStep:
             # communicator is opt-in (native=True) until a multi-GPU run has checked it against
             # torch's all-reduce bit for bit: torch.distributed's RCCL all-reduce by default
             native = hasattr(engine, "_h") and torch.cuda.is_available() and self.world_size == 1 and self.px is None
-        if native and self.split:
+        if self.shard_adam and (buckets != 1 or self.px is not None):
+            raise ValueError("shard_adam is the one-bucket RCCL path")
+        if native and self.split and not self.shard_adam:
             try:
                 self.rccl = NativeRccl(engine, group)
             except Exception as e:  # noqa: BLE001 — torch's all_reduce takes over, and the line says so
@@ -236,6 +244,11 @@ class DataParallelStep:
             eng.skip_step()
             ragged, scale = True, 1.0
         g = eng.grads
+        if self.shard_adam:
+            if ragged and batch > 0:
+                g.mul_(batch / global_batch)
+            self._sharded_update(g, scale)
+            return eng.loss
         if two and self.rccl is not None:  # the communication stream: both buckets, in order
             main = torch.cuda.current_stream(eng.device)
             if self._comm_stream is None:
@@ -275,11 +288,71 @@ class DataParallelStep:
         eng.adam_step(grad_scale=scale)
         return eng.loss
 
+    # ---- the sharded optimizer (shard_adam)
+    def _shard_bufs(self):
+        """(n, shard, lo, count): the flat state cut into world slices of ``shard`` elements (a multiple
+        of 64), this rank's [lo, lo + count); buffers for the padded collectives."""
+        eng = self.engine
+        n, w = eng.n_params, self.world_size
+        shard = -(-(-(-n // w)) // 64) * 64
+        lo = self.rank * shard
+        cnt = max(0, min(shard, n - lo))
+        if self._sh is None:
+            kw = dict(device=eng.params.device, dtype=torch.float32)
+            self._sh = {"gpad": torch.zeros(w * shard, **kw), "gsh": torch.zeros(shard, **kw),
+                        "ppad": torch.zeros(w * shard, **kw), "psh": torch.zeros(shard, **kw)}
+        return n, shard, lo, cnt
+
+    def _reduce_scatter(self, out, inp):
+        if not dist.is_initialized():
+            out.copy_(inp)
+        elif dist.get_backend(self.group) == "nccl":
+            dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=self.group)
+        else:  # gloo has no reduce-scatter: the all-reduced sum, this rank's slice of it
+            t = inp.clone()
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+            out.copy_(t[self.rank * out.numel():(self.rank + 1) * out.numel()])
+
+    def _all_gather(self, out, inp):
+        if not dist.is_initialized():
+            out.copy_(inp)
+        elif dist.get_backend(self.group) == "nccl":
+            dist.all_gather_into_tensor(out, inp, group=self.group)
+        else:
+            dist.all_gather(list(out.chunk(self.world_size)), inp, group=self.group)
+
+    def _gather_flat(self, t):
+        """Whole ``t`` (a flat n-element state buffer current on each rank's shard) on every rank."""
+        n, shard, lo, cnt = self._shard_bufs()
+        b = self._sh
+        b["psh"].zero_()
+        b["psh"][:cnt].copy_(t[lo:lo + cnt])
+        self._all_gather(b["ppad"], b["psh"])
+        t.copy_(b["ppad"][:n])
+
+    def _sharded_update(self, g, grad_scale):
+        """reduce-scatter(grads) → Adam on this rank's shard → all-gather(params) → repack."""
+        eng = self.engine
+        n, shard, lo, cnt = self._shard_bufs()
+        b = self._sh
+        b["gpad"][:n].copy_(g)
+        self._reduce_scatter(b["gsh"], b["gpad"])
+        if cnt > 0:
+            eng.adam_flat(b["gsh"][:cnt], lo, grad_scale)
+        else:
+            eng.adam_flat(b["gsh"][:0], 0, grad_scale)  # no elements: nothing to update
+        self._gather_flat(eng.params)
+        eng.pack()
+
     def sync_state(self):
         """Whole parameters and Adam moments on every rank (the peer exchange keeps each element
-        current on its owner only); a no-op for the all-reduce path, where every rank holds all."""
+        current on its owner only, shard_adam keeps m and v current on their shard); a no-op for the
+        all-reduce path, where every rank holds all."""
         if self.px is not None:
             self.px.gather_state()
+        if self.shard_adam and self.world_size > 1:
+            self._gather_flat(self.engine.m)
+            self._gather_flat(self.engine.v)
 
     def counters_changed(self):
         """The device step counter was set from outside the step (a resume, a restore): the peer

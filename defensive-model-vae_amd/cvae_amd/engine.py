@@ -472,6 +472,15 @@ class CVAEEngine:
         check(lib().cvae_adam(self._h, ptr(self.params), ptr(self.grads), ptr(self.m), ptr(self.v), 0,
                               C.byref(a), float(grad_scale), ptr(self.counters), self._stream()), "cvae_adam")
 
+    def adam_flat(self, grads, lo, grad_scale=1.0):
+        """Adam on params/m/v[lo, lo + len(grads)) from the summed gradient shard ``grads``
+        (cvae_adam_flat: the sharded optimizer of the RCCL data-parallel step); the step number is
+        the device counter.  The operand copies are left stale: ``pack()`` after the all-gather."""
+        a = self._adam()
+        check(lib().cvae_adam_flat(self._h, ptr(self.params), ptr(grads), ptr(self.m), ptr(self.v), int(lo),
+                                   int(grads.numel()), 0, C.byref(a), float(grad_scale), ptr(self.counters),
+                                   self._stream()), "cvae_adam_flat")
+
     def skip_step(self):
         """A data-parallel step with no rows on this rank (cvae_step_skip): the device counters
         advance as a forward_backward would (step begun + its Adam scalars, Philox offset), so the

@@ -119,7 +119,8 @@ def save_checkpoint(path, model, eng, epoch, loss_history):
 def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidden_dim=128,
           weights=(0.1, 0.1, 1.0, 1.0), model_save_path=None, loss_save_path=None, dtype="fp32",
           eps="host", device=None, seed=None, engine_seed=0, log=print, model=None, buckets=1,
-          checkpoint_path=None, resume=None, classes=None, class_dim=0, exchange="auto", epochs_per_call=64):
+          checkpoint_path=None, resume=None, classes=None, class_dim=0, exchange="auto", epochs_per_call=64,
+          shard_adam=False):
     """Train like ``python Training_VAE.py`` (mode='training').
 
     data: path to the (N, seq_len, dim) ``.npy`` (TrajectoryDataset, :105-115) or an array; or a
@@ -133,7 +134,9 @@ def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidd
     then per rank (global batch = batch_size · world) and rank 0 logs and saves; ``exchange``
     picks the gradient exchange ("auto": the in-kernel peer exchange where the configuration has
     it — cvae_amd.peer — else the RCCL all-reduce; "rccl"; "peer"); ``buckets=2`` overlaps the
-    decoder gradients' all-reduce with the rest of the dW GEMMs (rccl).
+    decoder gradients' all-reduce with the rest of the dW GEMMs (rccl); ``shard_adam`` replaces the
+    all-reduce and the whole Adam on every rank by a reduce-scatter, Adam on the rank's 1/world of
+    the flat state and an all-gather of the parameters (rccl, one bucket).
 
     checkpoint_path: write a resume point (save_checkpoint) after every epoch; resume: continue
     from one — ``epochs`` counts the total, so train(epochs=4, resume=ckpt_after_2) runs epochs 3-4
@@ -179,7 +182,8 @@ def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidd
     eng.set_optimizer(lr=lr)
     eng.weights = tuple(float(w) for w in weights)
     eng.keep_f32 = True                                   # relative transform in fp32 (see above)
-    step = dp.DataParallelStep(eng, buckets=buckets, exchange="rccl" if classes is not None else exchange)
+    step = dp.DataParallelStep(eng, buckets=buckets, exchange="rccl" if classes is not None or shard_adam else exchange,
+                               shard_adam=shard_adam)
     step.broadcast_params()
     x_dev = eng.as_input(torch.from_numpy(arr), keep_f32=True)  # resident for the whole run
     cls_dev = None if classes is None else torch.from_numpy(classes).to(x_dev.device)

@@ -225,6 +225,16 @@ int cvae_backward(cvae_handle* h, const void* x, const int64_t* idx, const int32
 int cvae_adam(cvae_handle* h, float* params, const float* grads, float* m, float* v, int64_t step,
               const cvae_adam_config* adam, float grad_scale, const uint64_t* counters, void* stream);
 
+/* Adam on one contiguous range of the flat fp32 state — the sharded optimizer of the RCCL data-
+ * parallel step (cvae_amd.dist, shard_adam): after a reduce-scatter of the flat gradient each rank
+ * updates params/m/v[lo, lo + count) from `grads` (its summed shard, count floats, times
+ * grad_scale), torch's op order (as cvae_adam); the step's scalars from `counters` (or `step`).  The
+ * operand copies are NOT rewritten: the caller all-gathers the parameters and calls
+ * cvae_pack_weights.  Replaces optimizer.step() (Training_VAE.py:363) for one shard. */
+int cvae_adam_flat(cvae_handle* h, float* params, const float* grads, float* m, float* v, int64_t lo, int64_t count,
+                   int64_t step, const cvae_adam_config* adam, float grad_scale, const uint64_t* counters,
+                   void* stream);
+
 /* Fused single-device step: cvae_train_fwd_bwd + cvae_adam with the weight
  * gradient GEMMs and Adam in one kernel (the gradient never round-trips HBM).
  * Replaces the whole body of Training_VAE.py:345-370 for one batch. */

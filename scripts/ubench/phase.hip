@@ -83,6 +83,41 @@ __global__ __launch_bounds__(512) void kA(const __bf16* W, __bf16* out, int nste
   }
 }
 
+// ---- E: the step's B operand from a resident LDS weight image (the decoder layers'
+// forward fragments kept in LDS and read transposed for their dX instead of streaming the Wᵀ copy).
+// The 32-KB image holds 8 n-tiles × [128 K-features][16 columns] bf16 in the activation-image layout
+// (row quad q of feature f at slot q ^ ((f >> 2) & 3)), so a wave's fragment of chunk c is two
+// ds_read_b64_tr_b16 — the same transposed read as its X operand.  MODE bit1: no global stores.
+template <int MODE>
+__global__ __launch_bounds__(512) void kE(const __bf16* W, __bf16* out, int nstep) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  auto img = [&](int i) { return (__bf16*)(smem + (i & 1) * 4096); };
+  const __bf16* wimg = (const __bf16*)(smem + 8192);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, n16 = lane & 15, q = lane >> 4;
+  const int n = wave * 16 + n16;
+  if (tid < 512) ((u32x4*)smem)[tid] = u32x4{0, 0, 0, 0};
+  for (int i = tid; i < 32768 / 16; i += 512) ((u32x4*)(smem + 8192))[i] = *(const G u32x4*)((const char*)W + i * 16);
+  lbar();
+  for (int s = 0; s < nstep; ++s) {
+    const __bf16* in = img(s);
+    __bf16* o = img(s + 1);
+    bf16x8 x[4], w[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) x[c] = xfrag(in, c);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) w[c] = xfrag(wimg + wave * 2048, c);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[c], w[c], acc, 0, 0, 0);
+    bf16x4 h;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h[i] = (__bf16)fmaxf(acc[i] * 0.01f, 0.f);
+    *(bf16x4*)(o + n * 16 + 4 * q) = h;
+    if (!(MODE & 2)) *(G bf16x4*)(out + ((size_t)blockIdx.x * nstep + s) * 2048 + n * 16 + 4 * q) = h;
+    lbar();
+  }
+}
+
 // ---- B: loader waves
 template <int L, int LA>
 __global__ __launch_bounds__(64 * (8 + L)) void kB(const __bf16* W, __bf16* out, int nstep) {
@@ -371,6 +406,18 @@ int main(int argc, char** argv) {
   hipFuncSetAttribute((const void*)kC<3, 0, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 8192 + 3 * WSTEP + 64);
   hipFuncSetAttribute((const void*)kC<3, 0, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 8192 + 3 * WSTEP + 64);
   hipFuncSetAttribute((const void*)kC<3, 2, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 8192 + 3 * WSTEP + 64);
+  if (argc > 1 && argv[1][0] == 'E') {  // B from a resident LDS image vs streamed
+    hipFuncSetAttribute((const void*)kE<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 8192 + 32768);
+    hipFuncSetAttribute((const void*)kE<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 8192 + 32768);
+    for (int rep = 0; rep < 2; ++rep) {
+      per_step("A LA=2 (the chain's form)", [&](int s) { hipLaunchKernelGGL((kA<0, 3>), dim3(64), dim3(512), 8192, 0, W, out, s); });
+      per_step("E B from LDS (tr reads)", [&](int s) { hipLaunchKernelGGL((kE<0>), dim3(64), dim3(512), 8192 + 32768, 0, W, out, s); });
+      per_step("A LA=2 no loads", [&](int s) { hipLaunchKernelGGL((kA<1, 3>), dim3(64), dim3(512), 8192, 0, W, out, s); });
+      per_step("A LA=2 no stores", [&](int s) { hipLaunchKernelGGL((kA<2, 3>), dim3(64), dim3(512), 8192, 0, W, out, s); });
+      per_step("E B from LDS, no stores", [&](int s) { hipLaunchKernelGGL((kE<2>), dim3(64), dim3(512), 8192 + 32768, 0, W, out, s); });
+    }
+    return 0;
+  }
   if (only_d) {
     unsigned* ctr;
     __bf16* xch;

@@ -94,6 +94,23 @@ class OracleEngine:
         self.params.addcdiv_(self.m, denom, value=-(self.lr / bc1))
         self.pack()
 
+    @property
+    def n_params(self):
+        return self.params.numel()
+
+    def adam_flat(self, grads, lo, grad_scale=1.0):
+        """cvae_adam_flat: adam_step's arithmetic on params/m/v[lo, lo + len(grads)) only."""
+        b1, b2 = self.betas
+        hi = lo + grads.numel()
+        g = grads * grad_scale if grad_scale != 1.0 else grads
+        m, v, p = self.m[lo:hi], self.v[lo:hi], self.params[lo:hi]
+        m.lerp_(g, 1 - b1)
+        v.mul_(b2).addcmul_(g, g, value=1 - b2)
+        bc1 = 1 - b1 ** self.step_count
+        bc2 = 1 - b2 ** self.step_count
+        denom = (v.sqrt() / (bc2 ** 0.5)).add_(self.eps)
+        p.addcdiv_(m, denom, value=-(self.lr / bc1))
+
     def train_step(self, x, idx=None, eps=None, batch=None, weights=None, accumulate=True, row0=0, classes=None):
         self.forward_backward(x, idx=idx, eps=eps, batch=batch, weights=weights, accumulate=accumulate,
                               classes=classes)

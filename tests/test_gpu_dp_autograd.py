@@ -217,6 +217,40 @@ def test_dp_split_buckets_graph_rccl_equal_fused(cvae, native):
         tdist.destroy_process_group()
 
 
+def test_dp_sharded_adam_rccl_equals_fused(cvae):
+    """The sharded optimizer of the RCCL data-parallel step (shard_adam: reduce-scatter of the flat
+    gradient, Adam on this rank's 1/world of the flat state — cvae_adam_flat —, all-gather of the
+    parameters, repack) through a real world-1 RCCL group equals the fused single-GPU step bit for
+    bit after 4 steps: parameters, moments, device counters, and the operand copies the next steps
+    multiply (their losses)."""
+    import torch.distributed as tdist
+    from cvae_amd.dist import DataParallelStep
+    assert not tdist.is_initialized()
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    tdist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1,
+                             device_id=torch.device("cuda", 0))
+    try:
+        torch.manual_seed(0)
+        ref = OracleCVAE(100, 6, 8)
+        e0 = _model(cvae, 100, 6, 8, sd=ref.state_dict(), dtype="bf16", max_batch=256)[1]
+        e1 = _model(cvae, 100, 6, 8, sd=ref.state_dict(), dtype="bf16", max_batch=256)[1]
+        x = e0.as_input(torch.randn(256, 100, 6, generator=torch.Generator().manual_seed(7)))
+        d = DataParallelStep(e1, force_split=True, shard_adam=True)
+        assert d.rccl is None  # the collectives are torch.distributed's (RCCL under the nccl backend)
+        for _ in range(4):
+            l0 = e0.train_step(x).clone()
+            l1 = d.step(x, batch=256).clone()
+            assert torch.equal(l0, l1)
+        torch.cuda.synchronize()
+        assert torch.equal(e0.params, e1.params)
+        assert torch.equal(e0.m, e1.m) and torch.equal(e0.v, e1.v)
+        assert torch.equal(e0.counters, e1.counters)
+        assert e0.operand_checksum() == e1.operand_checksum()
+        d.close()
+    finally:
+        tdist.destroy_process_group()
+
+
 # ---------------------------------------------------------------- autograd boundary
 def test_loss_backward_matches_autograd(cvae):
     """cvae_loss_backward (the a9 loss-gradient kernel) == torch autograd of the oracle loss, for an
