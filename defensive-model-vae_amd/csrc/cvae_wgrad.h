@@ -95,8 +95,13 @@ struct LossArgs {
 // Adam — the fused dW ⊕ Adam epilogues, param_kernel, the peer exchange's owners, the sharded flat Adam
 // (cvae_adam_flat) — rounds each torch op separately, so they agree bit for bit whatever code
 // surrounds the inlined call.
+#ifndef CVAE_ADAM_CONTRACT
+#define CVAE_ADAM_CONTRACT 0  // diagnostic builds only: hipcc's default contraction (the A/B of its cost)
+#endif
 __device__ __forceinline__ float adam_math(float p, float g, float& m, float& v, const AdamArgs& a) {
+#if !CVAE_ADAM_CONTRACT
 #pragma clang fp contract(off)
+#endif
   if (CVAE_DIAG_NOADAM) return p + a.lr_neg_step * g;
   // exp_avg.lerp_(grad, 1 - beta1): weight < 0.5 branch of at::lerp
   m = a.beta1_w < 0.5f ? m + a.beta1_w * (g - m) : g - (g - m) * (1.f - a.beta1_w);
