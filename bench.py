@@ -265,7 +265,7 @@ def rank_envs(n, env, port):
     return out
 
 
-def run_ranks(cmd, envs, out, grace_s=60.0, poll_s=0.05):
+def run_ranks(cmd, envs, out, grace_s=60.0, poll_s=0.05, done_grace_s=300.0):
     """Start one child per environment running ``cmd``, forward rank 0's result line to ``out``, and
     return the worst exit status (the first non-zero one in rank order among the ranks that ended by
     themselves, else 0).  Rank 0's stdout is
@@ -292,10 +292,17 @@ def run_ranks(cmd, envs, out, grace_s=60.0, poll_s=0.05):
                 print(s, file=sys.stderr, flush=True)
     th = threading.Thread(target=pump, daemon=True)
     th.start()
-    deadline, killed = None, set()
+    deadline, fail_at, killed = None, None, set()
     while None in [p.poll() for p in procs]:  # a list: every child polled each round
-        if deadline is None and any(p.returncode not in (None, 0) for p in procs):
-            deadline = time.monotonic() + grace_s
+        # a rank that failed: the rest get grace_s; one that finished cleanly while others still run
+        # (rank 0's CPU-baseline leg, or a peer stuck in a collective the finished rank never entered):
+        # done_grace_s, then the rest are killed
+        now = time.monotonic()
+        if fail_at is None and any(p.returncode not in (None, 0) for p in procs):
+            fail_at = now
+            deadline = min(deadline or float("inf"), now + grace_s)
+        if deadline is None and any(p.returncode == 0 for p in procs):
+            deadline = now + done_grace_s
         if deadline is not None and time.monotonic() > deadline:
             for r, p in enumerate(procs):
                 if p.poll() is None:

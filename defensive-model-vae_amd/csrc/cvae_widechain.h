@@ -828,6 +828,9 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   // other wave (3) has the lightest one — and reaches wave 0's lanes (which hold mu, logvar)
   // through LDS across the prologue barrier (the recon time-channel buffer, idle until the loss)
   const bool eps_mine = !A::SZ || wave == NW - 1;  // wave-uniform
+  // SZ: the eps hand-off (last wave → wave 0) in the recon time-channel buffer — in an F8 layout that
+  // offset is also the e4m3 input / decoder-input twin the prologue writes
+  static_assert(!(A::SZ && A::F8), "EPSX would overlap L_X8 / L_DCAT8");
   float* const EPSX = (float*)(smem + A::L_RCH0);
 
   // ---- prologue: x tile (relative transform, Training_VAE.py:345-348), biases, LDS pads

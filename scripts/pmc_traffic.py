@@ -15,7 +15,7 @@ from collections import defaultdict
 
 
 def short(name):
-    if "rowchain_kernel" in name or "fastchain_kernel" in name or "widechain_kernel" in name:
+    if any(k in name for k in ("rowchain_kernel", "fastchain_kernel", "widechain_kernel", "f32chain_kernel")):
         return "rowchain"
     if "wgrad_kernel" in name:  # wgrad_kernel and fastwgrad_kernel
         return "wgrad_adam"

@@ -8,6 +8,7 @@ import json
 import os
 import subprocess
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -112,3 +113,17 @@ def test_cli_mismatch_exits_before_gpu():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4096"], env=env,
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == 2 and "GPU(s) are visible" in p.stderr and p.stdout == ""
+
+
+def test_run_ranks_bounds_a_peer_left_behind_by_a_clean_exit():
+    """rank 0 exits 0 while rank 1 hangs (e.g. in a collective rank 0 skipped) — the parent
+    kills it after done_grace_s instead of polling forever."""
+    child = ("import os, sys, time\n"
+             "if os.environ['RANK'] == '1': time.sleep(60)\n"
+             "sys.exit(0)\n")
+    out = io.StringIO()
+    t0 = time.monotonic()
+    rc = bench.run_ranks([sys.executable, "-c", child], bench.rank_envs(2, dict(os.environ), 1), out, grace_s=1,
+                         done_grace_s=1)
+    assert time.monotonic() - t0 < 30
+    assert rc != 0
