@@ -23,6 +23,12 @@
  * accumulators are fp64 (the reference sums loss.item()*B in Python doubles,
  * Training_VAE.py:366-370), eps rows are keyed by a global row offset, and the
  * training calls take optional device step counters.
+ *
+ * ABI 3 (rounds 5-6): the library's own RCCL communicator (cvae_rccl_*), an armed
+ * tap consumed by cvae_train_fwd_bwd only, the fp32 chain's kernel id
+ * (CVAE_KERNEL_F32), arena introspection (cvae_read_activation), whole shuffled
+ * epochs in one call (cvae_train_epochs) and Adam over a flat range
+ * (cvae_adam_flat, the sharded-Adam data-parallel step).
  */
 #ifndef CVAE_H
 #define CVAE_H

@@ -84,6 +84,7 @@ def test_fwd_bwd_fixed_weights_grads(cvae, golden):
     d = golden("sce_fixed.npz")
     sd = {k[2:]: d[k] for k in d.files if k.startswith("w/")}
     m, eng = _model(cvae, 10, 3, 8, sd=sd)
+    assert eng.train_kernel == "f32"  # the reference's shape runs the fp32 ring chain (cvae_f32chain.h)
     x = torch.from_numpy(d["sce1_x"])
     loss = eng.forward_backward(x, eps=torch.from_numpy(d["sce1_eps"])).cpu().numpy()
     np.testing.assert_allclose(loss, d["sce1_losses_eps"], rtol=2e-5)
@@ -151,6 +152,7 @@ def test_traj20_reference_train_loop(cvae, golden):
     torch.manual_seed(int(d["seed"]))
     ref = OracleCVAE(10, 3, 8)
     m, eng = _model(cvae, 10, 3, 8, sd=ref.state_dict())
+    assert eng.train_kernel == "f32"
     data = torch.from_numpy(x).cuda()
     order, eps_all, rows = d["order"], d["eps"], d["eps_rows"]
     o = 0
@@ -182,11 +184,12 @@ def test_idx_gather_equals_pregathered(cvae):
     assert torch.equal(e1.grads, e2.grads)
 
 
-@pytest.mark.parametrize("B", [1, 17, 33, 256])
+@pytest.mark.parametrize("B", [1, 17, 33, 38, 256])
 def test_ragged_batches_vs_oracle(cvae, B):
     torch.manual_seed(B)
     ref = OracleCVAE(10, 3, 8)
     m, eng = _model(cvae, 10, 3, 8, sd=ref.state_dict())
+    assert eng.train_kernel == "f32"
     x = torch.randn(B, 10, 3) * 10
     eps = torch.randn(B, 8)
     loss = eng.forward_backward(x, eps=eps).cpu().numpy()
