@@ -23,6 +23,7 @@
 #include "cvae_widechain.h"
 #include "cvae_widewgrad.h"
 #include "cvae_f32chain.h"
+#include "cvae_f32wgrad.h"
 #include "cvae_extract.h"
 #include "cvae_mpc.h"
 
@@ -114,6 +115,7 @@ struct cvae_handle {
   int ring_lds = 0;
   bool f32c = false;        // fp32 training at the reference's own shape (seq_len 10, dim 3): f32c::f32chain_kernel<Cfg1>
   int f32c_lds = 0;
+  bool f32c_dw = false;      // ... and its dW ⊕ Adam with the compile-time tile decode (f32c::f32wgrad_kernel)
   bool timing = false;
   // timing: per call, a chain of events on the caller's stream; segment i of a
   // call spans ev[i] → ev[i+1] and is named by the kernel launched after ev[i]
@@ -806,6 +808,35 @@ bool f32c_layout_matches(const cvae_handle* h) {
   return true;
 }
 
+// the fp32 chain's compile-time dW decode (cvae_f32wgrad.h) covers the handle's 32 × 32 tile list
+// exactly (as a set: each tile is one independent wgrad_body) and restates every layer record
+template <class A>
+bool f32c_dw_matches(const cvae_handle* h) {
+  using WT = f32c::WTiles<A>;
+  if (h->wtiles_ni2 || (int)h->wtiles.size() != WT::total()) return false;
+  std::vector<int> seen(WT::total(), 0);
+  for (int b = 0; b < WT::total(); ++b) {
+    const TileDesc t = WT::at(b);
+    int hit = -1;
+    for (int u = 0; u < (int)h->wtiles.size(); ++u) {
+      const TileDesc& w = h->wtiles[u];
+      if (w.layer == t.layer && w.o0 == t.o0 && w.i0 == t.i0 && w.ni <= 1) hit = u;
+    }
+    if (hit < 0 || seen[hit]++) return false;
+  }
+  for (int l = 0; l < f32c::NL; ++l) {
+    const LayerDev& L = h->net.L[l];
+    const LayerDev F = f32c::f32_layer<A>(l, h->arena, h->net.Bp);
+    if (F.K != L.K || F.N != L.N || F.Kp != L.Kp || F.Np != L.Np || F.relu != L.relu || F.nseg != L.nseg ||
+        F.seg_rows0 != L.seg_rows0 || F.f8 != L.f8 || F.wt != L.wt || F.has_bias != L.has_bias || F.Wf != L.Wf ||
+        F.Wb != L.Wb || F.bias != L.bias || F.xT != L.xT || F.gT != L.gT || F.f8b != L.f8b || F.Wb8 != L.Wb8)
+      return false;
+    for (int g = 0; g < 2; ++g)
+      if (F.pw[g] != L.pw[g] || F.pb[g] != L.pb[g]) return false;
+  }
+  return true;
+}
+
 int plan_f32c(cvae_handle* h) {
   using A = f32c::Cfg1;
   const cvae_config& c = h->cfg;
@@ -820,6 +851,8 @@ int plan_f32c(cvae_handle* h) {
                             A::L_TOTAL));
   h->f32c = true;
   h->f32c_lds = A::L_TOTAL;
+  const char* dw = std::getenv("CVAE_F32_DW");  // "generic": the tile-list kernel (A/B)
+  h->f32c_dw = !(dw && std::strcmp(dw, "generic") == 0) && f32c_dw_matches<A>(h);
   return CVAE_OK;
 }
 
@@ -1068,6 +1101,9 @@ int launch_wgrad(cvae_handle* h, int batch, const AdamArgs& aa, const LossArgs& 
     return klaunch(h, wchain::widewgrad_kernel<wchain::Cfg5, MODE>, dim3(g), dim3(WG_THREADS), 0, s, h->arena,
                    aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), aa, la, sk);
   }
+  if (h->f32c_dw)
+    return klaunch(h, f32c::f32wgrad_kernel<f32c::Cfg1, MODE>, dim3(f32c::WTiles<f32c::Cfg1>::total() * sk.S + 1),
+                   dim3(WG_THREADS), 0, s, h->arena, aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), aa, la, sk);
   if (h->fast_nki == 19)
     return klaunch(h, fchain::fastwgrad_kernel<19, MODE>, dim3(fchain::Tiles<19>::total() * sk.S + 1),
                    dim3(WG_THREADS), 0, s, h->arena, aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), h->net.S,

@@ -47,6 +47,9 @@ __device__ unsigned long long* g_wstamps;
 #else
 #define WSTAMP(k) do { } while (0)
 #endif
+#ifndef CVAE_DIAG_WSTAMP_ENTRY
+#define CVAE_DIAG_WSTAMP_ENTRY 0  // diagnostic builds: stamp 0 at kernel entry, before the tile decode
+#endif
 
 struct AdamArgs {
   float* params;      // flat fp32 master (state_dict order)
@@ -528,7 +531,7 @@ __device__ __forceinline__ void wgrad_body(const LayerDev& L, const TileDesc td,
   using VE = typename VecF<EPT>::T;
   const int o = tid / TPR, iv = (tid % TPR) * EPT;
 
-  WSTAMP(0);
+  if (!CVAE_DIAG_WSTAMP_ENTRY) WSTAMP(0);
   const adam_f32x2 t_step = MODE == PM_ADAM ? adam_step_load(aa) : adam_f32x2{0.f, 0.f};
   f32x4 acc[2][NX];
 #pragma unroll
@@ -719,6 +722,7 @@ template <typename T, int MODE, bool NI2 = false>
 __global__ __launch_bounds__(WG_THREADS, 4) void wgrad_kernel(NetDev net, const TileDesc* __restrict__ tiles,
                                                            int Bk, AdamArgs aa, LossArgs la, SplitK sk) {
   __shared__ __attribute__((aligned(16))) WgradLds<NI2 ? 2 : 1> sh;
+  if (CVAE_DIAG_WSTAMP_ENTRY) WSTAMP(0);
   const int ntiles = gridDim.x / sk.S;
   sk.s = blockIdx.x / ntiles;
   sk.tile = blockIdx.x - sk.s * ntiles;

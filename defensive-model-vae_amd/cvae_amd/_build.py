@@ -16,7 +16,7 @@ LIB = os.environ.get("CVAE_LIB") or os.path.join(HERE, "libcvae_hip.so")  # CVAE
 SOURCES = ["cvae_capi.hip"]
 HEADERS = ["cvae_device.h", "cvae_rowchain.h", "cvae_fastchain.h", "cvae_fastwgrad.h", "cvae_wgrad.h", "cvae_loss.h",
            "cvae_extract.h", "cvae_mpc.h", "cvae_widechain.h", "cvae_peer.h", "cvae_widewgrad.h",
-           "cvae_f32chain.h"]
+           "cvae_f32chain.h", "cvae_f32wgrad.h"]
 ARCH = "gfx950"
 
 

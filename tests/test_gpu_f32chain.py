@@ -173,3 +173,40 @@ def test_f32_chain_split_equals_fused(cvae, monkeypatch):
     torch.cuda.synchronize()
     assert torch.equal(e1.params, e3.params)
     assert torch.equal(e1.m, e3.m) and torch.equal(e1.v, e3.v)
+
+
+@pytest.mark.parametrize("B", [32, 38, 6, 256])
+def test_f32_dw_decode_equals_generic_tile_list(cvae, monkeypatch, B):
+    """The fp32 chain's dW ⊕ Adam launch decodes its tile and layer record from blockIdx
+    (cvae_f32wgrad.h); CVAE_F32_DW=generic keeps the tile-list kernel.  Each tile is one
+    independent wgrad_body, so the two equal each other bit for bit: gradients (split path), then
+    params, moments, losses and counters after fused training steps (ragged last batch, Philox eps)."""
+    torch.manual_seed(3)
+    ref = OracleCVAE(10, 3, 8)
+    engines = []
+    for mode in (None, "generic"):
+        if mode:
+            monkeypatch.setenv("CVAE_F32_DW", mode)
+        m = cvae.ConditionalTrajectoryVAE(10, 3, 8)
+        m.load_state_dict(ref.state_dict())
+        e = m.attach(dtype="fp32", max_batch=256, device="cuda:0", seed=11)
+        monkeypatch.delenv("CVAE_F32_DW", raising=False)
+        assert e.train_kernel == "f32"
+        engines.append(e)
+    e1, e2 = engines
+    x = _data(300, seed=B)
+    xd1, xd2 = e1.as_input(x), e2.as_input(x)
+    idx = torch.randperm(300, generator=torch.Generator().manual_seed(B))[:B].cuda()
+    for e, xd in ((e1, xd1), (e2, xd2)):
+        e.forward_backward(xd, idx=idx)
+    torch.cuda.synchronize()
+    assert torch.equal(e1.grads, e2.grads)
+    for step in range(4):
+        b = B if step < 3 else max(1, B // 3)  # a ragged last batch
+        for e, xd in ((e1, xd1), (e2, xd2)):
+            e.train_step(xd, idx=idx[:b])
+    torch.cuda.synchronize()
+    assert torch.equal(e1.params, e2.params)
+    assert torch.equal(e1.m, e2.m) and torch.equal(e1.v, e2.v)
+    assert torch.equal(e1.loss, e2.loss)
+    assert torch.equal(e1.loss_accum, e2.loss_accum)
