@@ -445,10 +445,19 @@ def main():
             epochs drawn on the host, uploaded once and issued through one cvae_train_epochs call
             (what cvae_amd.train does); data-parallel: per step."""
             if not dp.split:
-                E = (k + len(sizes) - 1) // len(sizes)  # epochs touched (the last may be cut short)
-                perms = torch.stack([torch.randperm(n_rows, generator=gen) for _ in range(E)])
-                eps = torch.randn(E * n_rows, Z, generator=gen)
-                eng.train_epochs(x, perms.to(dev), B, n_steps=k, eps=eps.to(dev))
+                # in chunks of whole epochs (the last may be cut short), as cvae_amd.train issues them:
+                # a chunk's draws run on the host while the device runs the previous chunk (the engine
+                # uploads through pinned memory, queued behind the kernels); a small first chunk
+                # keeps the one draw that nothing hides short
+                spe, left, ce = len(sizes), k, 4
+                while left > 0:
+                    ks = min(left, ce * spe)
+                    E = (ks + spe - 1) // spe
+                    perms = torch.stack([torch.randperm(n_rows, generator=gen) for _ in range(E)])
+                    eps = torch.randn(E * n_rows, Z, generator=gen)
+                    eng.train_epochs(x, perms, B, n_steps=ks, eps=eps)
+                    left -= ks
+                    ce = 32
                 return
             for _ in range(k):
                 if state["k"] == len(sizes):

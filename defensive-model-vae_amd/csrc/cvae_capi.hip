@@ -115,6 +115,7 @@ struct cvae_handle {
   int ring_lds = 0;
   bool f32c = false;        // fp32 training at the reference's own shape (seq_len 10, dim 3): f32c::f32chain_kernel<Cfg1>
   int f32c_lds = 0;
+  bool cls_dw = false;       // BASELINE cfg4's dW ⊕ Adam with the compile-time decode (wchain::clswgrad_kernel)
   bool f32c_dw = false;      // ... and its dW ⊕ Adam with the compile-time tile decode (f32c::f32wgrad_kernel)
   bool timing = false;
   // timing: per call, a chain of events on the caller's stream; segment i of a
@@ -763,8 +764,31 @@ int plan_ring(cvae_handle* h) {
   return CVAE_OK;
 }
 
-// BASELINE cfg4 (the class embedding) at cfg2's shape on the ring chain (wchain::Cfg4; its dW ⊕ Adam
-// is the generic tile-list kernel: the fast dW decode knows the 11 reference layers only)
+// cfg4's compile-time dW decode (cvae_widewgrad.h CTiles / cls_layer) restates the handle's tile list
+// (order included) and every layer record for this handle's n_classes and class_dim
+template <class A>
+bool cls_dw_matches(const cvae_handle* h) {
+  using CT = wchain::CTiles<A>;
+  if (h->wtiles_ni2 || (int)h->wtiles.size() != CT::total()) return false;
+  for (int b = 0; b < CT::total(); ++b) {
+    const TileDesc t = CT::at(b), u = h->wtiles[b];
+    if (t.layer != u.layer || t.o0 != u.o0 || t.i0 != u.i0 || u.ni > 1) return false;
+  }
+  for (int l = 0; l < A::NL; ++l) {
+    const LayerDev& L = h->net.L[l];
+    const LayerDev F = wchain::cls_layer<A>(l, h->arena, h->net.Bp, h->cfg.n_classes, h->cfg.class_dim);
+    if (F.K != L.K || F.N != L.N || F.Kp != L.Kp || F.Np != L.Np || F.relu != L.relu || F.nseg != L.nseg ||
+        F.seg_rows0 != L.seg_rows0 || F.f8 != L.f8 || F.wt != L.wt || F.has_bias != L.has_bias || F.Wf != L.Wf ||
+        F.Wb != L.Wb || F.bias != L.bias || F.xT != L.xT || F.gT != L.gT || F.f8b != L.f8b || F.Wb8 != L.Wb8)
+      return false;
+    for (int g = 0; g < 2; ++g)
+      if (F.pw[g] != L.pw[g] || F.pb[g] != L.pb[g]) return false;
+  }
+  return true;
+}
+
+// BASELINE cfg4 (the class embedding) at cfg2's shape on the ring chain (wchain::Cfg4), its dW ⊕ Adam
+// on the compile-time decode (wchain::clswgrad_kernel; CVAE_CLS_DW=generic keeps the tile list)
 int plan_ring_cls(cvae_handle* h) {
   using A = wchain::Cfg4;
   const cvae_config& c = h->cfg;
@@ -783,6 +807,8 @@ int plan_ring_cls(cvae_handle* h) {
                             hipFuncAttributeMaxDynamicSharedMemorySize, A::L_TOTAL));
   h->ring_cls = true;
   h->ring_lds = A::L_TOTAL;
+  const char* dw = std::getenv("CVAE_CLS_DW");
+  h->cls_dw = !(dw && std::strcmp(dw, "generic") == 0) && cls_dw_matches<A>(h);
   return CVAE_OK;
 }
 
@@ -1101,6 +1127,10 @@ int launch_wgrad(cvae_handle* h, int batch, const AdamArgs& aa, const LossArgs& 
     return klaunch(h, wchain::widewgrad_kernel<wchain::Cfg5, MODE>, dim3(g), dim3(WG_THREADS), 0, s, h->arena,
                    aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), aa, la, sk);
   }
+  if (h->cls_dw)
+    return klaunch(h, wchain::clswgrad_kernel<wchain::Cfg4, MODE>, dim3(wchain::CTiles<wchain::Cfg4>::total() * sk.S + 1),
+                   dim3(WG_THREADS), 0, s, h->arena, aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch),
+                   h->cfg.n_classes, h->cfg.class_dim, aa, la, sk);
   if (h->f32c_dw)
     return klaunch(h, f32c::f32wgrad_kernel<f32c::Cfg1, MODE>, dim3(f32c::WTiles<f32c::Cfg1>::total() * sk.S + 1),
                    dim3(WG_THREADS), 0, s, h->arena, aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), aa, la, sk);
@@ -1263,6 +1293,16 @@ int cvae_train_kernel(const cvae_handle* h, int* kind) {
            : h->wide              ? CVAE_KERNEL_WIDE
            : h->f32c              ? CVAE_KERNEL_F32
                                   : CVAE_KERNEL_GENERIC;
+  return CVAE_OK;
+}
+
+int cvae_dw_kernel(const cvae_handle* h, int* kind) {
+  if (!h || !kind) return fail(CVAE_E_INVALID, "null argument");
+  *kind = h->wide_dw        ? CVAE_DW_WIDE
+          : h->cls_dw       ? CVAE_DW_CLS
+          : h->f32c_dw      ? CVAE_DW_F32
+          : h->fast_nki == 19 ? CVAE_DW_FAST
+                            : CVAE_DW_GENERIC;
   return CVAE_OK;
 }
 

@@ -142,4 +142,109 @@ __global__ __launch_bounds__(WG_THREADS, 4) void widewgrad_kernel(char* arena, f
     wgrad_body<__bf16, MODE, 1>(L, td, Bk, aa, la, false, A::S, A::D, A::Z, sh.red, sh.dbp, sk);
 }
 
+// BASELINE cfg4 (A::CLS, the class embedding at the reference architecture's shape): the handle's
+// list there is 32 × 32 tiles only (fewer than 512), in the same order (layer by layer, the longer
+// of Np / Kp outermost, XCD chunks); the class-dependent widths — fc's input [h_traj ‖ h_c ‖ e] and
+// decoder L0's [z ‖ h_c ‖ e] grow by class_dim, the table is n_classes × class_dim and the last
+// parameter tensor — come from two runtime arguments.  plan_ring_cls checks the tile list and every
+// layer record against the handle before enabling it (cvae_capi.hip cls_dw_matches).
+template <class A>
+struct CTiles {
+  static constexpr int NL = A::NL;
+  __host__ __device__ static constexpr int count(int l) { return (A::Np(l) / 32) * (A::Kp(l) / 32); }
+  __host__ __device__ static constexpr int start(int l) {
+    int t = 0;
+    for (int k = 0; k < l; ++k) t += count(k);
+    return t;
+  }
+  __host__ __device__ static constexpr int total() { return start(NL); }
+  __host__ __device__ static constexpr int log2i(int v) { return v <= 1 ? 0 : 1 + log2i(v / 2); }
+  __host__ __device__ static constexpr bool i_outer(int l) { return A::Kp(l) > A::Np(l); }
+  __host__ __device__ static constexpr int inner(int l) { return i_outer(l) ? A::Np(l) / 32 : A::Kp(l) / 32; }
+  __host__ __device__ static constexpr bool pow2_inner() {
+    for (int l = 0; l < NL; ++l)
+      if (inner(l) & (inner(l) - 1)) return false;
+    return true;
+  }
+  static_assert(pow2_inner(), "tile decode assumes power-of-two inner tile counts");
+  __host__ __device__ static TileDesc at(int b) {
+    constexpr int NTL = total(), q = NTL / 8, r = NTL % 8;
+    const int x = b & 7, j = b >> 3;
+    const int s = x * q + (x < r ? x : r) + j;
+#ifdef __HIP_DEVICE_COMPILE__
+    int l = 0;
+#pragma unroll
+    for (int k = 1; k < NL; ++k) l += s >= start(k) ? 1 : 0;
+    const int loc = s - (int)fchain::pick<NL>(l, [](int k) { return (int64_t)start(k); });
+    const int sh = (int)fchain::pick<NL>(l, [](int k) { return (int64_t)log2i(inner(k)); });
+    const bool io = fchain::pick<NL>(l, [](int k) { return (int64_t)i_outer(k); }) != 0;
+    const int a = loc >> sh, c = loc & ((1 << sh) - 1);
+    return TileDesc{l, 32 * (io ? c : a), 32 * (io ? a : c), 0};
+#else
+    int l = 0;
+    while (l + 1 < NL && s >= start(l + 1)) ++l;
+    const int loc = s - start(l), a = loc / inner(l), c = loc % inner(l);
+    return TileDesc{l, 32 * (i_outer(l) ? c : a), 32 * (i_outer(l) ? a : c), 0};
+#endif
+  }
+};
+
+template <class A>
+__host__ __device__ inline LayerDev cls_layer(int l, char* arena, int Bp, int ncls, int E) {
+#ifdef __HIP_DEVICE_COMPILE__
+  auto P = [&](auto f) { return fchain::pick<A::NL>(l, f); };
+#else
+  auto P = [&](auto f) { return f(l); };
+#endif
+  static_assert(A::CLS && !A::F8, "the class-embedding form (bf16)");
+  LayerDev L{};
+  const bool ce = l == A::LCE, fc = l == A::LFC;
+  L.K = ce ? ncls : (int)P([](int k) { return (int64_t)wK<A>(k); }) + ((fc || l == A::LD0) ? E : 0);
+  L.N = ce ? E : (int)P([](int k) { return (int64_t)wN<A>(k); });
+  L.Kp = (int)P([](int k) { return (int64_t)A::Kp(k); });
+  L.Np = (int)P([](int k) { return (int64_t)A::Np(k); });
+  L.relu = (fc || l == A::LDL || ce) ? 0 : 1;
+  L.wt = ce ? 1 : 0;
+  L.has_bias = ce ? 0 : 1;
+  // state_dict order with fc and decoder L0 widened by E; the table is the last tensor
+  const int64_t off = P([](int k) { return wpoff<A>(k); }) + (l > A::LFC ? 2LL * A::Z * E : 0) +
+                      (l > A::LD0 ? (int64_t)H * E : 0);
+  L.nseg = fc ? 2 : 1;
+  L.seg_rows0 = fc ? A::Z : L.N;
+  const int R0 = fc ? A::Z : L.N;
+  L.pw[0] = off;
+  L.pb[0] = ce ? -1 : off + (int64_t)R0 * L.K;
+  L.pw[1] = fc ? L.pb[0] + A::Z : off;
+  L.pb[1] = fc ? L.pw[1] + (int64_t)A::Z * L.K : L.pb[0];
+  const int64_t Bp2 = 2 * (int64_t)Bp;
+  L.Wf = arena + P([](int k) { return A::wf(k); });
+  L.Wb = arena + P([](int k) { return A::wb(k); });
+  L.bias = (float*)(arena + A::bias_base) + P([](int k) { return (int64_t)A::bias_off(k); });
+  L.xT = arena + A::act0 + Bp2 * P([](int k) { return A::xrows(k); });
+  L.gT = arena + A::act0 + Bp2 * P([](int k) { return A::grows(k); });
+  return L;
+}
+
+// grid = total tiles × sk.S + 1 (split-major; the last block finishes the loss)
+template <class A, int MODE>
+__global__ __launch_bounds__(WG_THREADS, 4) void clswgrad_kernel(char* arena, float* params, float* mst, float* vst,
+                                                               int Bp, int Bk, int ncls, int E, AdamArgs a, LossArgs la,
+                                                               SplitK sk) {
+  AdamArgs aa = a;
+  aa.params = params;
+  aa.m = mst;
+  aa.v = vst;
+  constexpr int NTL = CTiles<A>::total();
+  if ((int)blockIdx.x == NTL * sk.S) {
+    if (threadIdx.x < 64 && la.partials) finish_loss(la, A::S, A::D, A::Z);
+    return;
+  }
+  __shared__ __attribute__((aligned(16))) WgradLds<1> sh;
+  sk.s = blockIdx.x / NTL;
+  sk.tile = blockIdx.x - sk.s * NTL;
+  const TileDesc td = CTiles<A>::at(sk.tile);
+  const LayerDev L = cls_layer<A>(td.layer, arena, Bp, ncls, E);
+  wgrad_body<__bf16, MODE, 1>(L, td, Bk, aa, la, false, A::S, A::D, A::Z, sh.red, sh.dbp, sk);
+}
+
 }  // namespace wchain

@@ -220,6 +220,16 @@ class CVAEEngine:
         if batch > self.max_batch:
             raise ValueError(f"batch {batch} > max_batch {self.max_batch}")
 
+    def _dev(self, t, dtype):
+        """``t`` on the device, contiguous, as ``dtype``.  A host tensor goes through pinned memory
+        with a non-blocking copy: the upload then queues on the stream behind the kernels already
+        there instead of waiting for them, so the host can prepare its next call meanwhile (the
+        pinned staging block stays allocated until the copy has run: torch's host allocator)."""
+        t = torch.as_tensor(t)
+        if t.device.type == "cpu":
+            return t.to(dtype).contiguous().pin_memory().to(self.device, non_blocking=True)
+        return t.to(device=self.device, dtype=dtype).contiguous()
+
     def _idx(self, idx, n_rows):
         """int64 row indices on the device.  A host index tensor is range-checked before the upload
         (the kernels gather x[idx[b]] without bounds checks); a device one is trusted."""
@@ -229,13 +239,13 @@ class CVAEEngine:
         if idx.device.type == "cpu" and idx.numel() and (int(idx.min()) < 0 or int(idx.max()) >= n_rows):
             raise IndexError(f"row index out of range [0, {n_rows})")
         if idx.device != self.device or idx.dtype != torch.int64:
-            idx = idx.to(device=self.device, dtype=torch.int64)
+            idx = self._dev(idx, torch.int64)
         return idx.contiguous()
 
     def _eps(self, eps, batch):
         if eps is None:
             return None
-        eps = torch.as_tensor(eps).to(device=self.device, dtype=torch.float32).contiguous()
+        eps = self._dev(eps, torch.float32)
         if eps.shape != (batch, self.shape[2]):
             raise ValueError(f"eps must be ({batch},{self.shape[2]})")
         return eps
@@ -308,7 +318,7 @@ class CVAEEngine:
             raise ValueError(f"idx holds {idx.numel()} rows, {n_steps} steps of {B} need {n_steps * B}")
         e = None
         if eps is not None:
-            e = torch.as_tensor(eps).to(device=self.device, dtype=torch.float32).contiguous()
+            e = self._dev(eps, torch.float32)
             if e.shape != (n_steps * B, self.shape[2]):
                 raise ValueError(f"eps must be ({n_steps * B},{self.shape[2]})")
         cl = self._classes(classes, x.shape[0])
@@ -345,7 +355,7 @@ class CVAEEngine:
         self._check_rows(x, idx[:min(B, n_rows)], min(B, n_rows))
         e = None
         if eps is not None:
-            e = torch.as_tensor(eps).to(device=self.device, dtype=torch.float32).contiguous()
+            e = self._dev(eps, torch.float32)
             if e.shape != (E * n_rows, self.shape[2]):
                 raise ValueError(f"eps must be ({E * n_rows},{self.shape[2]})")
         if loss_accum is None:
@@ -612,6 +622,14 @@ class CVAEEngine:
         k = C.c_int()
         check(lib().cvae_train_kernel(self._h, C.byref(k)))
         return ("generic", "fast", "wide", "ring", "f32")[k.value]
+
+    @property
+    def dw_kernel(self):
+        """'generic' (tile list from memory) or the compile-time tile decode the dW ⊕ Adam launch
+        uses: 'fast', 'wide', 'f32' or 'cls' (cvae_dw_kernel)."""
+        k = C.c_int()
+        check(lib().cvae_dw_kernel(self._h, C.byref(k)))
+        return ("generic", "fast", "wide", "f32", "cls")[k.value]
 
     def workspace_bytes(self):
         b = C.c_int64()

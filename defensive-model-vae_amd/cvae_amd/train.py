@@ -209,20 +209,30 @@ def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidd
     if fused:  # whole epochs per C call: the host draws, uploads once, and reads the losses once
         chunk = 1 if checkpoint_path else max(1, int(epochs_per_call))
         spe = (n + gb - 1) // gb
-        epoch = first
-        while epoch < epochs:
-            k = min(chunk, epochs - epoch)
+        if eps not in ("host", "philox"):
+            raise ValueError("eps must be 'host' or 'philox'")
+
+        def draw(k):
+            """k epochs' host draws, in the reference's order: each epoch's DataLoader permutation
+            (:340), then reparameterize's randn_like per batch (:205)."""
             perms, eps_rows = [], []
             for _ in range(k):
-                perms.append(loader_permutation(n))      # (:340) the epoch's DataLoader order
+                perms.append(loader_permutation(n))
                 if eps == "host":
-                    for lo in range(0, n, gb):            # reparameterize's randn_like (:205), per batch
+                    for lo in range(0, n, gb):
                         eps_rows.append(torch.randn(min(gb, n - lo), Z))
-                elif eps != "philox":
-                    raise ValueError("eps must be 'host' or 'philox'")
-            idx = torch.stack(perms).to(x_dev.device)
-            e = torch.cat(eps_rows).to(x_dev.device) if eps == "host" else None
-            acc = eng.train_epochs(x_dev, idx, gb, n_steps=k * spe, eps=e)
+            return k, torch.stack(perms), torch.cat(eps_rows) if eps == "host" else None
+
+        epoch = first
+        nxt = draw(min(chunk, epochs - epoch)) if epoch < epochs else None
+        while nxt is not None:
+            k, idx, e = nxt
+            acc = eng.train_epochs(x_dev, idx, gb, n_steps=k * spe, eps=e)  # uploads queue behind the kernels
+            # the next chunk's draws while the device runs this one (they come next in the generator's
+            # stream either way; a checkpoint run draws after saving, so its saved RNG state is exact)
+            nxt = None
+            if epoch + k < epochs and not checkpoint_path:
+                nxt = draw(min(chunk, epochs - epoch - k))
             sums = acc.cpu().numpy()                      # the only host sync of the k epochs
             for j in range(k):
                 means = sums[j] / n
@@ -233,6 +243,7 @@ def train(data, seq_len, dim, latent_dim, batch_size=32, lr=1e-3, epochs=1, hidd
             epoch += k
             if checkpoint_path:
                 save_checkpoint(checkpoint_path, model, eng, epoch, loss_history)
+                nxt = draw(min(chunk, epochs - epoch)) if epoch < epochs else None
     for epoch in range(first, epochs if not fused else first):
         for rows in loader:                               # (:340) one global batch
             g = rows.numel()

@@ -153,6 +153,17 @@ enum cvae_train_kernel_kind {
 };
 int cvae_train_kernel(const cvae_handle* h, int* kind);
 
+/* Which dW ⊕ Adam kernel the handle's training step launches (after the row chain,
+ * Training_VAE.py:362-363): CVAE_DW_GENERIC (tile descriptors and layer records read from memory),
+ * or a compile-time tile decode — CVAE_DW_FAST (the reference architecture, bf16, S*D = 600),
+ * CVAE_DW_WIDE (BASELINE cfg5's shape), CVAE_DW_F32 (the reference's own configuration in fp32),
+ * CVAE_DW_CLS (BASELINE cfg4's class embedding at S=100, D=6).  Introspection only;
+ * CVAE_F32_DW=generic / CVAE_CLS_DW=generic at creation keep the generic kernel for A/B. */
+enum cvae_dw_kernel_kind {
+  CVAE_DW_GENERIC = 0, CVAE_DW_FAST = 1, CVAE_DW_WIDE = 2, CVAE_DW_F32 = 3, CVAE_DW_CLS = 4
+};
+int cvae_dw_kernel(const cvae_handle* h, int* kind);
+
 /* Rebuild the device copies of the weights (padded operand-dtype W and Wᵀ,
  * padded fp32 biases) from the flat fp32 master `params`.  Call after the
  * caller writes parameters (init, load_state_dict, an optimizer outside this

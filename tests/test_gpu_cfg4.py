@@ -215,3 +215,42 @@ def test_cfg4_ring_training_split_equals_fused(cvae, monkeypatch):
         last = e1.train_step(xd, classes=cd)
     torch.cuda.synchronize()
     assert torch.isfinite(e1.params).all() and float(last[0]) < float(first[0])
+
+
+@pytest.mark.parametrize("E_", [4, 16, 24])
+def test_cfg4_dw_decode_equals_generic_tile_list(cvae, monkeypatch, E_):
+    """The ring chain's cfg4 form runs its dW ⊕ Adam with the tile and layer record decoded from
+    blockIdx (wchain::clswgrad_kernel, class-dependent widths from two runtime arguments);
+    CVAE_CLS_DW=generic keeps the tile-list kernel.  Same tiles, same order: gradients (split path),
+    then params, moments and losses after fused steps (Philox eps, a ragged batch) bit for bit, for
+    class_dim 4 / 16 / 24 (the padded widths do not move, the real ones and the offsets do)."""
+    torch.manual_seed(5)
+    ref = OracleCVAE(100, 6, 8, n_classes=NC, class_dim=E_)
+    engines = []
+    for mode in (None, "generic"):
+        if mode:
+            monkeypatch.setenv("CVAE_CLS_DW", mode)
+        m = cvae.ConditionalTrajectoryVAE(100, 6, 8, n_classes=NC, class_dim=E_)
+        m.load_state_dict(ref.state_dict())
+        e = m.attach(dtype="bf16", max_batch=512, device="cuda:0", seed=3)
+        monkeypatch.delenv("CVAE_CLS_DW", raising=False)
+        assert e.train_kernel == "ring"
+        engines.append(e)
+    e1, e2 = engines
+    assert e1.dw_kernel == "cls" and e2.dw_kernel == "generic"
+    gen = torch.Generator().manual_seed(E_)
+    data = torch.randn(600, 100, 6, generator=gen)
+    cls_all = torch.randint(0, NC, (600,), generator=gen, dtype=torch.int32).cuda()
+    x1, x2 = e1.as_input(data), e2.as_input(data)
+    idx = torch.randperm(600, generator=gen)[:512].cuda()
+    for e, x in ((e1, x1), (e2, x2)):
+        e.forward_backward(x, idx=idx, classes=cls_all)
+    torch.cuda.synchronize()
+    assert torch.equal(e1.grads, e2.grads)
+    for b in (512, 512, 300):
+        for e, x in ((e1, x1), (e2, x2)):
+            e.train_step(x, idx=idx[:b], classes=cls_all)
+    torch.cuda.synchronize()
+    assert torch.equal(e1.params, e2.params)
+    assert torch.equal(e1.m, e2.m) and torch.equal(e1.v, e2.v)
+    assert torch.equal(e1.loss, e2.loss)

@@ -194,6 +194,7 @@ def test_f32_dw_decode_equals_generic_tile_list(cvae, monkeypatch, B):
         assert e.train_kernel == "f32"
         engines.append(e)
     e1, e2 = engines
+    assert e1.dw_kernel == "f32" and e2.dw_kernel == "generic"
     x = _data(300, seed=B)
     xd1, xd2 = e1.as_input(x), e2.as_input(x)
     idx = torch.randperm(300, generator=torch.Generator().manual_seed(B))[:B].cuda()
