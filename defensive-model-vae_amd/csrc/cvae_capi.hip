@@ -115,9 +115,6 @@ struct cvae_handle {
   int ring_lds = 0;
   bool f32c = false;        // fp32 training at the reference's own shape (seq_len 10, dim 3): f32c::f32chain_kernel<Cfg1>
   int f32c_lds = 0;
-  // the wide chain's eps drawn ahead by the dW launch (wchain::EpsPre; CVAE_EPS_AHEAD=0 disables)
-  float* eps_pre = nullptr;    // [Bp][Z] fp32
-  uint64_t* eps_key = nullptr; // {offset, eps_row0, seed, rows}
   bool cls_dw = false;       // BASELINE cfg4's dW ⊕ Adam with the compile-time decode (wchain::clswgrad_kernel)
   bool f32c_dw = false;      // ... and its dW ⊕ Adam with the compile-time tile decode (f32c::f32wgrad_kernel)
   bool timing = false;
@@ -923,12 +920,6 @@ int plan_wide_as(cvae_handle* h) {
   // the MX dW (measured slower than the bf16 dW at B = 1024, DESIGN §4.5: an option, not the default)
   const char* mw = std::getenv("CVAE_FP8_DW");
   h->wide_mxw = std::is_same<A, wchain::Cfg5F8>::value && h->wide_dw && mw && std::strcmp(mw, "mx") == 0;
-  const char* ea = std::getenv("CVAE_EPS_AHEAD");  // "0": every chain draws its own eps (A/B)
-  if (h->wide_dw && !(ea && ea[0] == '0') && !h->eps_pre) {
-    HIPCK(hipMalloc(&h->eps_pre, sizeof(float) * (size_t)h->net.Bp * A::Z));
-    HIPCK(hipMalloc(&h->eps_key, 4 * sizeof(uint64_t)));
-    HIPCK(hipMemset(h->eps_key, 0, 4 * sizeof(uint64_t)));  // rows 0: no launch matches
-  }
   return CVAE_OK;
 }
 
@@ -978,8 +969,6 @@ RowArgs row_args(cvae_handle* h, const CallX& c) {
   ra.partials = h->d_partials;
   ra.ncls = h->net.n_cls;
   ra.cdim = h->net.cls_dim;
-  ra.eps_pre = h->eps_pre;
-  ra.eps_key = h->eps_key;
   return ra;
 }
 
@@ -1103,7 +1092,7 @@ int splits_of(const cvae_handle* h, int batch) {
 
 template <int MODE>
 int launch_wgrad(cvae_handle* h, int batch, const AdamArgs& aa, const LossArgs& la, hipStream_t s,
-                 int parts = CVAE_PART_DW_DEC | CVAE_PART_DW_REST, const RowArgs* ra = nullptr) {
+                 int parts = CVAE_PART_DW_DEC | CVAE_PART_DW_REST) {
   const int dw = parts & (CVAE_PART_DW_DEC | CVAE_PART_DW_REST);
   SplitK sk{splits_of(h, batch), 0, h->splitk_ws, h->splitk_tickets, 0};
   if (dw != (CVAE_PART_DW_DEC | CVAE_PART_DW_REST)) {
@@ -1128,26 +1117,15 @@ int launch_wgrad(cvae_handle* h, int batch, const AdamArgs& aa, const LossArgs& 
     static_assert(wchain::WTiles<wchain::Cfg5>::total() == wchain::WTiles<wchain::Cfg5F8>::total(), "tile lists");
     if (h->cfg.dtype == CVAE_FP8 && h->wide_mxw && batch % 128 == 0)  // the MX dW: 128-row chunks
       return klaunch(h, wchain::widewgrad_kernel<wchain::Cfg5F8, MODE, true>, dim3(g), dim3(WG_THREADS), 0, s,
-                     h->arena, aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), aa, la, sk, wchain::EpsPre{});
-    // a Philox step with device counters: EpsPre blocks behind the tiles draw the next step's eps
-    // (one block per 16-row chain tile of this batch; the chain behind checks the key)
-    const bool pre = h->eps_pre && ra && !ra->eps && ra->ctr && la.ctr;
-    const wchain::EpsPre ep{h->eps_pre, h->eps_key, ra ? ra->seed : 0, ra ? ra->eps_row0 : 0, bk_of(h, batch)};
-    const int gp = g + (pre ? bk_of(h, batch) / wchain::R : 0);
+                     h->arena, aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), aa, la, sk);
     if (h->cfg.dtype == CVAE_FP8 && h->wide_mx)
-      return pre ? klaunch(h, wchain::widewgrad_kernel<wchain::Cfg5F8, MODE, false, true>, dim3(gp), dim3(WG_THREADS),
-                           0, s, h->arena, aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), aa, la, sk, ep)
-                 : klaunch(h, wchain::widewgrad_kernel<wchain::Cfg5F8, MODE>, dim3(g), dim3(WG_THREADS), 0, s, h->arena,
-                           aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), aa, la, sk, ep);
+      return klaunch(h, wchain::widewgrad_kernel<wchain::Cfg5F8, MODE>, dim3(g), dim3(WG_THREADS), 0, s, h->arena,
+                     aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), aa, la, sk);
     if (h->cfg.dtype == CVAE_FP8)
-      return pre ? klaunch(h, wchain::widewgrad_kernel<wchain::Cfg5F8B, MODE, false, true>, dim3(gp), dim3(WG_THREADS),
-                           0, s, h->arena, aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), aa, la, sk, ep)
-                 : klaunch(h, wchain::widewgrad_kernel<wchain::Cfg5F8B, MODE>, dim3(g), dim3(WG_THREADS), 0, s,
-                           h->arena, aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), aa, la, sk, ep);
-    return pre ? klaunch(h, wchain::widewgrad_kernel<wchain::Cfg5, MODE, false, true>, dim3(gp), dim3(WG_THREADS), 0,
-                         s, h->arena, aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), aa, la, sk, ep)
-               : klaunch(h, wchain::widewgrad_kernel<wchain::Cfg5, MODE>, dim3(g), dim3(WG_THREADS), 0, s, h->arena,
-                         aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), aa, la, sk, ep);
+      return klaunch(h, wchain::widewgrad_kernel<wchain::Cfg5F8B, MODE>, dim3(g), dim3(WG_THREADS), 0, s, h->arena,
+                     aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), aa, la, sk);
+    return klaunch(h, wchain::widewgrad_kernel<wchain::Cfg5, MODE>, dim3(g), dim3(WG_THREADS), 0, s, h->arena,
+                   aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), aa, la, sk);
   }
   if (h->cls_dw)
     return klaunch(h, wchain::clswgrad_kernel<wchain::Cfg4, MODE>, dim3(wchain::CTiles<wchain::Cfg4>::total() * sk.S + 1),
@@ -1214,7 +1192,7 @@ int fwd_bwd_impl(cvae_handle* h, const CallX& c, float* grads, float* loss_out, 
   const int dw = parts & (CVAE_PART_DW_DEC | CVAE_PART_DW_REST);
   if ((rc = tmark(h, s, dw == CVAE_PART_DW_DEC ? "wgrad_dec" : dw == CVAE_PART_DW_REST ? "wgrad_rest" : "wgrad")))
     return rc;
-  return launch_wgrad<PM_GRAD>(h, c.batch, aa, la, s, parts, &ra);
+  return launch_wgrad<PM_GRAD>(h, c.batch, aa, la, s, parts);
 }
 
 int train_step_impl(cvae_handle* h, const CallX& c, float* params, float* m, float* v, int64_t step,
@@ -1228,7 +1206,7 @@ int train_step_impl(cvae_handle* h, const CallX& c, float* params, float* m, flo
   if (rc) return rc;
   const LossArgs la = make_loss(h, ra, loss_out, loss_accum);
   if ((rc = tmark(h, s, "wgrad_adam"))) return rc;
-  return launch_wgrad<PM_ADAM>(h, c.batch, aa, la, s, CVAE_PART_DW_DEC | CVAE_PART_DW_REST, &ra);
+  return launch_wgrad<PM_ADAM>(h, c.batch, aa, la, s);
 }
 
 }  // namespace
@@ -1268,8 +1246,6 @@ int cvae_destroy(cvae_handle* h) {
   for (auto e : h->pool) (void)hipEventDestroy(e);
   if (h->arena) (void)hipFree(h->arena);
   if (h->fault_host) (void)hipHostFree(h->fault_host);
-  if (h->eps_pre) (void)hipFree(h->eps_pre);
-  if (h->eps_key) (void)hipFree(h->eps_key);
   cvae_px_close(h);
   cvae_rccl_close(h);
   delete h;

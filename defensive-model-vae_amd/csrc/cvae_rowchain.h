@@ -195,10 +195,6 @@ struct RowArgs {
   const float* d_hc;      // (batch, H)
   const int* classes;     // cfg4: class id per row of x (gathered by idx like x); NULL = class 0
   int ncls, cdim;         // cfg4: n_classes, class_dim (0 for the reference model)
-  // the wide chain: eps of this step drawn by the previous dW launch (wchain::EpsPre), [rows][Z] fp32,
-  // valid when its key {offset, eps_row0, seed, rows} names this launch's draw (checked on the device)
-  const float* eps_pre;
-  const uint64_t* eps_key;
 };
 
 // Philox offset of this launch's eps draws: the device counter when given (a replayable step)

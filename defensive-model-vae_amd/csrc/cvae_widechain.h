@@ -768,18 +768,6 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   // the Philox offset of this launch: a scalar load before anything else (a vector load here, under
   // the counter-pointer branch, made the compiler drain every in-flight load at the fc step)
   const uint64_t rng_off = a.ctr ? *(const __attribute__((address_space(4))) uint64_t*)a.ctr : a.offset;
-  // eps drawn ahead by the previous dW launch (widewgrad_kernel's EpsPre blocks: the same Philox
-  // values, off the chain's critical path), when its key names this launch's offset, global rows and
-  // seed; otherwise the chain draws (block-uniform)
-  // ahead: the prologue loads this tile's rows of the drawn-ahead buffer unconditionally (no load
-  // address waits on the key); the key, loaded here, is first needed after the prologue barrier,
-  // where a miss draws every tile's eps in the chain
-  const bool ahead = !A::SZ && a.eps_key && a.ctr && !a.eps;
-  bool pre = false;
-  if (ahead) {
-    const auto* k = (const __attribute__((address_space(4))) uint64_t*)a.eps_key;
-    pre = k[0] == rng_off && (int64_t)k[1] == a.eps_row0 && k[2] == a.seed && (uint64_t)(b0 + R) <= k[3];
-  }
 
   Ring<P> ring;
   // a dX GEMM of step S over the bf16 gradient image: e4m3 with MX scales where the layer is f8b
@@ -817,17 +805,9 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   auto eps_j0 = [&](int k) { return A::SZ ? min(4 * (n16 >> 2), Z - 4) : 16 * (wave + NW * k) + 4 * (n16 >> 2); };
   auto eps_load = [&](int k) {
     const int j0 = eps_j0(k);
-    const float* const ebase = a.eps ? a.eps : ahead ? a.eps_pre : (const float*)(AR + A::bias_base);  // global memory either way
-    const int erow = a.eps ? min(b0 + rowq, max(a.batch - 1, 0)) : b0 + rowq;
-    return gld<f32x4>(ebase + (a.eps || ahead ? (size_t)erow * Z + j0 : 0));
-  };
-  const bool ebuf = a.eps || ahead;  // block-uniform: the chain's own draws interleave only without either
-  auto eps_take = [&](int k, f32x4 e) {
-    if (rowq >= nrows) e = f32x4{0.f, 0.f, 0.f, 0.f};
-    ep[k] = quad_t(e);
-  };
-  auto eps_draw = [&](int k) {
-    eps_take(k, philox_normal4(a.seed, rng_off, (uint32_t)(a.eps_row0 + b0 + rowq), (uint32_t)eps_j0(k)));
+    const float* const ebase = a.eps ? a.eps : (const float*)(AR + A::bias_base);  // global memory either way
+    const int erow = a.eps ? min(b0 + rowq, max(a.batch - 1, 0)) : 0;
+    return gld<f32x4>(ebase + (a.eps ? (size_t)erow * Z + j0 : 0));
   };
   auto eps_make = [&](auto kk, f32x4 eh) {
     constexpr int k = decltype(kk)::value;
@@ -853,7 +833,6 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   static_assert(!(A::SZ && A::F8), "EPSX would overlap L_X8 / L_DCAT8");
   float* const EPSX = (float*)(smem + A::L_RCH0);
 
-  f32x4 ehw[A::SZ ? 1 : NZT];  // the wide form's eps from memory (host or drawn ahead), per latent tile
   // ---- prologue: x tile (relative transform, Training_VAE.py:345-348), biases, LDS pads
   // x_f32 (CVAE_X_F32: real data with ~200 m absolute coordinates): fp32 rows, the start point
   // subtracted in fp32 and the relative offsets rounded to bf16 once
@@ -917,11 +896,9 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
       if (x32) x_loads(std::false_type{}, std::true_type{});
       else x_loads(std::false_type{}, std::false_type{});
     }
-    // EPS_PRO: the host-eps load right behind the x tile (the x wait then covers it); the wide form
-    // loads every tile's (host or drawn-ahead) eps here and takes them after the prologue barrier
+    // EPS_PRO: the host-eps load right behind the x tile (the x wait then covers it)
     f32x4 eh0[NPRO > 0 ? NPRO : 1];
-    if constexpr (A::SZ) sfor<0, NPRO>([&](auto kk) { eh0[decltype(kk)::value] = eps_load(decltype(kk)::value); });
-    else sfor<0, NZT>([&](auto kk) { ehw[decltype(kk)::value] = eps_load(decltype(kk)::value); });
+    sfor<0, NPRO>([&](auto kk) { eh0[decltype(kk)::value] = eps_load(decltype(kk)::value); });
     constexpr int NB4 = A::nbias / 4, UB = (NB4 + NT - 1) / NT;
     f32x4 bv[UB];
 #pragma unroll
@@ -955,8 +932,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     sfor<0, NPRO>([&](auto kk) {  // the Philox VALU issues while the x tile is in flight
       constexpr int k = decltype(kk)::value;
       if (CVAE_DIAG_NOPHILOX || !eps_mine) ep[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-      else if constexpr (A::SZ) eps_make(kk, eh0[k]);
-      else if (!ebuf) eps_draw(k);
+      else eps_make(kk, eh0[k]);
     });
     if constexpr (A::SZ)
       if (wave == NW - 1) *(f32x4*)(EPSX + 4 * lane) = ep[0];
@@ -974,9 +950,6 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
         if (a.adam_pre)
           __hip_atomic_store(a.ctr + 2, __builtin_bit_cast(uint64_t, adam_f32x2{s0, s1}), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
-        // the next step's Philox offset (the dW launch behind advances ctr[0] to it): what its EpsPre
-        // blocks draw ahead with, whatever order they and the loss finisher run in
-        if (!A::SZ) __hip_atomic_store(a.ctr + 3, rng_off + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     sub();
@@ -1055,12 +1028,6 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
   bar();
   if constexpr (A::SZ)
     if (wave == 0) ep[0] = *(const f32x4*)(EPSX + 4 * lane);
-  if constexpr (!A::SZ) {
-    if (ebuf && !CVAE_DIAG_NOPHILOX) {
-      if (a.eps || pre) sfor<0, NZT>([&](auto kk) { eps_take(decltype(kk)::value, ehw[decltype(kk)::value]); });
-      else sfor<0, NZT>([&](auto kk) { eps_draw(decltype(kk)::value); });  // the key missed: draw here
-    }
-  }
   if constexpr (A::CLS) {
     // the one-hot class image (xT(LCE)) and e = table[class] into both concatenations at 2H + k and
     // Z + H + k (bf16: what one-hot · Wf(LCE) gives the generic chain; zeros in the K padding)
@@ -1097,9 +1064,7 @@ __device__ __forceinline__ void wide_body(char* const AR, const int Bp, const Ro
     constexpr int c = decltype(cc)::value;
     if constexpr (c % ES == 2 && c / ES >= NPRO && c / ES < NZT) {
       if (CVAE_DIAG_NOPHILOX) ep[c / ES] = f32x4{0.f, 0.f, 0.f, 0.f};  // timing only
-      else if constexpr (!A::SZ) {
-        if (!ebuf) eps_draw(c / ES);  // else taken after the prologue
-      } else if (eps_mine) draw_eps(integral_constant<int, c / ES>{});
+      else if (eps_mine) draw_eps(integral_constant<int, c / ES>{});
       else ep[c / ES] = f32x4{0.f, 0.f, 0.f, 0.f};  // SZ: only wave 0's lanes hold the latents
     }
   };

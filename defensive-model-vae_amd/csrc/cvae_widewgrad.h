@@ -115,49 +115,13 @@ __host__ __device__ inline LayerDev wide_layer(int l, char* arena, int Bp) {
   return L;
 }
 
-// The next training step's eps, drawn by the dW launch of this one (PRE): the wide chain's 4 Philox
-// draws per lane (8192 normals per 16-row tile at latent 512) sit on its critical path wherever they
-// go; here they run in EpsPre blocks behind the tile blocks, in the workgroup slots the
-// 436 tiles leave free (512 at two per CU).  Block p draws rows 16p .. 16p + 15 — Philox(seed;
-// eps_row0 + row, latent/4, offset) with offset = ctr[3] (the chain that ran before published its
-// own + 1: the offset the loss finisher of this launch advances ctr[0] to) — into buf[row][Z], and
-// block 0 writes the key.  The next chain uses them when the key names its offset, rows and seed,
-// so the values are the chain's own draw either way.
-struct EpsPre {
-  float* buf;
-  uint64_t* key;  // {offset, eps_row0, seed, rows}
-  uint64_t seed;
-  int64_t row0;
-  int rows;       // rows drawn: this step's batch rounded up to the arena's 32-row tiles
-};
-
-template <class A>
-__device__ __forceinline__ void eps_pre_block(const EpsPre& ep, const uint64_t* ctr, int p) {
-  const uint64_t off = gld<uint64_t>(ctr + 3);
-  constexpr int QPR = A::Z / 4;  // Philox blocks (4 normals) per row
-#pragma unroll 1
-  for (int t = threadIdx.x; t < 16 * QPR; t += WG_THREADS) {
-    const int r = t / QPR, j0 = 4 * (t - r * QPR), row = 16 * p + r;
-    const f32x4 e = philox_normal4(ep.seed, off, (uint32_t)(ep.row0 + row), (uint32_t)j0);
-    gst<f32x4>(ep.buf + (size_t)row * A::Z + j0, e);
-  }
-  if (p == 0 && threadIdx.x == 0) {
-    ep.key[0] = off;
-    ep.key[1] = (uint64_t)ep.row0;
-    ep.key[2] = ep.seed;
-    ep.key[3] = (uint64_t)ep.rows;
-  }
-}
-
-// grid = total tiles × sk.S + 1 (split-major; the last block finishes the loss) [+ rows/16 EpsPre
-// blocks].  Two workgroups per CU (4 waves per SIMD): the 436 tiles of cfg5 fit the 512 slots in one
-// round.
+// grid = total tiles × sk.S + 1 (split-major; the last block finishes the loss).  Two workgroups per
+// CU (4 waves per SIMD): the 436 tiles of cfg5 fit the 512 slots in one round.
 // MXW: the 32 × 64 tiles' dW GEMMs in e4m3 with MX block scales along the batch (mx_dw_chunk,
 // CVAE_FP8_DW=mx; Bk % 128 == 0); the 32 × 32 tiles (the K=2 condition layer) stay bf16
-template <class A, int MODE, bool MXW = false, bool PRE = false>
+template <class A, int MODE, bool MXW = false>
 __global__ __launch_bounds__(WG_THREADS, 4) void widewgrad_kernel(char* arena, float* params, float* mst, float* vst,
-                                                                int Bp, int Bk, AdamArgs a, LossArgs la, SplitK sk,
-                                                                EpsPre ep) {
+                                                                int Bp, int Bk, AdamArgs a, LossArgs la, SplitK sk) {
   AdamArgs aa = a;
   aa.params = params;
   aa.m = mst;
@@ -166,12 +130,6 @@ __global__ __launch_bounds__(WG_THREADS, 4) void widewgrad_kernel(char* arena, f
   if ((int)blockIdx.x == NTL * sk.S) {  // one extra block finishes the loss beside the tiles
     if (threadIdx.x < 64 && la.partials) finish_loss(la, A::S, A::D, A::Z);
     return;
-  }
-  if constexpr (PRE) {
-    if ((int)blockIdx.x > NTL * sk.S) {  // block-uniform
-      eps_pre_block<A>(ep, la.ctr, (int)blockIdx.x - NTL * sk.S - 1);
-      return;
-    }
   }
   __shared__ __attribute__((aligned(16))) WgradLds<2> sh;
   sk.s = blockIdx.x / NTL;

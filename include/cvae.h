@@ -110,9 +110,7 @@ typedef struct cvae_adam_config {
  *   counters[0] = Philox offset of the next training step's eps draw,
  *   counters[1] = optimizer steps begun,
  *   counters[2] = the Adam scalars of step counters[1] (two fp32: -lr/(1-beta1^t), sqrt(1-beta2^t),
- *                 written by the library),
- *   counters[3] = (BASELINE cfg5's wide chain) the Philox offset of the step after the one begun:
- *                 what the dW launch draws the next step's eps with, ahead (CVAE_EPS_AHEAD).
+ *                 written by the library), counters[3] reserved.
  * A training call given counters reads them ON THE DEVICE and advances them: the row chain that
  * begins a step adds 1 to counters[1] and (given the Adam config) stores that step's scalars, the
  * Adam update uses t = counters[1] and those scalars, and the dW launch adds 1 to counters[0].  The
