@@ -15,8 +15,9 @@ Workloads:
        reference's default), fp32, the reference loop: one host permutation per epoch
        (DataLoader(shuffle=True)), batches 32|6, host eps — what `python Training_VAE.py`
        runs, with the epoch's rows gathered on the device; the timed steps' permutations and eps
-       are drawn on the host inside the timed region, uploaded once, and issued through one
-       cvae_train_epochs call (the fp32 ring chain, cvae_f32chain.h).
+       are drawn on the host inside the timed region and issued through cvae_train_epochs calls of
+       whole epochs (4, then 32 per call), each chunk drawn while the device runs the previous one
+       (the fp32 ring chain, cvae_f32chain.h, and its dW decode, cvae_f32wgrad.h).
   wide (BASELINE configs[4] shape): S=200, Z=512, 8+8 layers, bf16 (or --dtype fp8).
 
 Prints ONE JSON line (rank 0).  `roofline` is the dominant kernel's algorithmic
@@ -442,7 +443,7 @@ def main():
         def run(k):
             """k batches of the reference loop: a fresh permutation each epoch (host, DataLoader
             shuffle) and host eps per batch (randn_like on the CPU, :205).  One GPU: the k steps'
-            epochs drawn on the host, uploaded once and issued through one cvae_train_epochs call
+            epochs drawn on the host and issued through cvae_train_epochs calls of whole epochs
             (what cvae_amd.train does); data-parallel: per step."""
             if not dp.split:
                 # in chunks of whole epochs (the last may be cut short), as cvae_amd.train issues them:
