@@ -5,7 +5,7 @@
 # (SQ instruction mix, HBM traffic, L2 hit/miss).  Every GPU step has its own limit; the script
 # stops at the first failure.  SKIP_TESTS=1 skips the suite; PASSES overrides the PMC pass list.
 set -u
-T=${TAG:-r06e}
+T=${TAG:-r06z}
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$T
 mkdir -p $OUT
 cd $GRAFT_REPO_ROOT
