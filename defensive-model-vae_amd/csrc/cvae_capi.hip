@@ -116,8 +116,7 @@ struct cvae_handle {
   bool f32c = false;        // fp32 training at the reference's own shape (seq_len 10, dim 3): f32c::f32chain_kernel<Cfg1>
   int f32c_lds = 0;
   bool cls_dw = false;       // BASELINE cfg4's dW ⊕ Adam with the compile-time decode (wchain::clswgrad_kernel)
-  bool f32c_dw = false;
-  float* xg = nullptr;       // ... the next step's rows gathered by the dW launch ([Bp][S·D] fp32; CVAE_GATHER_AHEAD=0 off)      // ... and its dW ⊕ Adam with the compile-time tile decode (f32c::f32wgrad_kernel)
+  bool f32c_dw = false;      // ... and its dW ⊕ Adam with the compile-time tile decode (f32c::f32wgrad_kernel)
   bool timing = false;
   // timing: per call, a chain of events on the caller's stream; segment i of a
   // call spans ev[i] → ev[i+1] and is named by the kernel launched after ev[i]
@@ -880,9 +879,6 @@ int plan_f32c(cvae_handle* h) {
   h->f32c_lds = A::L_TOTAL;
   const char* dw = std::getenv("CVAE_F32_DW");  // "generic": the tile-list kernel (A/B)
   h->f32c_dw = !(dw && std::strcmp(dw, "generic") == 0) && f32c_dw_matches<A>(h);
-  const char* ga = std::getenv("CVAE_GATHER_AHEAD");
-  if (h->f32c_dw && !(ga && ga[0] == '0') && !h->xg)
-    HIPCK(hipMalloc(&h->xg, sizeof(float) * (size_t)h->net.Bp * A::I));
   return CVAE_OK;
 }
 
@@ -1094,16 +1090,9 @@ int splits_of(const cvae_handle* h, int batch) {
   return std::max(1, std::min(h->splitk_max, want));
 }
 
-// the rows the next step of a multi-step call will train on (cvae_train_epochs / cvae_train_steps)
-struct NextRows {
-  const void* x;
-  const int64_t* idx;
-  int rows;
-};
-
 template <int MODE>
 int launch_wgrad(cvae_handle* h, int batch, const AdamArgs& aa, const LossArgs& la, hipStream_t s,
-                 int parts = CVAE_PART_DW_DEC | CVAE_PART_DW_REST, const NextRows* nx = nullptr) {
+                 int parts = CVAE_PART_DW_DEC | CVAE_PART_DW_REST) {
   const int dw = parts & (CVAE_PART_DW_DEC | CVAE_PART_DW_REST);
   SplitK sk{splits_of(h, batch), 0, h->splitk_ws, h->splitk_tickets, 0};
   if (dw != (CVAE_PART_DW_DEC | CVAE_PART_DW_REST)) {
@@ -1142,13 +1131,9 @@ int launch_wgrad(cvae_handle* h, int batch, const AdamArgs& aa, const LossArgs& 
     return klaunch(h, wchain::clswgrad_kernel<wchain::Cfg4, MODE>, dim3(wchain::CTiles<wchain::Cfg4>::total() * sk.S + 1),
                    dim3(WG_THREADS), 0, s, h->arena, aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch),
                    h->cfg.n_classes, h->cfg.class_dim, aa, la, sk);
-  if (h->f32c_dw) {
-    const f32c::GatherNext gn = nx ? f32c::GatherNext{(const float*)nx->x, nx->idx, nx->rows, h->xg}
-                                   : f32c::GatherNext{nullptr, nullptr, 0, nullptr};
-    const int ng = nx ? (nx->rows + 63) / 64 : 0;
-    return klaunch(h, f32c::f32wgrad_kernel<f32c::Cfg1, MODE>, dim3(f32c::WTiles<f32c::Cfg1>::total() * sk.S + 1 + ng),
-                   dim3(WG_THREADS), 0, s, h->arena, aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), aa, la, sk, gn);
-  }
+  if (h->f32c_dw)
+    return klaunch(h, f32c::f32wgrad_kernel<f32c::Cfg1, MODE>, dim3(f32c::WTiles<f32c::Cfg1>::total() * sk.S + 1),
+                   dim3(WG_THREADS), 0, s, h->arena, aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), aa, la, sk);
   if (h->fast_nki == 19)
     return klaunch(h, fchain::fastwgrad_kernel<19, MODE>, dim3(fchain::Tiles<19>::total() * sk.S + 1),
                    dim3(WG_THREADS), 0, s, h->arena, aa.params, aa.m, aa.v, h->net.Bp, bk_of(h, batch), h->net.S,
@@ -1211,8 +1196,7 @@ int fwd_bwd_impl(cvae_handle* h, const CallX& c, float* grads, float* loss_out, 
 }
 
 int train_step_impl(cvae_handle* h, const CallX& c, float* params, float* m, float* v, int64_t step,
-                    const cvae_adam_config* adam, float* loss_out, double* loss_accum, hipStream_t s,
-                    const NextRows* nx = nullptr) {
+                    const cvae_adam_config* adam, float* loss_out, double* loss_accum, hipStream_t s) {
   tbegin(h);
   AdamArgs aa = make_adam(params, nullptr, m, v, step, *adam, 1.f, c.ctr);
   CallX ca = c;
@@ -1222,31 +1206,7 @@ int train_step_impl(cvae_handle* h, const CallX& c, float* params, float* m, flo
   if (rc) return rc;
   const LossArgs la = make_loss(h, ra, loss_out, loss_accum);
   if ((rc = tmark(h, s, "wgrad_adam"))) return rc;
-  return launch_wgrad<PM_ADAM>(h, c.batch, aa, la, s, CVAE_PART_DW_DEC | CVAE_PART_DW_REST, nx);
-}
-
-// one step of a multi-step call: the rows this step trains on come from the previous step's gather
-// when it made one (x = the handle's buffer, no indices), and this step gathers the next one's when
-// the handle has the buffer (the fp32 chain's configuration: fp32 rows, its dW decode)
-int train_step_multi(cvae_handle* h, const void* x, const int64_t* idx, const int32_t* classes, int batch, int xflags,
-                     const float* eps, uint64_t seed, uint64_t offset, int64_t eps_row0, const cvae_loss_weights* w,
-                     float* params, float* m, float* v, int64_t step, const cvae_adam_config* adam, float* loss_out,
-                     double* loss_accum, uint64_t* counters, hipStream_t s, const int64_t* next_idx, int next_rows,
-                     bool& gathered) {
-  if (!x || !params || !m || !v) return fail(CVAE_E_INVALID, "null argument");
-  if (!counters && step < 1) return fail(CVAE_E_INVALID, "step must be >= 1");
-  int rc = check_batch(h, batch);
-  if (!rc) rc = check_adam(adam);
-  if (!rc) rc = check_fault(h);
-  if (rc) return rc;
-  const bool from_buf = gathered;
-  const bool want = h->xg && next_idx && next_rows > 0 && !classes && (((uintptr_t)x) & 7) == 0;
-  const NextRows nx{x, next_idx, next_rows};
-  CallX c{from_buf ? (const void*)h->xg : x, from_buf ? nullptr : idx, classes, batch, xflags, eps, seed, offset,
-          eps_row0, w, counters, adam};
-  rc = train_step_impl(h, c, params, m, v, step, adam, loss_out, loss_accum, s, want ? &nx : nullptr);
-  gathered = want && !rc;
-  return rc;
+  return launch_wgrad<PM_ADAM>(h, c.batch, aa, la, s);
 }
 
 }  // namespace
@@ -1286,7 +1246,6 @@ int cvae_destroy(cvae_handle* h) {
   for (auto e : h->pool) (void)hipEventDestroy(e);
   if (h->arena) (void)hipFree(h->arena);
   if (h->fault_host) (void)hipHostFree(h->fault_host);
-  if (h->xg) (void)hipFree(h->xg);
   cvae_px_close(h);
   cvae_rccl_close(h);
   delete h;
@@ -1522,13 +1481,10 @@ int cvae_train_steps(cvae_handle* h, const void* x, const int64_t* idx, const in
   if (!h) return fail(CVAE_E_INVALID, "null handle");
   if (n_steps < 0) return fail(CVAE_E_INVALID, "n_steps must be >= 0");
   const int Z = h->cfg.latent_dim;
-  bool gathered = false;
   for (int i = 0; i < n_steps; ++i) {
-    const int64_t* nidx = idx && i + 1 < n_steps ? idx + (size_t)(i + 1) * batch : nullptr;
-    const int rc = train_step_multi(h, x, idx ? idx + (size_t)i * batch : nullptr, classes, batch, xflags,
-                                    eps ? eps + (size_t)i * batch * Z : nullptr, seed, offset + (uint64_t)i, eps_row0,
-                                    w, params, m, v, step0 + i, adam, loss_out, loss_accum, counters,
-                                    (hipStream_t)stream, nidx, batch, gathered);
+    const int rc = cvae_train_step(h, x, idx ? idx + (size_t)i * batch : nullptr, classes, batch, xflags,
+                                   eps ? eps + (size_t)i * batch * Z : nullptr, seed, offset + (uint64_t)i, eps_row0,
+                                   w, params, m, v, step0 + i, adam, loss_out, loss_accum, counters, stream);
     if (rc) return rc;
   }
   return CVAE_OK;
@@ -1543,18 +1499,13 @@ int cvae_train_epochs(cvae_handle* h, const void* x, const int64_t* idx, const i
   if (!idx || n_rows < 1 || batch < 1 || n_steps < 0) return fail(CVAE_E_INVALID, "idx, n_rows >= 1, batch >= 1, n_steps >= 0");
   const int Z = h->cfg.latent_dim;
   const int spe = (n_rows + batch - 1) / batch;
-  bool gathered = false;
   for (int s = 0; s < n_steps; ++s) {
     const int e = s / spe, k = s % spe;
     const int64_t r0 = (int64_t)e * n_rows + (int64_t)k * batch;  // first visited row of this step
     const int b = std::min(batch, n_rows - k * batch);
-    const int s1 = s + 1, e1 = s1 / spe, k1 = s1 % spe;  // the next step's rows
-    const int64_t* nidx = s1 < n_steps ? idx + (int64_t)e1 * n_rows + (int64_t)k1 * batch : nullptr;
-    const int nb = std::min(batch, n_rows - k1 * batch);
-    const int rc = train_step_multi(h, x, idx + r0, classes, b, xflags, eps ? eps + r0 * Z : nullptr, seed,
-                                    offset + (uint64_t)s, eps_row0, w, params, m, v, step0 + s, adam, loss_out,
-                                    loss_accum ? loss_accum + 5 * (int64_t)e : nullptr, counters, (hipStream_t)stream,
-                                    nidx, nb, gathered);
+    const int rc = cvae_train_step(h, x, idx + r0, classes, b, xflags, eps ? eps + r0 * Z : nullptr, seed,
+                                   offset + (uint64_t)s, eps_row0, w, params, m, v, step0 + s, adam, loss_out,
+                                   loss_accum ? loss_accum + 5 * (int64_t)e : nullptr, counters, stream);
     if (rc) return rc;
   }
   return CVAE_OK;

@@ -93,23 +93,10 @@ __host__ __device__ inline LayerDev f32_layer(int l, char* arena, int Bp) {
   return L;
 }
 
-// The next step's rows, gathered ahead (cvae_train_epochs / cvae_train_steps know them): the row
-// chain's prologue then loads its x tile directly instead of its row indices and then the rows (one
-// dependent memory round trip fewer, with the weight stream queued behind it).  A copy, so the next
-// step is bit for bit what it would be from the gather.
-struct GatherNext {
-  const float* x;      // (N, S, D) fp32 rows
-  const int64_t* idx;  // the next step's row indices
-  int rows;            // its batch
-  float* dst;          // [rows][S·D]; nullptr: no gather
-};
-
 // grid = total tiles × sk.S + 1 (split-major; the last block finishes the loss beside the tiles)
-// [+ ceil(rows / 64) gather blocks]
 template <class A, int MODE>
 __global__ __launch_bounds__(WG_THREADS) void f32wgrad_kernel(char* arena, float* params, float* mst, float* vst,
-                                                              int Bp, int Bk, AdamArgs a, LossArgs la, SplitK sk,
-                                                              GatherNext gn) {
+                                                              int Bp, int Bk, AdamArgs a, LossArgs la, SplitK sk) {
   AdamArgs aa = a;
   aa.params = params;
   aa.m = mst;
@@ -117,15 +104,6 @@ __global__ __launch_bounds__(WG_THREADS) void f32wgrad_kernel(char* arena, float
   constexpr int NTL = WTiles<A>::total();
   if ((int)blockIdx.x == NTL * sk.S) {
     if (threadIdx.x < 64 && la.partials) finish_loss(la, A::S, A::D, Z);
-    return;
-  }
-  if ((int)blockIdx.x > NTL * sk.S) {  // block-uniform: gather block g copies rows 64g .. 64g + 63
-    const int r0 = 64 * ((int)blockIdx.x - NTL * sk.S - 1);
-#pragma unroll 1
-    for (int t = threadIdx.x; t < 64 * A::I; t += WG_THREADS) {
-      const int r = r0 + t / A::I, f = t - (t / A::I) * A::I;
-      if (r < gn.rows) gn.dst[(size_t)r * A::I + f] = gn.x[(size_t)gn.idx[r] * A::I + f];
-    }
     return;
   }
   __shared__ __attribute__((aligned(16))) WgradLds<1> sh;

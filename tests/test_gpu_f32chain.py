@@ -211,42 +211,3 @@ def test_f32_dw_decode_equals_generic_tile_list(cvae, monkeypatch, B):
     assert torch.equal(e1.m, e2.m) and torch.equal(e1.v, e2.v)
     assert torch.equal(e1.loss, e2.loss)
     assert torch.equal(e1.loss_accum, e2.loss_accum)
-
-
-def test_gather_ahead_equals_gather_in_chain(cvae, monkeypatch):
-    """The multi-step calls (cvae_train_epochs, cvae_train_steps) at the reference's shape: each dW
-    launch copies the next step's rows into a buffer the next row chain reads without indices; with
-    CVAE_GATHER_AHEAD=0 every chain gathers its own.  A copy, so the two are bit-equal: shuffled
-    epochs with ragged last batches (38 rows, batches 32 + 6; 300 rows, 128 + 128 + 44) and host or
-    Philox eps, then index-gathered steps."""
-    torch.manual_seed(4)
-    ref = OracleCVAE(10, 3, 8)
-    engines = []
-    for ahead in ("1", "0"):
-        monkeypatch.setenv("CVAE_GATHER_AHEAD", ahead)
-        m = cvae.ConditionalTrajectoryVAE(10, 3, 8)
-        m.load_state_dict(ref.state_dict())
-        e = m.attach(dtype="fp32", max_batch=256, device="cuda:0", seed=5)
-        monkeypatch.delenv("CVAE_GATHER_AHEAD")
-        assert e.train_kernel == "f32" and e.dw_kernel == "f32"
-        engines.append(e)
-    e1, e2 = engines
-    g = torch.Generator().manual_seed(8)
-    for n, B in ((38, 32), (300, 128)):
-        x = _data(n, seed=n)
-        x1, x2 = e1.as_input(x), e2.as_input(x)
-        perms = torch.stack([torch.randperm(n, generator=g) for _ in range(3)])
-        eps = torch.randn(3 * n, 8, generator=g)
-        acc = [e.train_epochs(xx, perms, B, eps=eps) for e, xx in ((e1, x1), (e2, x2))]
-        acc += [e.train_epochs(xx, perms, B) for e, xx in ((e1, x1), (e2, x2))]  # Philox eps
-        torch.cuda.synchronize()
-        assert torch.equal(acc[0], acc[1]) and torch.equal(acc[2], acc[3])
-        assert torch.equal(e1.params, e2.params) and torch.equal(e1.m, e2.m) and torch.equal(e1.v, e2.v)
-    x = _data(300, seed=3)
-    x1, x2 = e1.as_input(x), e2.as_input(x)
-    idx = torch.randint(0, 300, (5 * 64,), generator=g).cuda()
-    for e, xx in ((e1, x1), (e2, x2)):
-        e.train_steps(xx, 5, idx=idx, batch=64)
-    torch.cuda.synchronize()
-    assert torch.equal(e1.params, e2.params) and torch.equal(e1.loss, e2.loss)
-    assert torch.equal(e1.counters, e2.counters)
