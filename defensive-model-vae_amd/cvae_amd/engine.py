@@ -99,6 +99,12 @@ class CVAEEngine:
     # ------------------------------------------------------------------ lifecycle
     def close(self):
         if getattr(self, "_h", None):
+            # the handle's arena and buffers are freed below: let every launch queued on this
+            # engine's device finish first (an engine dropped right after an asynchronous step)
+            try:
+                torch.cuda.synchronize(self.device)
+            except Exception:
+                pass
             lib().cvae_destroy(self._h)
             self._h = None
 
