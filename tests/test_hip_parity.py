@@ -1305,3 +1305,20 @@ def test_dw_buckets_equal_whole_launch(cvae, monkeypatch, B):
         torch.cuda.synchronize()
         assert torch.equal(eng.grads, g_all)
         assert torch.equal(eng.loss, l_all)
+
+
+def test_kernel_dispatch_per_configuration(cvae):
+    """Which row chain and which dW ⊕ Adam kernel each BASELINE configuration's handle runs
+    (cvae_train_kernel / cvae_dw_kernel): the specialised kernels, never the generic interpreter."""
+    cases = [  # (S, D, Z, n_enc, n_dec, dtype, extra, chain, dw)
+        (10, 3, 8, 4, 4, "fp32", {}, "f32", "f32"),                                # cfg1: the reference's own
+        (100, 6, 8, 4, 4, "bf16", {}, "ring", "fast"),                             # cfg2 / cfg3 per rank
+        (100, 6, 8, 4, 4, "bf16", dict(n_classes=4, class_dim=16), "ring", "cls"),  # cfg4
+        (200, 6, 512, 8, 8, "bf16", {}, "wide", "wide"),                           # cfg5 bf16
+        (200, 6, 512, 8, 8, "fp8", {}, "wide", "wide"),                            # cfg5 fp8
+    ]
+    for S, D, Z, ne, nd, dtype, extra, chain, dw in cases:
+        m = cvae.ConditionalTrajectoryVAE(S, D, Z, 128, ne, nd, **extra)
+        e = m.attach(dtype=dtype, max_batch=64, device="cuda:0")
+        assert (e.train_kernel, e.dw_kernel) == (chain, dw), (S, D, Z, dtype, extra, e.train_kernel, e.dw_kernel)
+        e.close()
