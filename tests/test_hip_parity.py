@@ -429,6 +429,25 @@ def test_train_loop_end_to_end_traj20(cvae, golden, tmp_path):
         assert rel_l2(sd[k].numpy(), d["final/" + k]) < 1e-4, k
 
 
+@pytest.mark.parametrize("dtype,S,D,eps", [("fp32", 10, 3, "host"), ("bf16", 100, 6, "philox")])
+def test_train_epoch_chunks_bit_equal(cvae, tmp_path, dtype, S, D, eps):
+    """train()'s fused epoch loop on device: chunks of 1 and 3 epochs per C call (the next chunk's
+    host draws and pinned non-blocking uploads queued behind the running chunk; a cut-short last
+    chunk) give the same loss history and parameters, bit for bit, as all 7 epochs in one call."""
+    from cvae_amd.train import LOSS_KEYS, train
+    x = np.random.default_rng(5).normal(size=(300, S, D)).astype(np.float32)
+    out = []
+    for epc in (64, 3, 1):
+        torch.manual_seed(11)
+        m, hist, _ = train(x, S, D, 8, batch_size=64, epochs=7, weights=W, seed=11, eps=eps, log=None,
+                           dtype=dtype, epochs_per_call=epc, model_save_path=str(tmp_path / f"m{epc}.pth"))
+        out.append((np.array([hist[k] for k in LOSS_KEYS]), torch.load(tmp_path / f"m{epc}.pth", weights_only=True)))
+    for h, sd in out[1:]:
+        np.testing.assert_array_equal(h, out[0][0])
+        for k, v in sd.items():
+            assert torch.equal(v, out[0][1][k]), k
+
+
 def test_train_steps_equals_repeated_train_step(cvae):
     """cvae_train_steps (one C call for n steps) == n train_step calls, bit for bit (bf16 fast
     chain and fp32 generic chain), with per-step rows from idx and Philox eps offsets."""
