@@ -116,6 +116,7 @@ struct cvae_handle {
   bool f32c = false;        // fp32 training at the reference's own shape (seq_len 10, dim 3): f32c::f32chain_kernel<Cfg1>
   int f32c_lds = 0;
   bool cls_dw = false;       // BASELINE cfg4's dW ⊕ Adam with the compile-time decode (wchain::clswgrad_kernel)
+  int f32c_r4_max = 0;       // ... on 4-row workgroups up to this batch (f32c_rows), 16-row above
   bool f32c_dw = false;      // ... and its dW ⊕ Adam with the compile-time tile decode (f32c::f32wgrad_kernel)
   bool timing = false;
   // timing: per call, a chain of events on the caller's stream; segment i of a
@@ -238,7 +239,7 @@ int build_plan(cvae_handle* h) {
   if (!h->R)
     return fail(CVAE_E_INVALID, "configuration needs " + std::to_string(lds_plan(n, 4, h->tsize).total) +
                                     " B of LDS per 4-row tile (> 160 KiB); reduce seq_len*dim or latent_dim");
-  h->max_row_tiles = rup_i(c.max_batch, 32) / h->R;
+  h->max_row_tiles = rup_i(c.max_batch, 32) / 4;  // loss partials of the smallest row tile any chain runs
   if (c.dim < 3) return fail(CVAE_E_INVALID, "dim must be >= 3 (channel 0 = time, 1:3 = x,y)");
   if (c.hidden_dim % 4 || c.latent_dim % 4)
     return fail(CVAE_E_INVALID, "hidden_dim and latent_dim must be multiples of 4 (4-feature epilogue vectors)");
@@ -873,9 +874,17 @@ int plan_f32c(cvae_handle* h) {
     return CVAE_OK;
   // the chain stores to the arena and streams its weights through 32-bit buffer offsets
   if (!f32c_layout_matches<A>(h) || h->arena_bytes >= ((int64_t)1 << 31)) return CVAE_OK;
-  HIPCK(hipFuncSetAttribute((const void*)f32c::f32chain_kernel<A>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  HIPCK(hipFuncSetAttribute((const void*)f32c::f32chain_kernel<A, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            A::L_TOTAL));
+  HIPCK(hipFuncSetAttribute((const void*)f32c::f32chain_kernel<A, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             A::L_TOTAL));
   h->f32c = true;
+  // CVAE_F32_ROWS=16 / =4: one row tiling at every batch (A/B); default: 4-row workgroups up to
+  // CVAE_F32_R4_MAX_BATCH rows (each workgroup streams all weights, so many small ones cost L2 traffic)
+  const char* rows = std::getenv("CVAE_F32_ROWS");
+  const char* r4max = std::getenv("CVAE_F32_R4_MAX_BATCH");
+  h->f32c_r4_max = rows && std::atoi(rows) == 16 ? 0 : rows && std::atoi(rows) == 4 ? (1 << 30)
+                 : r4max ? std::atoi(r4max) : CVAE_F32_R4_MAX;
   h->f32c_lds = A::L_TOTAL;
   const char* dw = std::getenv("CVAE_F32_DW");  // "generic": the tile-list kernel (A/B)
   h->f32c_dw = !(dw && std::strcmp(dw, "generic") == 0) && f32c_dw_matches<A>(h);
@@ -989,6 +998,7 @@ bool ring_cls_ok(const cvae_handle* h, const RowArgs& ra) {
 bool f32c_ok(const cvae_handle* h, const RowArgs& ra) {
   return h->f32c && (((uintptr_t)ra.x) & 7) == 0 && (((uintptr_t)ra.eps) & 15) == 0 && !ra.ext && !ra.x_relative;
 }
+int f32c_rows(const cvae_handle* h, int batch) { return batch <= h->f32c_r4_max ? 4 : 16; }
 bool wide_ok(const cvae_handle* h, const RowArgs& ra) {
   return h->wide && (((uintptr_t)ra.x) & 15) == 0 && (((uintptr_t)ra.eps) & 15) == 0 && !ra.ext &&
          !ra.x_relative;
@@ -998,7 +1008,7 @@ int chain_rows(const cvae_handle* h, const RowArgs& ra) {
   if (fast_ok(h, ra)) return fchain::R;
   if (ring_ok(h, ra) || ring_cls_ok(h, ra)) return wchain::R;
   if (wide_ok(h, ra)) return wchain::R;
-  if (f32c_ok(h, ra)) return f32c::R;
+  if (f32c_ok(h, ra)) return f32c_rows(h, ra.batch);
   return h->R;
 }
 
@@ -1059,9 +1069,9 @@ int launch_train_chain(cvae_handle* h, RowArgs ra, hipStream_t s, bool tap_ok = 
   }
   if (std::is_same<T, float>::value && f32c_ok(h, ra)) {
     ra.stamps = h->d_stamps;
-    const int grid = rup_i(ra.batch, 32) / f32c::R;
-    return klaunch(h, f32c::f32chain_kernel<f32c::Cfg1>, dim3(grid), dim3(f32c::NT), h->f32c_lds, s, h->arena, ra.x,
-                   ra.idx, h->net.Bp, ra.batch, ra.ctr, ra);
+    const int rows = f32c_rows(h, ra.batch), grid = rup_i(ra.batch, 32) / rows;
+    return klaunch(h, rows == 4 ? f32c::f32chain_kernel<f32c::Cfg1, 4> : f32c::f32chain_kernel<f32c::Cfg1, 16>,
+                   dim3(grid), dim3(f32c::NT), h->f32c_lds, s, h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra.ctr, ra);
   }
   return launch_rowchain<T, RC_TRAIN>(h, ra, s);
 }
@@ -1303,6 +1313,15 @@ int cvae_dw_kernel(const cvae_handle* h, int* kind) {
           : h->f32c_dw      ? CVAE_DW_F32
           : h->fast_nki == 19 ? CVAE_DW_FAST
                             : CVAE_DW_GENERIC;
+  return CVAE_OK;
+}
+
+int cvae_chain_rows(const cvae_handle* h, int batch, int* rows) {
+  if (!h || !rows) return fail(CVAE_E_INVALID, "null argument");
+  if (batch < 1 || batch > h->cfg.max_batch) return fail(CVAE_E_INVALID, "batch must be in [1, max_batch]");
+  RowArgs ra{};  // a call with 16-B aligned rows and host-relative-free input
+  ra.batch = batch;
+  *rows = chain_rows(h, ra);
   return CVAE_OK;
 }
 

@@ -159,18 +159,35 @@ __device__ __forceinline__ void ring_load(Ring<P>& ring, const char* AR, int wav
   }
 }
 
-// acc += W·Xᵀ over one 16-wide K chunk (four 16x16x4 fp32 MFMAs; element e of both fragments)
+// acc += W·Xᵀ over one 16-wide K chunk (element e of both fragments).  RR = 16: four 16x16x4 fp32
+// MFMAs.  RR = 4: four v_mfma_f32_4x4x1_16b_f32 — the weight fragment's lane (r, kg) is A row r % 4 of
+// block 4kg + r / 4, so block 4kg + m multiplies features 16t + 4m .. +3 by the X value of k
+// 16c + 4kg + e of rows 0..3 (B lanes (kg, m, j)); the result holds only k-group kg's share of the
+// chunk (kred sums the four groups)
+template <int RR>
 __device__ __forceinline__ f32x4 mm4(f32x4 w, f32x4 x, f32x4 acc) {
-  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w[0], x[0], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w[1], x[1], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w[2], x[2], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w[3], x[3], acc, 0, 0, 0);
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    acc = RR == 4 ? __builtin_amdgcn_mfma_f32_4x4x1f32(w[e], x[e], acc, 0, 0, 0)
+                  : __builtin_amdgcn_mfma_f32_16x16x4f32(w[e], x[e], acc, 0, 0, 0);
   return acc;
 }
-__device__ __forceinline__ f32x4 lds4(const char* img, int c) {
-  return *(const f32x4*)(img + c * 1024 + (threadIdx.x & 63) * 16);
+// RR = 4: the four k-groups' partial sums (lanes 16 and 32 apart), every lane the same total
+// ((P0 + P1) + (P2 + P3) in any lane: fp32 addition commutes)
+__device__ __forceinline__ f32x4 kred(f32x4 v) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] += __shfl_xor(v[i], 16);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] += __shfl_xor(v[i], 32);
+  return v;
 }
-__device__ __forceinline__ void sts4(char* img, int c, f32x4 v) { *(f32x4*)(img + c * 1024 + (threadIdx.x & 63) * 16) = v; }
+// the B operand (X fragment) of chunk c: RR = 16 lane (b, q) reads slot (q, b), its own lane's;
+// RR = 4 lane (kg, m, j) reads slot (kg, j)
+template <int RR>
+__device__ __forceinline__ f32x4 ldsB(const char* img, int c) {
+  const int lane = threadIdx.x & 63;
+  return *(const f32x4*)(img + c * 1024 + (RR == 4 ? (lane & 48) + (lane & 3) : lane) * 16);
+}
 // slot (quad q, row b) of chunk c
 __device__ __forceinline__ f32x4 lds_slot(const char* img, int c, int q, int b) {
   return *(const f32x4*)(img + c * 1024 + (q * 16 + b) * 16);
@@ -186,23 +203,34 @@ __device__ __forceinline__ void sts_slot(char* img, int c, int q, int b, f32x4 v
 struct NoX {
   __device__ f32x4 operator()(int, f32x4 x) const { return x; }
 };
-template <class A, int P, int s, int J0, int J1, class XC, class XR = NoX>
+template <class A, int RR, int P, int s, int J0, int J1, class XC, class XR = NoX>
 __device__ __forceinline__ f32x4 gemm(Ring<P>& ring, const char* img, XC xc, const char* AR, int wave, int lane,
                                       XR xr = XR{}) {
   constexpr int G0 = start(s), N = J1 - J0;
   f32x4 x[N];
   sfor<J0, J1>([&](auto jj) {
     constexpr int j = decltype(jj)::value;
-    x[j - J0] = xr(j, lds4(img, xc(j)));
+    x[j - J0] = xr(j, ldsB<RR>(img, xc(j)));
   });
+  if constexpr (RR == 4) {  // four independent accumulators (element e), k-groups summed at the end
+    f32x4 a[4] = {};
+    sfor<J0, J1>([&](auto jj) {
+      constexpr int j = decltype(jj)::value, g = G0 + j;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[e] = __builtin_amdgcn_mfma_f32_4x4x1f32(ring.r[g % P][e], x[j - J0][e], a[e], 0, 0, 0);
+      asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]));
+      ring_load<A, P, g + P>(ring, AR, wave, lane);
+    });
+    return kred((a[0] + a[1]) + (a[2] + a[3]));
+  }
   f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
   sfor<J0, J1>([&](auto jj) {
     constexpr int j = decltype(jj)::value, g = G0 + j;
     if constexpr ((j - J0) & 1) {
-      a1 = mm4(ring.r[g % P], x[j - J0], a1);
+      a1 = mm4<16>(ring.r[g % P], x[j - J0], a1);
       asm volatile("" : "+v"(a1));  // MFMA(g) before refill(g + P): the slot is not held twice
     } else {
-      a0 = mm4(ring.r[g % P], x[j - J0], a0);
+      a0 = mm4<16>(ring.r[g % P], x[j - J0], a0);
       asm volatile("" : "+v"(a0));
     }
     ring_load<A, P, g + P>(ring, AR, wave, lane);
@@ -210,12 +238,17 @@ __device__ __forceinline__ f32x4 gemm(Ring<P>& ring, const char* img, XC xc, con
   return N > 1 ? a0 + a1 : a0;
 }
 
-template <class A, int P>
+template <class A, int P, int RR>
 __device__ __forceinline__ void f32_body(char* const AR, const int Bp, const RowArgs& a, char* smem, int blk) {
+  static_assert(RR == 16 || RR == 4, "row tiles of 16 or 4");
   constexpr int S = A::S, D = A::D, I = A::I;
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
-  const int b = lane & 15, q = lane >> 4;
-  const int b0 = blk * R, nrows = max(0, min(R, a.batch - b0));
+  // a lane's output slot: row b, features 16t + 4q .. +3 of its wave's n-tile t.  RR = 16: lane
+  // (b, q).  RR = 4: lane (kg, q, b) — after kred the four k-groups hold the same values and only
+  // k-group 0 (`own`) writes them
+  const int b = RR == 4 ? lane & 3 : lane & 15, q = RR == 4 ? (lane >> 2) & 3 : lane >> 4;
+  const bool own = RR == 4 ? lane < 16 : true;
+  const int b0 = blk * RR, nrows = max(0, min(RR, a.batch - b0));
   char* const XIN = smem + A::L_XIN;
   char* const CIN = smem + A::L_CIN;
   char* const CB = smem + A::L_CB;
@@ -254,21 +287,29 @@ __device__ __forceinline__ void f32_body(char* const AR, const int Bp, const Row
   // rows): the quad transpose gives lane b = 4j + m feature F + m of rows 4j .. 4j+3, one 16-B
   // write-through store (a wave instruction covers 16 features x 16 rows: 1 KB contiguous).  Every
   // lane of the wave must run it (DPP); `on` predicates the store only.
+  // (RR = 4: the quad is rows 0..3 of one feature quad; the workgroup's 4 rows are rows
+  // 4(blk % 4) .. +3 of 16-row arena tile blk / 4)
   auto ast = [&](int mat, int Kf, int F, f32x4 v, bool on = true) {
     const f32x4 t = quad_t(v);
-    if (on && !CVAE_DIAG_NOSTORE)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, t), dst.rs,
-                                             mat + ((blk * Kf + F + (b & 3)) * 16 + (b & ~3)) * 4, 0, 16);
+    const int off = RR == 4 ? (((blk >> 2) * Kf + F + b) * 16 + (blk & 3) * 4) * 4
+                            : ((blk * Kf + F + (b & 3)) * 16 + (b & ~3)) * 4;
+    if (on && own && !CVAE_DIAG_NOSTORE)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, t), dst.rs, mat + off, 0, 16);
   };
   // a fragment image's features [0, NF) to an arena matrix (tasks t = 0 .. 4·NF-1: feature t/4, rows
   // 4(t%4) .. +3 — four LDS dwords, one 16-B store)
   auto img_arena = [&](const char* img, int NF, int mat, int Kf, int goff, int t) {
-    if (t < 0 || t >= 4 * NF || CVAE_DIAG_NOSTORE) return;
-    const int f = t >> 2, j = t & 3;
+    constexpr int TPF = RR / 4;  // 4-row tasks per feature
+    if (t < 0 || t >= TPF * NF || CVAE_DIAG_NOSTORE) return;
+    const int f = t / TPF, j = t % TPF;
     const float* p = (const float*)(img + ((f >> 4) * 64 + ((f & 15) >> 2) * 16 + 4 * j) * 16) + (f & 3);
     const f32x4 v = {p[0], p[4], p[8], p[12]};
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), dst.rs,
-                                           mat + ((blk * Kf + goff + f) * 16 + 4 * j) * 4, 0, 16);
+    const int off = RR == 4 ? (((blk >> 2) * Kf + goff + f) * 16 + (blk & 3) * 4) * 4 : ((blk * Kf + goff + f) * 16 + 4 * j) * 4;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), dst.rs, mat + off, 0, 16);
+  };
+  // this lane's output slot (row b, features 16c + 4q .. +3) of image chunk c
+  auto sto = [&](char* img, int c, f32x4 v) {
+    if (own) sts_slot(img, c, q, b, v);
   };
   auto bias4 = [&](int l, int f) { return *(const f32x4*)(BIAS + A::bias_off(l) + f); };
 
@@ -313,7 +354,7 @@ __device__ __forceinline__ void f32_body(char* const AR, const int Bp, const Row
     const int xr = tid >> 4, xp = tid & 15;
     u32x2 xv = {0u, 0u};
     float sx = 0.f, sy = 0.f;
-    if (tid < 16 * R) {  // wave-uniform
+    if (tid < 16 * RR) {  // wave-uniform
       int64_t g = min(b0 + xr, last);
       if (a.idx) g = gld<int64_t>(a.idx + g);
       const float* const row = (const float*)a.x + g * I;
@@ -356,7 +397,7 @@ __device__ __forceinline__ void f32_body(char* const AR, const int Bp, const Row
     if (kb >= 0 && kb + 256 < NB4) ((f32x4*)BIAS)[kb + 256] = bv1;
     // the decoder input's K padding (features 136..143: chunk 8, quads 2, 3) is read by D0
     if (tid >= 256 && tid < 256 + 32) sts_slot(DCAT, 8, 2 + ((tid - 256) >> 4), (tid - 256) & 15, f32x4{0.f, 0.f, 0.f, 0.f});
-    if (tid < 16 * R) {
+    if (tid < 16 * RR) {
       // the relative transform in fp32 (:345-348): channels 1, 2 minus the start point; rows past the
       // batch are zero
       const bool live = xr < nrows;
@@ -385,48 +426,48 @@ __device__ __forceinline__ void f32_body(char* const AR, const int Bp, const Row
 
   // ================================================================ forward
   {  // C0 ‖ E0 (:132-137, :141-151)
-    f32x4 acc = gemm<A, P, sC0, 0, 1>(ring, CIN, cid, AR, wave, lane);
+    f32x4 acc = gemm<A, RR, P, sC0, 0, 1>(ring, CIN, cid, AR, wave, lane);
     f32x4 y = relu(acc, bias4(LC0, n4), integral_constant<int, MC0>{});
-    sts4(CB, wave, y);
+    sto(CB, wave, y);
     ast(XT(LC1), H, n4, y);
-    acc = gemm<A, P, sE0, 0, 2>(ring, XIN, cid, AR, wave, lane);
+    acc = gemm<A, RR, P, sE0, 0, 2>(ring, XIN, cid, AR, wave, lane);
     y = relu(acc, bias4(LE0, n4), integral_constant<int, ME0>{});
-    sts4(A0, wave, y);
+    sto(A0, wave, y);
     ast(XT(LE1), H, n4, y);
     img_arena(XIN, 32, XT(LE0), A::Kp(LE0), 0, tid);        // x_rel → xT(E0)
     img_arena(CIN, 16, XT(LC0), A::Kp(LC0), 0, tid - 128);  // (x, y, 0..) → xT(C0)
   }
   bar();
   {  // C1 ‖ E1: h_c into both concatenations (fc input at H + n, decoder input at Z + n)
-    f32x4 acc = gemm<A, P, sC1, 0, 8>(ring, CB, cid, AR, wave, lane);
+    f32x4 acc = gemm<A, RR, P, sC1, 0, 8>(ring, CB, cid, AR, wave, lane);
     const f32x4 hc = relu(acc, bias4(LC1, n4), integral_constant<int, MC1>{});
-    sts4(HCAT, 8 + wave, hc);
-    sts_slot(DCAT, wave + (q >> 1), (q + 2) & 3, b, hc);  // decoder-input feature Z + n4
+    sto(HCAT, 8 + wave, hc);
+    if (own) sts_slot(DCAT, wave + (q >> 1), (q + 2) & 3, b, hc);  // decoder-input feature Z + n4
     ast(XT(LFC), A::Kp(LFC), H + n4, hc);
     ast(XT(LD0), A::Kp(LD0), Z + n4, hc);
-    acc = gemm<A, P, sE1, 0, 8>(ring, A0, cid, AR, wave, lane);
+    acc = gemm<A, RR, P, sE1, 0, 8>(ring, A0, cid, AR, wave, lane);
     const f32x4 y = relu(acc, bias4(LE1, n4), integral_constant<int, ME1>{});
-    sts4(A1, wave, y);
+    sto(A1, wave, y);
     ast(XT(LE2), H, n4, y);
   }
   bar();
   {  // E2
-    const f32x4 acc = gemm<A, P, sE2, 0, 8>(ring, A1, cid, AR, wave, lane);
+    const f32x4 acc = gemm<A, RR, P, sE2, 0, 8>(ring, A1, cid, AR, wave, lane);
     const f32x4 y = relu(acc, bias4(LE2, n4), integral_constant<int, ME2>{});
-    sts4(A0, wave, y);
+    sto(A0, wave, y);
     ast(XT(LE3), H, n4, y);
   }
   bar();
   {  // E3 → h_traj
-    const f32x4 acc = gemm<A, P, sE3, 0, 8>(ring, A0, cid, AR, wave, lane);
+    const f32x4 acc = gemm<A, RR, P, sE3, 0, 8>(ring, A0, cid, AR, wave, lane);
     const f32x4 y = relu(acc, bias4(LE3, n4), integral_constant<int, ME3>{});
-    sts4(HCAT, wave, y);
+    sto(HCAT, wave, y);
     ast(XT(LFC), A::Kp(LFC), n4, y);
   }
   bar();
   {  // fc_mu ‖ fc_logvar (:195-196): one n-tile, K chunks 2w, 2w+1 per wave → partial tiles
-    const f32x4 acc = gemm<A, P, sFC, 0, 2>(ring, HCAT, [wave](int j) { return 2 * wave + j; }, AR, wave, lane);
-    sts4(PART, wave, acc);
+    const f32x4 acc = gemm<A, RR, P, sFC, 0, 2>(ring, HCAT, [wave](int j) { return 2 * wave + j; }, AR, wave, lane);
+    sto(PART, wave, acc);
   }
   bar();
   // D0 over [z ‖ h_c]: every wave multiplies the h_c chunks 1..8 while wave 0 forms mu, logvar (lanes
@@ -447,50 +488,50 @@ __device__ __forceinline__ void f32_body(char* const AR, const int Bp, const Row
       lv = sl + bias4(LFC, Z + 4 * qq);
 #pragma unroll
       for (int i = 0; i < 4; ++i) zz[i] = mu[i] + ep[i] * expf(0.5f * lv[i]);
-      if (q < 2) {
+      if (q < 2 && own) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           if (b < nrows) s_kl += 1.f + lv[i] - mu[i] * mu[i] - expf(lv[i]);  // KL (:243)
         sts_slot(DCAT, 0, q, b, zz);
       }
     }
-    acc0 = gemm<A, P, sD0, 0, 8>(ring, DCAT, [](int j) { return j + 1; }, AR, wave, lane);
+    acc0 = gemm<A, RR, P, sD0, 0, 8>(ring, DCAT, [](int j) { return j + 1; }, AR, wave, lane);
     if (wave == 0) ast(XT(LD0), A::Kp(LD0), 4 * q, zz, q < 2);  // z → xT(D0) features 0..7
   }
   bar();
   {  // D0 chunk 0: [z ‖ h_c 0..7]
-    const f32x4 acc = acc0 + gemm<A, P, sD0, 8, 9>(ring, DCAT, [](int) { return 0; }, AR, wave, lane);
+    const f32x4 acc = acc0 + gemm<A, RR, P, sD0, 8, 9>(ring, DCAT, [](int) { return 0; }, AR, wave, lane);
     const f32x4 y = relu(acc, bias4(LD0, n4), integral_constant<int, MD0>{});
-    sts4(A0, wave, y);
+    sto(A0, wave, y);
     ast(XT(LD1), H, n4, y);
   }
   bar();
   {  // D1
-    const f32x4 acc = gemm<A, P, sD1, 0, 8>(ring, A0, cid, AR, wave, lane);
+    const f32x4 acc = gemm<A, RR, P, sD1, 0, 8>(ring, A0, cid, AR, wave, lane);
     const f32x4 y = relu(acc, bias4(LD1, n4), integral_constant<int, MD1>{});
-    sts4(A1, wave, y);
+    sto(A1, wave, y);
     ast(XT(LD2), H, n4, y);
   }
   bar();
   {  // D2
-    const f32x4 acc = gemm<A, P, sD2, 0, 8>(ring, A1, cid, AR, wave, lane);
+    const f32x4 acc = gemm<A, RR, P, sD2, 0, 8>(ring, A1, cid, AR, wave, lane);
     const f32x4 y = relu(acc, bias4(LD2, n4), integral_constant<int, MD2>{});
-    sts4(A0, wave, y);
+    sto(A0, wave, y);
     ast(XT(LD3), H, n4, y);
   }
   bar();
   {  // D3: n-tile w / 4, K chunks 2(w % 4), +1 → partial tiles
-    const f32x4 acc = gemm<A, P, sD3, 0, 2>(ring, A0, [wave](int j) { return 2 * (wave & 3) + j; }, AR, wave, lane);
-    sts4(PART, wave, acc);
+    const f32x4 acc = gemm<A, RR, P, sD3, 0, 2>(ring, A0, [wave](int j) { return 2 * (wave & 3) + j; }, AR, wave, lane);
+    sto(PART, wave, acc);
   }
   bar();
-  if (wave < 2) {  // recon n-tile u = wave + conditional_vae_loss (:229-268) + dL/drecon over x_rel in place
+  if (wave < 2 && own) {  // recon n-tile u = wave + conditional_vae_loss (:229-268) + dL/drecon over x_rel in place
     const int u = wave;
     f32x4 r = lds_slot(PART, 4 * u, q, b);
 #pragma unroll
     for (int v = 1; v < 4; ++v) r += lds_slot(PART, 4 * u + v, q, b);
     r += bias4(LD3, 16 * u + 4 * q);
-    const f32x4 xr = lds4(XIN, u);
+    const f32x4 xr = lds_slot(XIN, u, q, b);
     const bool live = b < nrows;
     const float cr = a.w_recon * 2.f;
     f32x4 g;
@@ -514,21 +555,21 @@ __device__ __forceinline__ void f32_body(char* const AR, const int Bp, const Row
           }
         }
         if (dd == 0) {
-          RCH0[(f / D) * R + b] = r[i];
-          GD0[(f / D) * R + b] = g[i];
+          RCH0[(f / D) * RR + b] = r[i];
+          GD0[(f / D) * RR + b] = g[i];
         }
       }
     }
-    sts4(XIN, u, g);
+    sto(XIN, u, g);
   }
   bar();
   // time-monotonicity term relu(r_s − r_{s+1}) (:261-262, ReLU'(0) = 0) into the time channel of
   // dL/drecon: one task per (timestep, row)
-  if (tid < S * R) {
-    const int s = tid / R, bb = tid % R;
-    float gv = GD0[s * R + bb];
+  if (tid < S * RR) {
+    const int s = tid / RR, bb = tid % RR;
+    float gv = GD0[s * RR + bb];
     if (use_time) {
-      const float rs = RCH0[s * R + bb], rn = RCH0[min(s + 1, S - 1) * R + bb], rp = RCH0[max(s - 1, 0) * R + bb];
+      const float rs = RCH0[s * RR + bb], rn = RCH0[min(s + 1, S - 1) * RR + bb], rp = RCH0[max(s - 1, 0) * RR + bb];
       const float u1 = rs - rn, u0 = rp - rs;  // 0 at the sequence ends
       if (bb < nrows && u1 > 0.f) {
         gv += a.w_time * inv_BS1;
@@ -543,31 +584,31 @@ __device__ __forceinline__ void f32_body(char* const AR, const int Bp, const Row
 
   // ================================================================ backward
   {  // D3ᵀ: dL/d h_D2 = GL · W_D3, mask of D2
-    const f32x4 acc = gemm<A, P, sD3b, 0, 2>(ring, XIN, cid, AR, wave, lane);
+    const f32x4 acc = gemm<A, RR, P, sD3b, 0, 2>(ring, XIN, cid, AR, wave, lane);
     const f32x4 g = masked(acc, integral_constant<int, MD2>{});
-    sts4(A1, wave, g);
+    sto(A1, wave, g);
     ast(GT(LD2), H, n4, g);
     img_arena(XIN, 32, GT(LD3), A::Np(LD3), 0, tid - 256);  // dL/drecon → gT(D3)
   }
   bar();
   {  // D2ᵀ
-    const f32x4 acc = gemm<A, P, sD2b, 0, 8>(ring, A1, cid, AR, wave, lane);
+    const f32x4 acc = gemm<A, RR, P, sD2b, 0, 8>(ring, A1, cid, AR, wave, lane);
     const f32x4 g = masked(acc, integral_constant<int, MD1>{});
-    sts4(A0, wave, g);
+    sto(A0, wave, g);
     ast(GT(LD1), H, n4, g);
   }
   bar();
   {  // D1ᵀ
-    const f32x4 acc = gemm<A, P, sD1b, 0, 8>(ring, A0, cid, AR, wave, lane);
+    const f32x4 acc = gemm<A, RR, P, sD1b, 0, 8>(ring, A0, cid, AR, wave, lane);
     const f32x4 g = masked(acc, integral_constant<int, MD0>{});
-    sts4(A1, wave, g);
+    sto(A1, wave, g);
     ast(GT(LD0), H, n4, g);
   }
   bar();
   {  // D0ᵀ: [dz ‖ dh_c (decoder share)]; tile w over all of K, tile 8 (features 128..143) K-split
-    const f32x4 acc = gemm<A, P, sD0b, 0, 8>(ring, A1, cid, AR, wave, lane);
-    const f32x4 p8 = gemm<A, P, sD0b, 8, 9>(ring, A1, [wave](int) { return wave; }, AR, wave, lane);
-    sts4(PART, wave, p8);
+    const f32x4 acc = gemm<A, RR, P, sD0b, 0, 8>(ring, A1, cid, AR, wave, lane);
+    const f32x4 p8 = gemm<A, RR, P, sD0b, 8, 9>(ring, A1, [wave](int) { return wave; }, AR, wave, lane);
+    sto(PART, wave, p8);
     if (wave == 0 && q < 2) {  // dz of latents 4q .. +3 → KL / reparameterisation backward (:199-206, :243)
       f32x4 gm, gl;
 #pragma unroll
@@ -577,25 +618,31 @@ __device__ __forceinline__ void f32_body(char* const AR, const int Bp, const Row
         gm[i] = live ? a.w_kld * mu[i] * inv_BZ + acc[i] : 0.f;
         gl[i] = live ? a.w_kld * 0.5f * (expf(lv[i]) - 1.f) * inv_BZ + acc[i] * ep[i] * 0.5f * sd : 0.f;
       }
-      sts_slot(GFC, 0, q, b, gm);
-      sts_slot(GFC, 0, q + 2, b, gl);
-    } else {  // h_c features n4 - Z .. +3 → the h_c-aligned image
+      if (own) {
+        sts_slot(GFC, 0, q, b, gm);
+        sts_slot(GFC, 0, q + 2, b, gl);
+      }
+    } else if (own) {  // h_c features n4 - Z .. +3 → the h_c-aligned image
       const int hf = n4 - Z;
       sts_slot(DHC2, hf >> 4, (hf & 15) >> 2, b, acc);
     }
   }
   bar();
   {  // fcᵀ: dh = G_fc · W_fc → h_traj gradient (mask E3) and h_c gradient (+ decoder share, mask C1)
-    const f32x4 x = lds4(GFC, 0);
+    const f32x4 x = ldsB<RR>(GFC, 0);
     constexpr int G0 = start(sFCb);
-    f32x4 ah = mm4(ring.r[G0 % P], x, f32x4{0.f, 0.f, 0.f, 0.f});
-    f32x4 ac = mm4(ring.r[(G0 + 1) % P], x, f32x4{0.f, 0.f, 0.f, 0.f});
+    f32x4 ah = mm4<RR>(ring.r[G0 % P], x, f32x4{0.f, 0.f, 0.f, 0.f});
+    f32x4 ac = mm4<RR>(ring.r[(G0 + 1) % P], x, f32x4{0.f, 0.f, 0.f, 0.f});
     asm volatile("" : "+v"(ah), "+v"(ac));
     ring_load<A, P, G0 + P>(ring, AR, wave, lane);
     ring_load<A, P, G0 + 1 + P>(ring, AR, wave, lane);
+    if constexpr (RR == 4) {
+      ah = kred(ah);
+      ac = kred(ac);
+    }
     img_arena(GFC, 16, GT(LFC), A::Np(LFC), 0, tid - 256);  // [dmu ‖ dlogvar] → gT(fc)
     const f32x4 gt = masked(ah, integral_constant<int, ME3>{});
-    sts4(A0, wave, gt);
+    sto(A0, wave, gt);
     ast(GT(LE3), H, n4, gt);
     f32x4 d2;  // the decoder share; h_c 120..127 (wave 7, q >= 2) is tile 8's partial sum
     if (wave == NW - 1 && q >= 2) {
@@ -603,31 +650,31 @@ __device__ __forceinline__ void f32_body(char* const AR, const int Bp, const Row
 #pragma unroll
       for (int v = 1; v < NW; ++v) d2 += lds_slot(PART, v, q - 2, b);
     } else {
-      d2 = lds4(DHC2, wave);
+      d2 = lds_slot(DHC2, wave, q, b);
     }
     const f32x4 gc = masked(ac + d2, integral_constant<int, MC1>{});
-    sts4(CB, wave, gc);
+    sto(CB, wave, gc);
     ast(GT(LC1), H, n4, gc);
   }
   bar();
   {  // E3ᵀ
-    const f32x4 acc = gemm<A, P, sE3b, 0, 8>(ring, A0, cid, AR, wave, lane);
+    const f32x4 acc = gemm<A, RR, P, sE3b, 0, 8>(ring, A0, cid, AR, wave, lane);
     const f32x4 g = masked(acc, integral_constant<int, ME2>{});
-    sts4(A1, wave, g);
+    sto(A1, wave, g);
     ast(GT(LE2), H, n4, g);
   }
   bar();
   {  // E2ᵀ
-    const f32x4 acc = gemm<A, P, sE2b, 0, 8>(ring, A1, cid, AR, wave, lane);
+    const f32x4 acc = gemm<A, RR, P, sE2b, 0, 8>(ring, A1, cid, AR, wave, lane);
     const f32x4 g = masked(acc, integral_constant<int, ME1>{});
-    sts4(A0, wave, g);
+    sto(A0, wave, g);
     ast(GT(LE1), H, n4, g);
   }
   bar();
   {  // E1ᵀ ‖ C1ᵀ: the last two gradients, gT(E0) and gT(C0), only feed the dW kernel
-    f32x4 acc = gemm<A, P, sE1b, 0, 8>(ring, A0, cid, AR, wave, lane);
+    f32x4 acc = gemm<A, RR, P, sE1b, 0, 8>(ring, A0, cid, AR, wave, lane);
     ast(GT(LE0), H, n4, masked(acc, integral_constant<int, ME0>{}));
-    acc = gemm<A, P, sC1b, 0, 8>(ring, CB, cid, AR, wave, lane);
+    acc = gemm<A, RR, P, sC1b, 0, 8>(ring, CB, cid, AR, wave, lane);
     ast(GT(LC0), H, n4, masked(acc, integral_constant<int, MC0>{}));
   }
   // ---- loss partial sums (deterministic order)
@@ -660,8 +707,13 @@ using Cfg1 = Arch<10, 3>;
 #ifndef CVAE_F32_RING
 #define CVAE_F32_RING 16
 #endif
+// the largest batch the 4-row form serves by default (CVAE_F32_R4_MAX_BATCH overrides at run time)
+#ifndef CVAE_F32_R4_MAX
+#define CVAE_F32_R4_MAX 0
+#endif
 
-template <class A>
+// RR rows per workgroup (16, or 4: the 4x4x1_16b form for small batches, cvae_capi.hip f32c_rows)
+template <class A, int RR>
 __global__ __launch_bounds__(NT) void f32chain_kernel(char* arena, const void* x, const int64_t* idx, int Bp,
                                                       int batch, uint64_t* ctr, RowArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -670,7 +722,7 @@ __global__ __launch_bounds__(NT) void f32chain_kernel(char* arena, const void* x
   ra.idx = idx;
   ra.batch = batch;
   ra.ctr = ctr;
-  f32_body<A, CVAE_F32_RING>(arena, Bp, ra, smem, blockIdx.x);
+  f32_body<A, CVAE_F32_RING, RR>(arena, Bp, ra, smem, blockIdx.x);
 }
 
 }  // namespace f32c

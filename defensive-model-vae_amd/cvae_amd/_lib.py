@@ -51,6 +51,7 @@ _SIGS = {
     "cvae_bucket_split": (_i, [_v, c_i64p]),
     "cvae_train_kernel": (_i, [_v, C.POINTER(_i)]),
     "cvae_dw_kernel": (_i, [_v, C.POINTER(_i)]),
+    "cvae_chain_rows": (_i, [_v, _i, C.POINTER(_i)]),
     "cvae_pack_weights": (_i, [_v, _v, _v]),
     # h, x, idx, classes, batch, xflags, start, eps, seed, offset, eps_row0, recon, mu, logvar, hc, eps_out, stream
     "cvae_forward": (_i, [_v, _v, _v, _v, _i, _i, _v, _v, _u64, _u64, _i64, _v, _v, _v, _v, _v, _v]),

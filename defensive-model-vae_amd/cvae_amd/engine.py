@@ -637,6 +637,13 @@ class CVAEEngine:
         check(lib().cvae_dw_kernel(self._h, C.byref(k)))
         return ("generic", "fast", "wide", "f32", "cls")[k.value]
 
+    def chain_rows(self, batch):
+        """Rows per workgroup of the training row chain a call of ``batch`` rows launches
+        (cvae_chain_rows: 4 or 16 for the fp32 chain, 16 for the bf16 ones)."""
+        r = C.c_int()
+        check(lib().cvae_chain_rows(self._h, int(batch), C.byref(r)), "cvae_chain_rows")
+        return r.value
+
     def workspace_bytes(self):
         b = C.c_int64()
         check(lib().cvae_workspace_bytes(self._h, C.byref(b)))

@@ -28,7 +28,8 @@
  * tap consumed by cvae_train_fwd_bwd only, the fp32 chain's kernel id
  * (CVAE_KERNEL_F32), arena introspection (cvae_read_activation), whole shuffled
  * epochs in one call (cvae_train_epochs) and Adam over a flat range
- * (cvae_adam_flat, the sharded-Adam data-parallel step).
+ * (cvae_adam_flat, the sharded-Adam data-parallel step), which dW kernel and how
+ * many rows per row-chain workgroup a handle runs (cvae_dw_kernel, cvae_chain_rows).
  */
 #ifndef CVAE_H
 #define CVAE_H
@@ -163,6 +164,13 @@ enum cvae_dw_kernel_kind {
   CVAE_DW_GENERIC = 0, CVAE_DW_FAST = 1, CVAE_DW_WIDE = 2, CVAE_DW_F32 = 3, CVAE_DW_CLS = 4
 };
 int cvae_dw_kernel(const cvae_handle* h, int* kind);
+
+/* Rows per workgroup of the training row chain a call of `batch` rows (1 <= batch <= max_batch, 16-B
+ * aligned inputs) launches: 16 for the bf16 chains and the generic fp32 one (or what fits its LDS);
+ * the fp32 chain of the reference's configuration runs 4-row workgroups up to
+ * CVAE_F32_R4_MAX_BATCH rows (default 64) and 16-row ones above (CVAE_F32_ROWS=4 / 16 at creation:
+ * one tiling at every batch).  Introspection only. */
+int cvae_chain_rows(const cvae_handle* h, int batch, int* rows);
 
 /* Rebuild the device copies of the weights (padded operand-dtype W and Wᵀ,
  * padded fp32 biases) from the flat fp32 master `params`.  Call after the

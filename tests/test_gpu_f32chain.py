@@ -6,6 +6,9 @@ Tolerances: both kernels are exact fp32 MFMA chains that sum K in different orde
 other losses rtol 1e-5 and gradients rel-L2 <= 1e-5; against the oracle (torch CPU fp32) the file-wide
 fp32 tolerances of tests/test_hip_parity.py (losses 5e-5, gradients rel-L2 2e-4).  Repeated launches
 are bit-identical (the K-split partials are reduced in a fixed order).
+
+Every test runs on both row tilings of the chain (the `rows` fixture: CVAE_F32_ROWS=4, the
+v_mfma_f32_4x4x1_16b_f32 form with K split over lane groups, and =16, the 16x16x4 form).
 """
 import numpy as np
 import pytest
@@ -31,7 +34,14 @@ def cvae():
     return cvae_amd
 
 
-def _pair(cvae, monkeypatch, max_batch=256, seed=0):
+@pytest.fixture(params=[4, 16], ids=["rows4", "rows16"])
+def rows(request, monkeypatch):
+    """The chain's row tiling for every engine the test creates (CVAE_F32_ROWS at creation)."""
+    monkeypatch.setenv("CVAE_F32_ROWS", str(request.param))
+    return request.param
+
+
+def _pair(cvae, monkeypatch, max_batch=256, seed=0, rows=None):
     """(f32-chain engine, generic-interpreter engine) bound to modules with the same init."""
     torch.manual_seed(seed)
     ref = OracleCVAE(10, 3, 8)
@@ -44,6 +54,8 @@ def _pair(cvae, monkeypatch, max_batch=256, seed=0):
     e2 = m2.attach(dtype="fp32", max_batch=max_batch, device="cuda:0", seed=7)
     monkeypatch.delenv("CVAE_GENERIC")
     assert e1.train_kernel == "f32" and e2.train_kernel == "generic"
+    if rows is not None:
+        assert e1.chain_rows(1) == rows and e1.chain_rows(max_batch) == rows
     return ref, (m1, e1), (m2, e2)
 
 
@@ -60,21 +72,21 @@ LAYERS = ["C0", "C1", "E0", "E1", "E2", "E3", "fc", "D0", "D1", "D2", "D3"]
 
 
 @pytest.mark.parametrize("B", [38, 6])
-def test_f32_chain_arena_matches_generic(cvae, monkeypatch, B):
+def test_f32_chain_arena_matches_generic(cvae, monkeypatch, rows, B):
     """Every arena matrix the two chains write — each layer's input xT and pre-activation gradient
     gT, the dW kernel's operands — agrees (rows past the batch: gT zero in both)."""
-    ref, (m1, e1), (m2, e2) = _pair(cvae, monkeypatch)
+    ref, (m1, e1), (m2, e2) = _pair(cvae, monkeypatch, rows=rows)
     x = _data().cuda()
     idx = torch.arange(B).cuda() * 3
     eps = torch.randn(B, 8, generator=torch.Generator().manual_seed(5))
     e1.forward_backward(x, idx=idx, eps=eps)
     e2.forward_backward(x, idx=idx, eps=eps)
-    rows = (B + 31) // 32 * 32
+    padded = (B + 31) // 32 * 32
     bad = []
     for l, name in enumerate(LAYERS):
         for which in ("x", "g"):
-            a1 = e1.activation(l, which, rows).cpu().numpy()
-            a2 = e2.activation(l, which, rows).cpu().numpy()
+            a1 = e1.activation(l, which, padded).cpu().numpy()
+            a2 = e2.activation(l, which, padded).cpu().numpy()
             r = rel_l2(a1[:B], a2[:B])
             print(f"{name} {which}T rel-L2 {r:.2e}")
             if not r < 1e-5:
@@ -85,8 +97,8 @@ def test_f32_chain_arena_matches_generic(cvae, monkeypatch, B):
 
 
 @pytest.mark.parametrize("B", [1, 6, 17, 32, 38, 64, 256])
-def test_f32_chain_matches_generic(cvae, monkeypatch, B):
-    ref, (m1, e1), (m2, e2) = _pair(cvae, monkeypatch)
+def test_f32_chain_matches_generic(cvae, monkeypatch, rows, B):
+    ref, (m1, e1), (m2, e2) = _pair(cvae, monkeypatch, rows=rows)
     x = _data().cuda()
     idx = torch.randperm(x.shape[0], generator=torch.Generator().manual_seed(B))[:B].cuda()
     eps = torch.randn(B, 8, generator=torch.Generator().manual_seed(100 + B))
@@ -98,10 +110,10 @@ def test_f32_chain_matches_generic(cvae, monkeypatch, B):
         assert rel_l2(g1[o:o + n], g2[o:o + n]) < 1e-5, (k, rel_l2(g1[o:o + n], g2[o:o + n]))
 
 
-def test_f32_chain_philox_matches_generic(cvae, monkeypatch):
+def test_f32_chain_philox_matches_generic(cvae, monkeypatch, rows):
     """In-kernel eps: the same Philox draws (seed, offset, global row) as the generic chain, also with
     a data-parallel row offset."""
-    ref, (m1, e1), (m2, e2) = _pair(cvae, monkeypatch)
+    ref, (m1, e1), (m2, e2) = _pair(cvae, monkeypatch, rows=rows)
     x = _data(64).cuda()
     for row0 in (0, 96):
         l1 = e1.forward_backward(x, batch=38, row0=row0).cpu().numpy()
@@ -111,8 +123,8 @@ def test_f32_chain_philox_matches_generic(cvae, monkeypatch):
 
 
 @pytest.mark.parametrize("B", [6, 38, 200])
-def test_f32_chain_vs_oracle(cvae, monkeypatch, B):
-    ref, (m1, e1), _ = _pair(cvae, monkeypatch)
+def test_f32_chain_vs_oracle(cvae, monkeypatch, rows, B):
+    ref, (m1, e1), _ = _pair(cvae, monkeypatch, rows=rows)
     x = _data(B, seed=B)
     eps = torch.randn(B, 8, generator=torch.Generator().manual_seed(B))
     loss = e1.forward_backward(x, eps=eps).cpu().numpy()
@@ -126,10 +138,10 @@ def test_f32_chain_vs_oracle(cvae, monkeypatch, B):
         assert rel_l2(g[k], p.grad.numpy()) < 2e-4, (k, rel_l2(g[k], p.grad.numpy()))
 
 
-def test_f32_chain_training_steps_match_generic(cvae, monkeypatch):
+def test_f32_chain_training_steps_match_generic(cvae, monkeypatch, rows):
     """30 fused steps (dW ⊕ Adam behind each chain) over shuffled ragged batches stay within fp32
     reordering noise of the generic interpreter's run; the device step counters agree."""
-    ref, (m1, e1), (m2, e2) = _pair(cvae, monkeypatch)
+    ref, (m1, e1), (m2, e2) = _pair(cvae, monkeypatch, rows=rows)
     x = _data(38).cuda()
     g = torch.Generator().manual_seed(3)
     for _ in range(15):
@@ -144,10 +156,10 @@ def test_f32_chain_training_steps_match_generic(cvae, monkeypatch):
     np.testing.assert_allclose(e1.loss_accum.cpu().numpy(), e2.loss_accum.cpu().numpy(), rtol=1e-5)
 
 
-def test_f32_chain_repeatable(cvae, monkeypatch):
+def test_f32_chain_repeatable(cvae, monkeypatch, rows):
     """Repeated launches on one input give the same bits (deterministic K-split reductions, no
     data race in the ring or the images)."""
-    _, (m1, e1), _ = _pair(cvae, monkeypatch)
+    _, (m1, e1), _ = _pair(cvae, monkeypatch, rows=rows)
     x = _data(64).cuda()
     eps = torch.randn(38, 8, generator=torch.Generator().manual_seed(9))
     l0 = e1.forward_backward(x, batch=38, eps=eps).clone()
@@ -157,13 +169,13 @@ def test_f32_chain_repeatable(cvae, monkeypatch):
         assert torch.equal(l, l0) and torch.equal(e1.grads, g0)
 
 
-def test_f32_chain_split_equals_fused(cvae, monkeypatch):
+def test_f32_chain_split_equals_fused(cvae, monkeypatch, rows):
     """fwd_bwd → Adam (the data-parallel route) equals the fused step bit for bit on the new chain."""
-    _, (m1, e1), _ = _pair(cvae, monkeypatch)
+    _, (m1, e1), _ = _pair(cvae, monkeypatch, rows=rows)
     m3 = cvae.ConditionalTrajectoryVAE(10, 3, 8)
     m3.load_state_dict(m1.state_dict())
     e3 = m3.attach(dtype="fp32", max_batch=256, device="cuda:0", seed=7)
-    assert e3.train_kernel == "f32"
+    assert e3.train_kernel == "f32" and e3.chain_rows(38) == rows
     x = _data(38).cuda()
     eps = torch.randn(38, 8, generator=torch.Generator().manual_seed(2))
     for _ in range(3):
@@ -176,7 +188,7 @@ def test_f32_chain_split_equals_fused(cvae, monkeypatch):
 
 
 @pytest.mark.parametrize("B", [32, 38, 6, 256])
-def test_f32_dw_decode_equals_generic_tile_list(cvae, monkeypatch, B):
+def test_f32_dw_decode_equals_generic_tile_list(cvae, monkeypatch, rows, B):
     """The fp32 chain's dW ⊕ Adam launch decodes its tile and layer record from blockIdx
     (cvae_f32wgrad.h); CVAE_F32_DW=generic keeps the tile-list kernel.  Each tile is one
     independent wgrad_body, so the two equal each other bit for bit: gradients (split path), then
@@ -191,7 +203,7 @@ def test_f32_dw_decode_equals_generic_tile_list(cvae, monkeypatch, B):
         m.load_state_dict(ref.state_dict())
         e = m.attach(dtype="fp32", max_batch=256, device="cuda:0", seed=11)
         monkeypatch.delenv("CVAE_F32_DW", raising=False)
-        assert e.train_kernel == "f32"
+        assert e.train_kernel == "f32" and e.chain_rows(B) == rows
         engines.append(e)
     e1, e2 = engines
     assert e1.dw_kernel == "f32" and e2.dw_kernel == "generic"
