@@ -709,7 +709,7 @@ using Cfg1 = Arch<10, 3>;
 #endif
 // the largest batch the 4-row form serves by default (CVAE_F32_R4_MAX_BATCH overrides at run time)
 #ifndef CVAE_F32_R4_MAX
-#define CVAE_F32_R4_MAX 0
+#define CVAE_F32_R4_MAX 1024
 #endif
 
 // RR rows per workgroup (16, or 4: the 4x4x1_16b form for small batches, cvae_capi.hip f32c_rows)

@@ -168,7 +168,7 @@ int cvae_dw_kernel(const cvae_handle* h, int* kind);
 /* Rows per workgroup of the training row chain a call of `batch` rows (1 <= batch <= max_batch, 16-B
  * aligned inputs) launches: 16 for the bf16 chains and the generic fp32 one (or what fits its LDS);
  * the fp32 chain of the reference's configuration runs 4-row workgroups up to
- * CVAE_F32_R4_MAX_BATCH rows (default 64) and 16-row ones above (CVAE_F32_ROWS=4 / 16 at creation:
+ * CVAE_F32_R4_MAX_BATCH rows (default 1024) and 16-row ones above (CVAE_F32_ROWS=4 / 16 at creation:
  * one tiling at every batch).  Introspection only. */
 int cvae_chain_rows(const cvae_handle* h, int batch, int* rows);
 
