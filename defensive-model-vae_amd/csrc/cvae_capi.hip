@@ -116,7 +116,8 @@ struct cvae_handle {
   bool f32c = false;        // fp32 training at the reference's own shape (seq_len 10, dim 3): f32c::f32chain_kernel<Cfg1>
   int f32c_lds = 0;
   bool cls_dw = false;       // BASELINE cfg4's dW ⊕ Adam with the compile-time decode (wchain::clswgrad_kernel)
-  int f32c_r4_max = 0;       // ... on 4-row workgroups up to this batch (f32c_rows), 16-row above
+  int f32c_r4_max = 0;
+  int f32c_spread = 8;       // XCDs the fp32 chain's row tiles occupy (CVAE_F32_SPREAD, A/B)       // ... on 4-row workgroups up to this batch (f32c_rows), 16-row above
   bool f32c_dw = false;      // ... and its dW ⊕ Adam with the compile-time tile decode (f32c::f32wgrad_kernel)
   bool timing = false;
   // timing: per call, a chain of events on the caller's stream; segment i of a
@@ -885,6 +886,8 @@ int plan_f32c(cvae_handle* h) {
   const char* r4max = std::getenv("CVAE_F32_R4_MAX_BATCH");
   h->f32c_r4_max = rows && std::atoi(rows) == 16 ? 0 : rows && std::atoi(rows) == 4 ? (1 << 30)
                  : r4max ? std::atoi(r4max) : CVAE_F32_R4_MAX;
+  const char* spread = std::getenv("CVAE_F32_SPREAD");
+  h->f32c_spread = spread && (std::atoi(spread) == 1 || std::atoi(spread) == 2 || std::atoi(spread) == 4) ? std::atoi(spread) : 8;
   h->f32c_lds = A::L_TOTAL;
   const char* dw = std::getenv("CVAE_F32_DW");  // "generic": the tile-list kernel (A/B)
   h->f32c_dw = !(dw && std::strcmp(dw, "generic") == 0) && f32c_dw_matches<A>(h);
@@ -1069,9 +1072,13 @@ int launch_train_chain(cvae_handle* h, RowArgs ra, hipStream_t s, bool tap_ok = 
   }
   if (std::is_same<T, float>::value && f32c_ok(h, ra)) {
     ra.stamps = h->d_stamps;
-    const int rows = f32c_rows(h, ra.batch), grid = rup_i(ra.batch, 32) / rows;
+    const int rows = f32c_rows(h, ra.batch), tiles = rup_i(ra.batch, 32) / rows;
+    // CVAE_F32_SPREAD=1|2|4: the tiles on that many XCDs (A/B; 8 = every XCD, the plain grid)
+    const int spread = h->f32c_spread < 8 && tiles % h->f32c_spread == 0 && tiles / h->f32c_spread <= 32 ? h->f32c_spread : 8;
+    const int grid = spread < 8 ? tiles / spread * 8 : tiles;
     return klaunch(h, rows == 4 ? f32c::f32chain_kernel<f32c::Cfg1, 4> : f32c::f32chain_kernel<f32c::Cfg1, 16>,
-                   dim3(grid), dim3(f32c::NT), h->f32c_lds, s, h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra.ctr, ra);
+                   dim3(grid), dim3(f32c::NT), h->f32c_lds, s, h->arena, ra.x, ra.idx, h->net.Bp, ra.batch, ra.ctr, ra,
+                   spread);
   }
   return launch_rowchain<T, RC_TRAIN>(h, ra, s);
 }

@@ -173,12 +173,33 @@ __device__ __forceinline__ f32x4 mm4(f32x4 w, f32x4 x, f32x4 acc) {
   return acc;
 }
 // RR = 4: the four k-groups' partial sums (lanes 16 and 32 apart), every lane the same total
-// ((P0 + P1) + (P2 + P3) in any lane: fp32 addition commutes)
+// ((P0 + P1) + (P2 + P3) in any lane: fp32 addition commutes).  gfx950's row swaps (VALU, no LDS
+// round trip): v_permlane16_swap of v with itself leaves one copy holding rows (0, 0, 2, 2) and the
+// other (1, 1, 3, 3), so their sum is the pair sum of rows 16 apart in every lane; v_permlane32_swap
+// does the same for the halves.  CVAE_F32_KRED_SWAP=0: the ds_bpermute butterfly (bit-equal).
+#ifndef CVAE_F32_KRED_SWAP
+#define CVAE_F32_KRED_SWAP 1
+#endif
 __device__ __forceinline__ f32x4 kred(f32x4 v) {
+#if CVAE_F32_KRED_SWAP
+  auto u = [](float f) { return __builtin_bit_cast(unsigned, f); };
+  auto f = [](unsigned x) { return __builtin_bit_cast(float, x); };
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const auto r = __builtin_amdgcn_permlane16_swap(u(v[i]), u(v[i]), false, false);
+    v[i] = f(r[0]) + f(r[1]);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const auto r = __builtin_amdgcn_permlane32_swap(u(v[i]), u(v[i]), false, false);
+    v[i] = f(r[0]) + f(r[1]);
+  }
+#else
 #pragma unroll
   for (int i = 0; i < 4; ++i) v[i] += __shfl_xor(v[i], 16);
 #pragma unroll
   for (int i = 0; i < 4; ++i) v[i] += __shfl_xor(v[i], 32);
+#endif
   return v;
 }
 // the B operand (X fragment) of chunk c: RR = 16 lane (b, q) reads slot (q, b), its own lane's;
@@ -713,16 +734,24 @@ using Cfg1 = Arch<10, 3>;
 #endif
 
 // RR rows per workgroup (16, or 4: the 4x4x1_16b form for small batches, cvae_capi.hip f32c_rows)
+// spread < 8: the row tiles on XCDs 0 .. spread-1 only (the grid is 8/spread times the tiles; block b
+// runs on XCD b % 8, the others exit at once), so fewer L2s fetch the weight stream
 template <class A, int RR>
 __global__ __launch_bounds__(NT) void f32chain_kernel(char* arena, const void* x, const int64_t* idx, int Bp,
-                                                      int batch, uint64_t* ctr, RowArgs a) {
+                                                      int batch, uint64_t* ctr, RowArgs a, int spread) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  int blk = blockIdx.x;
+  if (spread < 8) {
+    const int xcd = blockIdx.x & 7;
+    if (xcd >= spread) return;
+    blk = (blockIdx.x >> 3) * spread + xcd;
+  }
   RowArgs ra = a;
   ra.x = x;
   ra.idx = idx;
   ra.batch = batch;
   ra.ctr = ctr;
-  f32_body<A, CVAE_F32_RING, RR>(arena, Bp, ra, smem, blockIdx.x);
+  f32_body<A, CVAE_F32_RING, RR>(arena, Bp, ra, smem, blk);
 }
 
 }  // namespace f32c
