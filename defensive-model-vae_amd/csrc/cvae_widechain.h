@@ -263,15 +263,17 @@ struct Ring {
 //  * the start point of a row is one 8-B load (elements 0..3), not 16 B (-0.08 us);
 //  * small latent (SZ): only wave 0 (whose lanes hold mu, logvar) draws eps, in the prologue while
 //    the x tile is in flight (C0 ‖ E0 2.44 -> 1.80 us, profiles/r03g/eps_ab.txt);
-//  * wide latent: kEpsProWide of each wave's eps draws move from the E0 GEMM to the prologue — 2 of
-//    4 in the e4m3 form (its E0 streams half the bytes and is VALU-bound: step 54.8 -> 54.2 us), none
+//  * wide latent: kEpsProWide of each wave's eps draws move from the E0 GEMM to the prologue — 1 of
+//    4 in the e4m3 form (its E0 streams half the bytes; round 3 measured 2 against 0: step 54.8 ->
+//    54.2 us; round 6 on the current chain 1 against 0 / 2 / 3 / 4: 46.72-46.74 us against
+//    46.83-46.96 / 46.92-47.33 / 46.96-47.13 / 47.13-47.15, profiles/r06w/ab_epspro_*.json), none
 //    in bf16 (its E0 is stream-bound; the prologue only grows: +0.3-0.9 us;
 //    profiles/r03i/epswide_ab_*.txt);
 //  * an L2 warm-up of E0's fragments in the prologue measured +0.7-1.0 us (profiles/r03g/warm_ab.txt)
 //    and is not built.
 constexpr int kPreFill = 4;
 #ifndef CVAE_DIAG_EPS_PRO_F8
-#define CVAE_DIAG_EPS_PRO_F8 2  // diagnostic builds only: the e4m3 form's prologue draws (A/B)
+#define CVAE_DIAG_EPS_PRO_F8 1  // diagnostic builds only: the e4m3 form's prologue draws (A/B)
 #endif
 template <class A>
 constexpr int kEpsProWide = A::F8 ? CVAE_DIAG_EPS_PRO_F8 : 0;
