@@ -1,9 +1,9 @@
 #!/bin/bash
-# round 6, 4-row fp32 chain default: the -m gpu suite + smoke, the driver's command, cfg1 bench lines, its kernel trace and
-# PMC / traffic passes (TAG=r06w)
+# the -m gpu suite + smoke, the driver's command, cfg1 bench lines, its kernel trace and
+# PMC / traffic passes (TAG=...)
 set -u
 cd $GRAFT_REPO_ROOT
-T=${TAG:-r06w}
+T=${TAG:-cfg1}
 O=gpurun_out/$T; mkdir -p $O
 TAG=$T bash scripts/gpu_suite.sh || exit 1
 timeout -k 10 180 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_s20.json 2> $O/bench_s20.err || exit 1

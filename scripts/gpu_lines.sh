@@ -1,8 +1,8 @@
 #!/bin/bash
-# round 6 final tree: -m gpu suite + smoke, the driver's command, cfg1 / cfg4 / cfg5 (bf16, fp8) lines (TAG)
+# final-tree lines: -m gpu suite + smoke, the driver's command, cfg1 / cfg4 / cfg5 (bf16, fp8) lines (TAG)
 set -u
 cd $GRAFT_REPO_ROOT
-T=${TAG:-r06zg}
+T=${TAG:-lines}
 O=gpurun_out/$T; mkdir -p $O
 TAG=$T bash scripts/gpu_suite.sh || exit 1
 timeout -k 10 180 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_s20.json 2> $O/bench_s20.err || exit 1
