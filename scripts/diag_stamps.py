@@ -29,7 +29,7 @@ x = eng.as_input(torch.randn(B, 10, 3) * 5 if F32 else torch.randn(B, 200, 6) if
 L = lib()
 L.cvae_diag_set_stamps.argtypes = [C.c_void_p, C.c_void_p]
 L.cvae_diag_set_wstamps.argtypes = [C.c_void_p]
-R = 16
+R = eng.chain_rows(B)  # rows per chain workgroup (the fp32 chain: 4 up to 1,024 rows)
 nb = ((B + 31) // 32 * 32) // R
 dbuf = torch.zeros(nb * 64, dtype=torch.int64, device="cuda")
 NT = 4096
