@@ -26,8 +26,12 @@
 //  * arena stores: a quad transpose (4 DPP) turns a lane's 4 features of one row into 4 rows of one
 //    feature, one 16-B write-through store per lane (a wave stores 1 KB contiguous).
 // MFMA work per workgroup: 500 v_mfma_f32_16x16x4_f32 per wave (fp32 MFMA is 1/16 of the bf16 rate),
-// ≈13 us at 2 waves per SIMD: the chain is MFMA-issue bound by design, the weight stream (1 MB per
+// ≈13 us at 2 waves per SIMD: the 16-row form is MFMA-issue bound, the weight stream (1 MB per
 // workgroup) fits under it.
+// The 4-row form (RR = 4, the default up to 1,024 rows: cvae_capi.hip f32c_rows) runs the same
+// stream, images and arena with v_mfma_f32_4x4x1_16b_f32 (8 instead of 32 cycles; 4 rows, K split
+// over the four 16-lane groups, summed by kred).  It leaves the per-CU weight stream as the bound
+// (DESIGN §4.8 "Round 6, last").
 #pragma once
 #include <type_traits>
 #include "cvae_widechain.h"
