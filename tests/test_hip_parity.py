@@ -1328,16 +1328,19 @@ def test_dw_buckets_equal_whole_launch(cvae, monkeypatch, B):
 
 def test_kernel_dispatch_per_configuration(cvae):
     """Which row chain and which dW ⊕ Adam kernel each BASELINE configuration's handle runs
-    (cvae_train_kernel / cvae_dw_kernel): the specialised kernels, never the generic interpreter."""
-    cases = [  # (S, D, Z, n_enc, n_dec, dtype, extra, chain, dw)
-        (10, 3, 8, 4, 4, "fp32", {}, "f32", "f32"),                                # cfg1: the reference's own
-        (100, 6, 8, 4, 4, "bf16", {}, "ring", "fast"),                             # cfg2 / cfg3 per rank
-        (100, 6, 8, 4, 4, "bf16", dict(n_classes=4, class_dim=16), "ring", "cls"),  # cfg4
-        (200, 6, 512, 8, 8, "bf16", {}, "wide", "wide"),                           # cfg5 bf16
-        (200, 6, 512, 8, 8, "fp8", {}, "wide", "wide"),                            # cfg5 fp8
+    (cvae_train_kernel / cvae_dw_kernel): the specialised kernels, never the generic interpreter;
+    and the chain's rows per workgroup (cvae_chain_rows): 4 for the fp32 chain up to 1,024 rows, 16
+    above and for the bf16 chains."""
+    cases = [  # (S, D, Z, n_enc, n_dec, dtype, extra, chain, dw, rows at B = 32 / 2048)
+        (10, 3, 8, 4, 4, "fp32", {}, "f32", "f32", (4, 16)),                                # cfg1: the reference's own
+        (100, 6, 8, 4, 4, "bf16", {}, "ring", "fast", (16, 16)),                             # cfg2 / cfg3 per rank
+        (100, 6, 8, 4, 4, "bf16", dict(n_classes=4, class_dim=16), "ring", "cls", (16, 16)),  # cfg4
+        (200, 6, 512, 8, 8, "bf16", {}, "wide", "wide", (16, 16)),                           # cfg5 bf16
+        (200, 6, 512, 8, 8, "fp8", {}, "wide", "wide", (16, 16)),                            # cfg5 fp8
     ]
-    for S, D, Z, ne, nd, dtype, extra, chain, dw in cases:
+    for S, D, Z, ne, nd, dtype, extra, chain, dw, rows in cases:
         m = cvae.ConditionalTrajectoryVAE(S, D, Z, 128, ne, nd, **extra)
-        e = m.attach(dtype=dtype, max_batch=64, device="cuda:0")
+        e = m.attach(dtype=dtype, max_batch=2048, device="cuda:0")
         assert (e.train_kernel, e.dw_kernel) == (chain, dw), (S, D, Z, dtype, extra, e.train_kernel, e.dw_kernel)
+        assert (e.chain_rows(32), e.chain_rows(2048)) == rows, (S, D, Z, dtype, e.chain_rows(32), e.chain_rows(2048))
         e.close()
