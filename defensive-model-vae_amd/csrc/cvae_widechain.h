@@ -271,7 +271,10 @@ struct Ring {
 //    profiles/r03i/epswide_ab_*.txt);
 //  * an L2 warm-up of E0's fragments in the prologue measured +0.7-1.0 us (profiles/r03g/warm_ab.txt)
 //    and is not built.
-constexpr int kPreFill = 4;
+#ifndef CVAE_WIDE_PREFILL
+#define CVAE_WIDE_PREFILL 4  // diagnostic builds: A/B of the ring items issued before the x-tile wait
+#endif
+constexpr int kPreFill = CVAE_WIDE_PREFILL;
 #ifndef CVAE_DIAG_EPS_PRO_F8
 #define CVAE_DIAG_EPS_PRO_F8 1  // diagnostic builds only: the e4m3 form's prologue draws (A/B)
 #endif
